@@ -1,0 +1,152 @@
+/* madpose_mi355x.h -- C ABI of the MI355X-native hybrid-RANSAC relative-pose engine.
+ *
+ * Drop-in boundary for kocurvik/madpose's Python estimator API.  Each entry point
+ * replaces one binding of the reference's pybind11 module (src/bindings.cpp) and
+ * keeps its argument meaning; the reference signatures are cited per function.
+ * Plain pointers and sizes only.  All buffers are owned by the caller; inputs are
+ * copied to device memory inside the call.  Calls are re-entrant per device.
+ *
+ * Return codes: MP_OK, MP_EINVAL (bad sizes/options), MP_EDEVICE (HIP error; text
+ * via mp_last_error()).  There is no CPU fallback: without a usable MI355X device
+ * every compute entry point returns MP_EDEVICE.
+ */
+#ifndef MADPOSE_MI355X_H
+#define MADPOSE_MI355X_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MP_OK 0
+#define MP_EINVAL 1
+#define MP_EDEVICE 2
+
+/* estimator variants */
+#define MP_CALIBRATED 0   /* HybridEstimatePoseScaleOffset          */
+#define MP_SHARED_FOCAL 1 /* HybridEstimatePoseScaleOffsetSharedFocal */
+#define MP_TWO_FOCAL 2    /* HybridEstimatePoseScaleOffsetTwoFocal    */
+
+/* ExtendedHybridLORansacOptions (src/hybrid_ransac.h:17-25, src/bindings.cpp:78-95) */
+typedef struct mp_ransac_options {
+    double success_probability;
+    double squared_inlier_thresholds[2]; /* [reprojection^2, epipolar^2] (user units) */
+    double data_type_weights[2];         /* [reprojection, epipolar]                  */
+    double threshold_multiplier;
+    uint32_t min_num_iterations;
+    uint32_t max_num_iterations;
+    uint32_t max_num_iterations_per_solver;
+    uint32_t random_seed;
+    int32_t num_lo_steps;
+    int32_t num_lsq_iterations;
+    int32_t min_sample_multiplicator;
+    int32_t non_min_sample_multiplier;
+    int32_t lo_starting_iterations;
+    int32_t final_least_squares;
+    int32_t use_ours;
+    int32_t use_4p4d;
+} mp_ransac_options;
+
+/* EstimatorConfig (src/estimator_config.h:7-33, src/bindings.cpp:99-109) */
+typedef struct mp_estimator_config {
+    double ceres_function_tolerance;
+    double ceres_gradient_tolerance;
+    double ceres_parameter_tolerance;
+    double ceres_max_num_iterations;
+    int32_t solver_type; /* 0 HYBRID, 1 EPI_ONLY, 2 MD_ONLY */
+    int32_t score_type;
+    int32_t lo_type;
+    int32_t min_depth_constraint;
+    int32_t use_shift;
+    int32_t ceres_use_nonmonotonic_steps;
+    int32_t ceres_num_threads;
+    int32_t reserved;
+} mp_estimator_config;
+
+/* PoseScaleOffset{,SharedFocal,TwoFocal} (src/pose.h:7-56); R row-major, x1 = R x0 + t */
+typedef struct mp_model {
+    double R[9];
+    double t[3];
+    double scale, offset0, offset1;
+    double focal0, focal1; /* SF: focal0 == focal1 == focal */
+} mp_model;
+
+/* HybridRansacStatistics (src/bindings.cpp:67-76) + engine counters */
+typedef struct mp_stats {
+    double best_model_score;
+    double inlier_ratios[3];
+    uint64_t num_hypotheses;       /* models scored by minimal-sample iterations */
+    uint64_t num_lo_sweeps;        /* full 3N sweeps issued by LO / termination   */
+    uint32_t num_iterations_total;
+    uint32_t num_iterations_per_solver[2];
+    int32_t best_num_inliers;
+    int32_t best_solver_type;
+    int32_t number_lo_iterations;
+    int32_t num_inliers[3]; /* lengths of the three inlier lists */
+    int32_t num_batches;     /* speculative GPU batches issued */
+    double seconds_total, seconds_lo, seconds_gpu_wait;
+} mp_stats;
+
+/* Full estimator.  Replaces
+ *   HybridEstimatePoseScaleOffset            (src/hybrid_pose_estimator.cpp:8-35, bindings.cpp:169-170)
+ *   HybridEstimatePoseScaleOffsetSharedFocal (src/hybrid_pose_shared_focal_estimator.cpp:8-51, :171-172)
+ *   HybridEstimatePoseScaleOffsetTwoFocal    (src/hybrid_pose_two_focal_estimator.cpp:34-75, :173-174)
+ * x0, x1: n x 2 row-major pixels; d0, d1: n depth priors; min_depth[2];
+ * cam0/cam1: K (9, row-major) for MP_CALIBRATED, principal point (2) otherwise.
+ * inlier_idx: optional caller buffer of 3*n int32; list t starts at t*n and has
+ * stats->num_inliers[t] entries (reproj0, reproj1, sampson). */
+int mp_estimate(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
+                const double *min_depth, const double *cam0, const double *cam1, const mp_ransac_options *options,
+                const mp_estimator_config *config, mp_model *out_model, mp_stats *out_stats, int32_t *inlier_idx,
+                int device);
+
+/* Many independent pairs in one call (pairs concatenated; offsets[p]..offsets[p+1]).
+ * min_depth: 2 per pair; cams: 9 or 2 doubles per pair; inlier buffers per pair at
+ * 3*offsets[p].  Pairs run concurrently on one device. */
+int mp_estimate_batch(int variant, int32_t num_pairs, const int64_t *offsets, const double *x0, const double *x1,
+                      const double *d0, const double *d1, const double *min_depth, const double *cam0,
+                      const double *cam1, const mp_ransac_options *options, const mp_estimator_config *config,
+                      mp_model *out_models, mp_stats *out_stats, int32_t *inlier_idx, int device, int num_streams);
+
+/* solve_scale_and_shift{,_shared_focal,_two_focal} (src/solver.cpp:35-480, bindings.cpp:157-161).
+ * x_homo, y_homo: K homogeneous points stored point-major (3*K doubles: x,y,w per point),
+ * K = 3 (cal) or 4 (sf/tf).  out: max_out rows of width 4/5/6; returns count (>=0) or -code. */
+int mp_solve_scale_and_shift(int variant, const double *x_homo, const double *y_homo, const double *depth_x,
+                             const double *depth_y, double *out, int max_out, int device);
+
+/* solve_scale_shift_pose{,_shared_focal,_two_focal} (src/solver.cpp:482-534, 682-739, 986-1043,
+ * wrappers 1408-1433, bindings.cpp:162-166).  Returns count or -code. */
+int mp_solve_scale_shift_pose(int variant, const double *x_homo, const double *y_homo, const double *depth_x,
+                              const double *depth_y, mp_model *out, int max_out, int device);
+
+/* Batched device sweep over one pair's correspondences (ScoreModel / GetInliers,
+ * src/hybrid_ransac.h:265-349) for num_models models given in problem units.
+ * Used by tests to check the scoring kernel directly.  scores: num_models;
+ * errors (optional): num_models x 3 x n squared errors (is_for_inlier = true). */
+int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
+                    const double *cam0, const double *cam1, const mp_ransac_options *options,
+                    const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
+                    double *errors, int device);
+
+/* Point minimal solver (PoseLib relpose_5pt, src/hybrid_pose_estimator.cpp:134) on unit bearings
+ * (5 points, point-major 3 doubles each).  Returns count or -code. */
+int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device);
+
+/* Test hooks for the host-side random streams (no device needed).
+ * mp_debug_random_stream: kind 0 raw mt19937 words, 1 uniform_int(a, b),
+ * 2 uniform_real(0, b), 3 uniform_int(i % 300, 300 + i % 17) for i = 0..count-1.
+ * mp_debug_iteration_stream: the solver-type / minimal-sample sequence the engine
+ * replays (SelectMinimalSolver + HybridUniformSampling, src/hybrid_ransac.h:64,
+ * 98-109); idx holds 8 slots per iteration (unused slots -1). */
+int mp_debug_random_stream(int kind, uint32_t seed, int32_t a, int32_t b, int32_t count, double *out);
+int mp_debug_iteration_stream(int variant, int32_t n, uint32_t seed, int32_t solver_type, int32_t iterations,
+                              int32_t *types, int32_t *idx);
+
+const char *mp_last_error(void);
+int mp_device_count(void);
+const char *mp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,38 @@
+"""madpose_amd -- MI355X-native hybrid-RANSAC relative pose with monocular depth priors.
+
+Drop-in for the Python API of kocurvik/madpose (`import madpose` resolves to this
+package through the thin `madpose/` alias).  Minimal samples are solved and every
+hypothesis is scored on the GPU (HIP kernels for gfx950); local optimisation runs on
+the host.  See DESIGN.md.
+"""
+from .api import (  # noqa: F401
+    EstimatorConfig,
+    HybridEstimatePoseAndScale,
+    HybridEstimatePoseScaleOffset,
+    HybridEstimatePoseScaleOffsetSharedFocal,
+    HybridEstimatePoseScaleOffsetTwoFocal,
+    HybridLORansacOptions,
+    HybridRansacStatistics,
+    LORansacOptions,
+    PoseAndScale,
+    PoseScaleOffset,
+    PoseScaleOffsetSharedFocal,
+    PoseScaleOffsetTwoFocal,
+    RansacOptions,
+    RansacStats,
+    device_count,
+    estimate_batch,
+    relpose_5pt,
+    score_models,
+    set_device,
+    solve_scale_and_shift,
+    solve_scale_and_shift_shared_focal,
+    solve_scale_and_shift_two_focal,
+    solve_scale_shift_pose,
+    solve_scale_shift_pose_shared_focal,
+    solve_scale_shift_pose_two_focal,
+    version,
+)
+from . import utils  # noqa: F401
+
+__all__ = [n for n in dir() if not n.startswith("_")]

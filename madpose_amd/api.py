@@ -1,0 +1,503 @@
+"""Python surface of the reference's pybind11 module (src/bindings.cpp), backed by the
+MI355X engine through the C ABI.  Names, defaults, argument meaning and return types
+follow src/bindings.cpp:34-175 so user code written for `import madpose` runs unchanged.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib as L
+
+
+# ---------------------------------------------------------------------------
+# option / config containers (src/bindings.cpp:78-109, src/hybrid_ransac.h:17-25,
+# src/estimator_config.h:7-33; RansacLib defaults as restated in DESIGN.md)
+class HybridLORansacOptions:
+    def __init__(self):
+        self.min_num_iterations = 100
+        self.max_num_iterations = 10000
+        self.max_num_iterations_per_solver = 10000
+        self.success_probability = 0.99
+        self.squared_inlier_thresholds = []
+        self.data_type_weights = []
+        self.random_seed = 0
+        self.num_lo_steps = 10
+        self.threshold_multiplier = math.sqrt(2.0)
+        self.num_lsq_iterations = 4
+        self.min_sample_multiplicator = 7
+        self.non_min_sample_multiplier = 3
+        self.lo_starting_iterations = 50
+        self.final_least_squares = False
+        self.use_ours = False
+        self.use_4p4d = False
+
+    def _to_c(self):
+        o = L.mp_ransac_options()
+        thr = list(self.squared_inlier_thresholds)
+        w = list(self.data_type_weights)
+        if len(thr) < 2:
+            raise ValueError("squared_inlier_thresholds must hold [reprojection^2, epipolar^2]")
+        if len(w) < 2:
+            raise ValueError("data_type_weights must hold [reprojection, epipolar]")
+        o.success_probability = float(self.success_probability)
+        o.squared_inlier_thresholds[0] = float(thr[0])
+        o.squared_inlier_thresholds[1] = float(thr[1])
+        o.data_type_weights[0] = float(w[0])
+        o.data_type_weights[1] = float(w[1])
+        o.threshold_multiplier = float(self.threshold_multiplier)
+        o.min_num_iterations = int(self.min_num_iterations)
+        o.max_num_iterations = int(self.max_num_iterations)
+        o.max_num_iterations_per_solver = int(self.max_num_iterations_per_solver)
+        o.random_seed = int(self.random_seed)
+        o.num_lo_steps = int(self.num_lo_steps)
+        o.num_lsq_iterations = int(self.num_lsq_iterations)
+        o.min_sample_multiplicator = int(self.min_sample_multiplicator)
+        o.non_min_sample_multiplier = int(self.non_min_sample_multiplier)
+        o.lo_starting_iterations = int(self.lo_starting_iterations)
+        o.final_least_squares = int(bool(self.final_least_squares))
+        o.use_ours = int(bool(self.use_ours))
+        o.use_4p4d = int(bool(self.use_4p4d))
+        return o
+
+
+class EstimatorConfig:
+    HYBRID, EPI_ONLY, MD_ONLY = 0, 1, 2
+
+    def __init__(self, solver=0, score=0, LO=0):
+        self.solver_type = int(solver)
+        self.score_type = int(score)
+        self.LO_type = int(LO)
+        self.min_depth_constraint = True
+        self.use_shift = True
+        self.ceres_function_tolerance = 1e-6
+        self.ceres_gradient_tolerance = 1e-8
+        self.ceres_parameter_tolerance = 1e-6
+        self.ceres_max_num_iterations = 25.0
+        self.ceres_use_nonmonotonic_steps = True
+        self.ceres_num_threads = 1
+
+    def _to_c(self):
+        c = L.mp_estimator_config()
+        c.ceres_function_tolerance = float(self.ceres_function_tolerance)
+        c.ceres_gradient_tolerance = float(self.ceres_gradient_tolerance)
+        c.ceres_parameter_tolerance = float(self.ceres_parameter_tolerance)
+        c.ceres_max_num_iterations = float(self.ceres_max_num_iterations)
+        c.solver_type = int(self.solver_type)
+        c.score_type = int(self.score_type)
+        c.lo_type = int(self.LO_type)
+        c.min_depth_constraint = int(bool(self.min_depth_constraint))
+        c.use_shift = int(bool(self.use_shift))
+        c.ceres_use_nonmonotonic_steps = int(bool(self.ceres_use_nonmonotonic_steps))
+        c.ceres_num_threads = int(self.ceres_num_threads)
+        return c
+
+
+class RansacOptions:
+    def __init__(self):
+        self.min_num_iterations_ = 100
+        self.max_num_iterations_ = 10000
+        self.success_probability_ = 0.99
+        self.squared_inlier_threshold_ = 1.0
+        self.random_seed_ = 0
+
+
+class LORansacOptions:
+    def __init__(self):
+        self.min_num_iterations = 100
+        self.max_num_iterations = 10000
+        self.success_probability = 0.99
+        self.squared_inlier_threshold = 1.0
+        self.random_seed = 0
+        self.num_lo_steps = 10
+        self.threshold_multiplier = math.sqrt(2.0)
+        self.num_lsq_iterations = 4
+        self.min_sample_multiplicator = 7
+        self.non_min_sample_multiplier = 3
+        self.lo_starting_iterations = 50
+        self.final_least_squares = False
+
+
+class RansacStats:
+    def __init__(self):
+        self.num_iterations = 0
+        self.best_num_inliers = 0
+        self.best_model_score = float("inf")
+        self.inlier_ratio = 0.0
+        self.inlier_indices = []
+        self.number_lo_iterations = 0
+
+
+class HybridRansacStatistics:
+    def __init__(self):
+        self.num_iterations_total = 0
+        self.num_iterations_per_solver = [0, 0]
+        self.best_num_inliers = 0
+        self.best_solver_type = -1
+        self.best_model_score = float("inf")
+        self.inlier_ratios = [0.0, 0.0, 0.0]
+        self.inlier_indices = [[], [], []]
+        self.number_lo_iterations = 0
+        # engine counters (not in the reference)
+        self.num_hypotheses = 0
+        self.num_lo_sweeps = 0
+        self.num_batches = 0
+        self.seconds_total = 0.0
+        self.seconds_lo = 0.0
+        self.seconds_gpu_wait = 0.0
+
+    def __repr__(self):
+        return (f"HybridRansacStatistics(iterations={self.num_iterations_total}, per_solver={self.num_iterations_per_solver}, "
+                f"inliers={self.best_num_inliers}, score={self.best_model_score:.6g}, lo={self.number_lo_iterations})")
+
+
+# ---------------------------------------------------------------------------
+# model types (src/pose.h:7-56, src/bindings.cpp:111-154)
+class PoseAndScale:
+    def __init__(self, *args):
+        self.pose = np.zeros((3, 4))
+        self.scale = 1.0
+        if len(args) == 2:
+            self.pose = np.array(args[0], dtype=np.float64).reshape(3, 4)
+            self.scale = float(args[1])
+        elif len(args) == 3:
+            self.pose[:, :3] = np.asarray(args[0], dtype=np.float64).reshape(3, 3)
+            self.pose[:, 3] = np.asarray(args[1], dtype=np.float64).reshape(3)
+            self.scale = float(args[2])
+        elif args:
+            raise TypeError("PoseAndScale(pose, scale) or PoseAndScale(R, t, scale)")
+
+    def R(self):
+        return self.pose[:, :3].copy()
+
+    def t(self):
+        return self.pose[:, 3].copy()
+
+
+class PoseScaleOffset(PoseAndScale):
+    _n_extra = 0
+
+    def __init__(self, *args):
+        self.pose = np.zeros((3, 4))
+        self.scale, self.offset0, self.offset1 = 1.0, 0.0, 0.0
+        self._init_extra()
+        k = self._n_extra
+        if len(args) == 4 + k:  # pose, scale, b0, b1, [focals]
+            self.pose = np.array(args[0], dtype=np.float64).reshape(3, 4)
+            vals = args[1:]
+        elif len(args) == 5 + k:  # R, t, scale, b0, b1, [focals]
+            self.pose[:, :3] = np.asarray(args[0], dtype=np.float64).reshape(3, 3)
+            self.pose[:, 3] = np.asarray(args[1], dtype=np.float64).reshape(3)
+            vals = args[2:]
+        elif not args:
+            return
+        else:
+            raise TypeError(f"{type(self).__name__}: unexpected constructor arguments")
+        self.scale, self.offset0, self.offset1 = float(vals[0]), float(vals[1]), float(vals[2])
+        self._set_extra([float(v) for v in vals[3:]])
+
+    def _init_extra(self):
+        pass
+
+    def _set_extra(self, vals):
+        pass
+
+    def __repr__(self):
+        return f"{type(self).__name__}(scale={self.scale:.6g}, offset0={self.offset0:.6g}, offset1={self.offset1:.6g})"
+
+
+class PoseScaleOffsetSharedFocal(PoseScaleOffset):
+    _n_extra = 1
+
+    def _init_extra(self):
+        self.focal = 1.0
+
+    def _set_extra(self, vals):
+        self.focal = vals[0]
+
+
+class PoseScaleOffsetTwoFocal(PoseScaleOffset):
+    _n_extra = 2
+
+    def _init_extra(self):
+        self.focal0 = 1.0
+        self.focal1 = 1.0
+
+    def _set_extra(self, vals):
+        self.focal0, self.focal1 = vals[0], vals[1]
+
+
+def _model_from_c(m, variant):
+    R = np.array(m.R[:]).reshape(3, 3)
+    t = np.array(m.t[:])
+    if variant == L.CALIBRATED:
+        return PoseScaleOffset(R, t, m.scale, m.offset0, m.offset1)
+    if variant == L.SHARED_FOCAL:
+        return PoseScaleOffsetSharedFocal(R, t, m.scale, m.offset0, m.offset1, m.focal0)
+    return PoseScaleOffsetTwoFocal(R, t, m.scale, m.offset0, m.offset1, m.focal0, m.focal1)
+
+
+def _model_to_c(p, variant):
+    m = L.mp_model()
+    pose = np.asarray(p.pose, dtype=np.float64).reshape(3, 4)
+    m.R[:] = pose[:, :3].ravel().tolist()
+    m.t[:] = pose[:, 3].tolist()
+    m.scale, m.offset0, m.offset1 = float(p.scale), float(getattr(p, "offset0", 0.0)), float(getattr(p, "offset1", 0.0))
+    if variant == L.SHARED_FOCAL:
+        m.focal0 = m.focal1 = float(p.focal)
+    elif variant == L.TWO_FOCAL:
+        m.focal0, m.focal1 = float(p.focal0), float(p.focal1)
+    else:
+        m.focal0 = m.focal1 = 1.0
+    return m
+
+
+def _stats_from_c(s, idx, n):
+    out = HybridRansacStatistics()
+    out.num_iterations_total = int(s.num_iterations_total)
+    out.num_iterations_per_solver = [int(s.num_iterations_per_solver[0]), int(s.num_iterations_per_solver[1])]
+    out.best_num_inliers = int(s.best_num_inliers)
+    out.best_solver_type = int(s.best_solver_type)
+    out.best_model_score = float(s.best_model_score)
+    out.inlier_ratios = [float(v) for v in s.inlier_ratios]
+    out.inlier_indices = [idx[t * n: t * n + s.num_inliers[t]].tolist() for t in range(3)]
+    out.number_lo_iterations = int(s.number_lo_iterations)
+    out.num_hypotheses = int(s.num_hypotheses)
+    out.num_lo_sweeps = int(s.num_lo_sweeps)
+    out.num_batches = int(s.num_batches)
+    out.seconds_total = float(s.seconds_total)
+    out.seconds_lo = float(s.seconds_lo)
+    out.seconds_gpu_wait = float(s.seconds_gpu_wait)
+    return out
+
+
+# ---------------------------------------------------------------------------
+def _pts(a, name):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if a.ndim != 2 or a.shape[1] != 2:
+        raise ValueError(f"{name} must be an N x 2 array of pixel coordinates")
+    return a
+
+
+def _vec(a, n, name):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1))
+    if a.shape[0] != n:
+        raise ValueError(f"{name} must hold one value per correspondence ({n}), got {a.shape[0]}")
+    return a
+
+
+def _dp(a):
+    return a.ctypes.data_as(L.c_double_p)
+
+
+_DEFAULT_DEVICE = 0
+
+
+def set_device(device):
+    """Select the HIP device used by subsequent calls (one process per GPU)."""
+    global _DEFAULT_DEVICE
+    _DEFAULT_DEVICE = int(device)
+
+
+def _estimate(variant, x0, x1, depth0, depth1, min_depth, cam0, cam1, options, est_config, device):
+    x0 = _pts(x0, "x0")
+    x1 = _pts(x1, "x1")
+    n = x0.shape[0]
+    if x1.shape[0] != n:
+        raise ValueError("x0 and x1 must have the same number of rows")
+    d0 = _vec(depth0, n, "depth0")
+    d1 = _vec(depth1, n, "depth1")
+    md = np.ascontiguousarray(np.asarray(min_depth, dtype=np.float64).reshape(-1))
+    if md.shape[0] != 2:
+        raise ValueError("min_depth must hold two values")
+    ncam = 9 if variant == L.CALIBRATED else 2
+    c0 = np.ascontiguousarray(np.asarray(cam0, dtype=np.float64).reshape(-1))
+    c1 = np.ascontiguousarray(np.asarray(cam1, dtype=np.float64).reshape(-1))
+    if c0.shape[0] != ncam or c1.shape[0] != ncam:
+        raise ValueError("K0/K1 must be 3x3" if ncam == 9 else "pp0/pp1 must hold two values")
+    if est_config is None:
+        est_config = EstimatorConfig()
+    o = options._to_c()
+    c = est_config._to_c()
+    model = L.mp_model()
+    stats = L.mp_stats()
+    idx = np.zeros(3 * max(n, 1), dtype=np.int32)
+    code = L.lib().mp_estimate(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(md), _dp(c0), _dp(c1),
+                               ctypes.byref(o), ctypes.byref(c), ctypes.byref(model), ctypes.byref(stats),
+                               idx.ctypes.data_as(L.c_int32_p), _DEFAULT_DEVICE if device is None else int(device))
+    L.check(code)
+    return _model_from_c(model, variant), _stats_from_c(stats, idx, n)
+
+
+def HybridEstimatePoseScaleOffset(x0, x1, depth0, depth1, min_depth, K0, K1, options, est_config=None, device=None):
+    """src/hybrid_pose_estimator.cpp:8-35 (bindings.cpp:169-170)."""
+    return _estimate(L.CALIBRATED, x0, x1, depth0, depth1, min_depth, K0, K1, options, est_config, device)
+
+
+def HybridEstimatePoseScaleOffsetSharedFocal(x0, x1, depth0, depth1, min_depth, pp0, pp1, options, est_config=None,
+                                             device=None):
+    """src/hybrid_pose_shared_focal_estimator.cpp:8-51 (bindings.cpp:171-172)."""
+    return _estimate(L.SHARED_FOCAL, x0, x1, depth0, depth1, min_depth, pp0, pp1, options, est_config, device)
+
+
+def HybridEstimatePoseScaleOffsetTwoFocal(x0, x1, depth0, depth1, min_depth, pp0, pp1, options, est_config=None,
+                                          device=None):
+    """src/hybrid_pose_two_focal_estimator.cpp:34-75 (bindings.cpp:173-174)."""
+    return _estimate(L.TWO_FOCAL, x0, x1, depth0, depth1, min_depth, pp0, pp1, options, est_config, device)
+
+
+def HybridEstimatePoseAndScale(x0, x1, depth0, depth1, K0, K1, options, est_config=None):
+    """src/hybrid_pose_estimator.cpp:37-63 -- scale-only estimator (not yet ported)."""
+    raise NotImplementedError("HybridEstimatePoseAndScale is not available in this build yet")
+
+
+def estimate_batch(variant, pairs, options, est_config=None, device=None, num_streams=4):
+    """Many independent pairs on one device (host threads x HIP streams).
+
+    pairs: list of dicts with x0, x1, depth0, depth1, min_depth, and K0/K1 (calibrated)
+    or pp0/pp1.  Returns a list of (model, stats)."""
+    if est_config is None:
+        est_config = EstimatorConfig()
+    x0s, x1s, d0s, d1s, mds, c0s, c1s, offs = [], [], [], [], [], [], [], [0]
+    for p in pairs:
+        x0 = _pts(p["x0"], "x0")
+        n = x0.shape[0]
+        x0s.append(x0)
+        x1s.append(_pts(p["x1"], "x1"))
+        d0s.append(_vec(p["depth0"], n, "depth0"))
+        d1s.append(_vec(p["depth1"], n, "depth1"))
+        mds.append(np.asarray(p["min_depth"], dtype=np.float64).reshape(2))
+        if variant == L.CALIBRATED:
+            c0s.append(np.asarray(p["K0"], dtype=np.float64).reshape(9))
+            c1s.append(np.asarray(p["K1"], dtype=np.float64).reshape(9))
+        else:
+            c0s.append(np.asarray(p["pp0"], dtype=np.float64).reshape(2))
+            c1s.append(np.asarray(p["pp1"], dtype=np.float64).reshape(2))
+        offs.append(offs[-1] + n)
+    P = len(pairs)
+    cat = lambda xs, w: np.ascontiguousarray(np.concatenate(xs).reshape(-1)) if xs else np.zeros(w)
+    X0, X1, D0, D1 = cat(x0s, 2), cat(x1s, 2), cat(d0s, 1), cat(d1s, 1)
+    MD, C0, C1 = cat(mds, 2), cat(c0s, 9), cat(c1s, 9)
+    offsets = np.asarray(offs, dtype=np.int64)
+    models = (L.mp_model * max(P, 1))()
+    stats = (L.mp_stats * max(P, 1))()
+    idx = np.zeros(3 * max(offs[-1], 1), dtype=np.int32)
+    o = options._to_c()
+    c = est_config._to_c()
+    code = L.lib().mp_estimate_batch(variant, P, offsets.ctypes.data_as(L.c_int64_p), _dp(X0), _dp(X1), _dp(D0),
+                                     _dp(D1), _dp(MD), _dp(C0), _dp(C1), ctypes.byref(o), ctypes.byref(c), models,
+                                     stats, idx.ctypes.data_as(L.c_int32_p),
+                                     _DEFAULT_DEVICE if device is None else int(device), int(num_streams))
+    L.check(code)
+    out = []
+    for p in range(P):
+        n = offs[p + 1] - offs[p]
+        out.append((_model_from_c(models[p], variant), _stats_from_c(stats[p], idx[3 * offs[p]:], n)))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# standalone solver bindings (src/bindings.cpp:156-166)
+def _homog_pm(a, k, name):
+    a = np.asarray(a, dtype=np.float64)
+    if a.shape == (3, k):
+        return np.ascontiguousarray(a.T)
+    raise ValueError(f"{name} must be a 3 x {k} matrix of homogeneous points (columns)")
+
+
+def _solve_ss(variant, x_homo, y_homo, depth_x, depth_y):
+    k = 3 if variant == L.CALIBRATED else 4
+    x = _homog_pm(x_homo, k, "x_homo")
+    y = _homog_pm(y_homo, k, "y_homo")
+    dx = _vec(depth_x, k, "depth_x")
+    dy = _vec(depth_y, k, "depth_y")
+    w = [4, 5, 6][variant]
+    out = np.zeros(8 * w)
+    n = L.lib().mp_solve_scale_and_shift(variant, _dp(x), _dp(y), _dp(dx), _dp(dy), _dp(out), 8, _DEFAULT_DEVICE)
+    if n < 0:
+        L.check(-n)
+    return [out[i * w:(i + 1) * w].copy() for i in range(n)]
+
+
+def _solve_pose(variant, x_homo, y_homo, depth_x, depth_y):
+    k = 3 if variant == L.CALIBRATED else 4
+    x = _homog_pm(x_homo, k, "x_homo")
+    y = _homog_pm(y_homo, k, "y_homo")
+    dx = _vec(depth_x, k, "depth_x")
+    dy = _vec(depth_y, k, "depth_y")
+    out = (L.mp_model * 8)()
+    n = L.lib().mp_solve_scale_shift_pose(variant, _dp(x), _dp(y), _dp(dx), _dp(dy), out, 8, _DEFAULT_DEVICE)
+    if n < 0:
+        L.check(-n)
+    return [_model_from_c(out[i], variant) for i in range(n)]
+
+
+def solve_scale_and_shift(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:35-125: list of (1, b1, a2, b2*a2)."""
+    return _solve_ss(L.CALIBRATED, x_homo, y_homo, depth_x, depth_y)
+
+
+def solve_scale_and_shift_shared_focal(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:127-293: list of (1, b1, a2, b2*a2, f)."""
+    return _solve_ss(L.SHARED_FOCAL, x_homo, y_homo, depth_x, depth_y)
+
+
+def solve_scale_and_shift_two_focal(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:295-480: list of (1, b1, a2, b2*a2, f1, f2)."""
+    return _solve_ss(L.TWO_FOCAL, x_homo, y_homo, depth_x, depth_y)
+
+
+def solve_scale_shift_pose(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:482-534 (wrapper :1408-1415)."""
+    return _solve_pose(L.CALIBRATED, x_homo, y_homo, depth_x, depth_y)
+
+
+def solve_scale_shift_pose_shared_focal(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:682-739 (wrapper :1417-1424)."""
+    return _solve_pose(L.SHARED_FOCAL, x_homo, y_homo, depth_x, depth_y)
+
+
+def solve_scale_shift_pose_two_focal(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:986-1043 (wrapper :1426-1433)."""
+    return _solve_pose(L.TWO_FOCAL, x_homo, y_homo, depth_x, depth_y)
+
+
+def relpose_5pt(x1, x2):
+    """Device 5-point solver on unit bearings (5 x 3 each): list of PoseScaleOffset (scale 1)."""
+    b1 = np.ascontiguousarray(np.asarray(x1, dtype=np.float64).reshape(5, 3))
+    b2 = np.ascontiguousarray(np.asarray(x2, dtype=np.float64).reshape(5, 3))
+    out = (L.mp_model * 16)()
+    n = L.lib().mp_relpose_5pt(_dp(b1), _dp(b2), out, 16, _DEFAULT_DEVICE)
+    if n < 0:
+        L.check(-n)
+    return [_model_from_c(out[i], L.CALIBRATED) for i in range(min(n, 16))]
+
+
+def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, models, with_errors=False):
+    """Device ScoreModel over explicit models given in problem units (tests / diagnostics)."""
+    x0 = _pts(x0, "x0")
+    x1 = _pts(x1, "x1")
+    n = x0.shape[0]
+    d0 = _vec(depth0, n, "depth0")
+    d1 = _vec(depth1, n, "depth1")
+    c0 = np.ascontiguousarray(np.asarray(cam0, dtype=np.float64).reshape(-1))
+    c1 = np.ascontiguousarray(np.asarray(cam1, dtype=np.float64).reshape(-1))
+    nm = len(models)
+    arr = (L.mp_model * max(nm, 1))(*[_model_to_c(m, variant) for m in models])
+    scores = np.zeros(max(nm, 1))
+    errors = np.zeros((max(nm, 1), 3, n)) if with_errors else None
+    o = options._to_c()
+    c = (est_config or EstimatorConfig())._to_c()
+    code = L.lib().mp_score_models(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1), ctypes.byref(o),
+                                   ctypes.byref(c), arr, nm, _dp(scores),
+                                   _dp(errors) if with_errors else None, _DEFAULT_DEVICE)
+    L.check(code)
+    return (scores[:nm], errors[:nm]) if with_errors else scores[:nm]
+
+
+def device_count():
+    return int(L.lib().mp_device_count())
+
+
+def version():
+    return L.lib().mp_version().decode()

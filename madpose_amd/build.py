@@ -1,0 +1,71 @@
+"""Build the MI355X engine library in-tree: madpose_amd/lib/libmadpose_mi355x.so.
+
+hipcc cross-compiles for gfx950 without a GPU.  Every translation unit is built as
+HIP (host + device); the shared library exports the C ABI of
+include/madpose_mi355x.h.
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+OBJDIR = os.path.join(HERE, "lib", "obj")
+LIB = os.path.join(LIBDIR, "libmadpose_mi355x.so")
+
+SOURCES = [
+    os.path.join(CSRC, "kernels", "kernels.hip"),
+    os.path.join(CSRC, "host", "engine.cpp"),
+    os.path.join(CSRC, "host", "lm.cpp"),
+    os.path.join(CSRC, "capi.cpp"),
+]
+HEADERS = [
+    os.path.join(dp, f)
+    for dp, _, fs in os.walk(CSRC)
+    for f in fs
+    if f.endswith(".h")
+] + [os.path.join(ROOT, "include", "madpose_mi355x.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"), "-Wall",
+         "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src):
+    obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
+    if _newer(obj, [src] + HEADERS):
+        cmd = [HIPCC, "-x", "hip"] + FLAGS + ["-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build_library(verbose=False):
+    os.makedirs(OBJDIR, exist_ok=True)
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if _newer(LIB, objs):
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build_library(verbose=True)
+    sys.exit(0)

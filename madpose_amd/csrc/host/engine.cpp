@@ -1,0 +1,798 @@
+// Host controller of the MI355X hybrid LO-MSAC estimator.
+//
+// Semantics follow HybridLOMSAC::EstimateModel (src/hybrid_ransac.h:38-206) step for
+// step; the difference is WHERE the work runs.  The reference draws one minimal
+// sample, solves it and scores its models over all 3N residuals before drawing the
+// next.  Here the controller replays the reference's two random streams
+// (sampler mt19937, solver-selection/LO mt19937, both seeded with random_seed) to
+// generate a *speculative batch* of B iterations, assuming no local optimisation
+// happens inside the batch; the GPU solves every sample and scores every model of
+// the batch in one pass; the host then scans the per-iteration best scores in
+// order, reproducing the sequential decisions exactly.  The only event that
+// invalidates the rest of a batch is an LO run (it consumes the selection stream);
+// the controller then rewinds both streams to the end of that iteration, runs LO
+// and starts the next batch there.  New-best events before lo_starting_iterations
+// do not consume randomness and do not cut the batch.  Results are therefore
+// independent of the batch size (tests/test_engine_gpu.py checks this).
+//
+// Local optimisation stays on the host (north star); its full-data sweeps
+// (ScoreModel / GetInliers) run on the GPU through the single-model sweep kernel.
+#include "engine.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+#include "../include/mp_score.h"
+#include "../kernels/kernels.h"
+#include "rng.h"
+
+namespace mp {
+
+#define MP_HIP(expr)                                                                                                    \
+    do {                                                                                                               \
+        hipError_t e_ = (expr);                                                                                        \
+        if (e_ != hipSuccess)                                                                                          \
+            throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #expr);               \
+    } while (0)
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::now() - a).count(); }
+
+const double kMax = DBL_MAX;
+
+// ---------------------------------------------------------------------------
+// Device context: stream + cached buffers (one per device and concurrent caller)
+struct DeviceCtx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int64_t cap_n = 0;
+    int cap_b = 0, cap_m = 0;
+    double *d_pair = nullptr; // 8 arrays of cap_n
+    int *d_samples = nullptr, *d_md_list = nullptr, *d_pt_list = nullptr, *d_counts = nullptr, *d_best_slot = nullptr;
+    Model *d_models = nullptr;
+    ScoreRec *d_recs = nullptr;
+    double *d_scores = nullptr, *d_best = nullptr;
+    ScoreRec *d_rec1 = nullptr;
+    double *d_err = nullptr, *d_score1 = nullptr;
+    // pinned host mirrors
+    int *h_samples = nullptr, *h_md_list = nullptr, *h_pt_list = nullptr, *h_counts = nullptr, *h_best_slot = nullptr;
+    double *h_best = nullptr, *h_err = nullptr, *h_score1 = nullptr;
+    ScoreRec *h_rec1 = nullptr;
+    Model *h_model1 = nullptr;
+
+    void free_all() {
+        hipSetDevice(device);
+        for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_md_list, (void *)d_pt_list, (void *)d_counts,
+                        (void *)d_best_slot, (void *)d_models, (void *)d_recs, (void *)d_scores, (void *)d_best,
+                        (void *)d_rec1, (void *)d_err, (void *)d_score1})
+            if (p) hipFree(p);
+        for (void *p : {(void *)h_samples, (void *)h_md_list, (void *)h_pt_list, (void *)h_counts, (void *)h_best_slot,
+                        (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1})
+            if (p) hipHostFree(p);
+        d_pair = d_err = d_scores = d_best = d_score1 = nullptr;
+        d_samples = d_md_list = d_pt_list = d_counts = d_best_slot = nullptr;
+        d_models = nullptr;
+        d_recs = d_rec1 = nullptr;
+        h_samples = h_md_list = h_pt_list = h_counts = h_best_slot = nullptr;
+        h_best = h_err = h_score1 = nullptr;
+        h_rec1 = nullptr;
+        h_model1 = nullptr;
+        cap_n = 0;
+        cap_b = cap_m = 0;
+    }
+
+    void ensure(int64_t n, int B, int M) {
+        if (n <= cap_n && B <= cap_b && M <= cap_m) return;
+        const int64_t nn = std::max<int64_t>(std::max<int64_t>(n, cap_n), 64);
+        const int bb = std::max(B, cap_b), mm = std::max(M, cap_m);
+        free_all();
+        MP_HIP(hipSetDevice(device));
+        MP_HIP(hipMalloc(&d_pair, sizeof(double) * 8 * nn));
+        MP_HIP(hipMalloc(&d_err, sizeof(double) * 3 * nn));
+        MP_HIP(hipMalloc(&d_samples, sizeof(int) * 8 * bb));
+        MP_HIP(hipMalloc(&d_md_list, sizeof(int) * bb));
+        MP_HIP(hipMalloc(&d_pt_list, sizeof(int) * bb));
+        MP_HIP(hipMalloc(&d_counts, sizeof(int) * bb));
+        MP_HIP(hipMalloc(&d_best_slot, sizeof(int) * bb));
+        MP_HIP(hipMalloc(&d_best, sizeof(double) * bb));
+        MP_HIP(hipMalloc(&d_models, sizeof(Model) * (size_t)bb * mm));
+        MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * (size_t)bb * mm));
+        MP_HIP(hipMalloc(&d_scores, sizeof(double) * (size_t)bb * mm));
+        MP_HIP(hipMalloc(&d_rec1, sizeof(ScoreRec) * 64));
+        MP_HIP(hipMalloc(&d_score1, sizeof(double) * 64));
+        MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 8 * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_md_list, sizeof(int) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_pt_list, sizeof(int) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_counts, sizeof(int) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_best_slot, sizeof(int) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_best, sizeof(double) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_err, sizeof(double) * 3 * nn, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_model1, sizeof(Model) * 64, hipHostMallocDefault));
+        cap_n = nn;
+        cap_b = bb;
+        cap_m = mm;
+    }
+};
+
+std::mutex g_pool_mu;
+std::vector<DeviceCtx *> g_pool;
+
+struct CtxLease {
+    DeviceCtx *c = nullptr;
+    explicit CtxLease(int device) {
+        {
+            std::lock_guard<std::mutex> lk(g_pool_mu);
+            for (size_t i = 0; i < g_pool.size(); ++i)
+                if (g_pool[i]->device == device) {
+                    c = g_pool[i];
+                    g_pool.erase(g_pool.begin() + i);
+                    break;
+                }
+        }
+        if (!c) {
+            int cnt = 0;
+            if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0)
+                throw std::runtime_error("no HIP device available (MI355X required; there is no CPU fallback)");
+            if (device < 0 || device >= cnt) throw std::invalid_argument("device index out of range");
+            c = new DeviceCtx();
+            c->device = device;
+            MP_HIP(hipSetDevice(device));
+            MP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        }
+        MP_HIP(hipSetDevice(device));
+    }
+    ~CtxLease() {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        g_pool.push_back(c);
+    }
+};
+
+// ---------------------------------------------------------------------------
+void inv3(const double *K, double *Ki) {
+    const double d = K[0] * (K[4] * K[8] - K[5] * K[7]) - K[1] * (K[3] * K[8] - K[5] * K[6]) +
+                     K[2] * (K[3] * K[7] - K[4] * K[6]);
+    Ki[0] = (K[4] * K[8] - K[5] * K[7]) / d;
+    Ki[1] = (K[2] * K[7] - K[1] * K[8]) / d;
+    Ki[2] = (K[1] * K[5] - K[2] * K[4]) / d;
+    Ki[3] = (K[5] * K[6] - K[3] * K[8]) / d;
+    Ki[4] = (K[0] * K[8] - K[2] * K[6]) / d;
+    Ki[5] = (K[2] * K[3] - K[0] * K[5]) / d;
+    Ki[6] = (K[3] * K[7] - K[4] * K[6]) / d;
+    Ki[7] = (K[1] * K[6] - K[0] * K[7]) / d;
+    Ki[8] = (K[0] * K[4] - K[1] * K[3]) / d;
+}
+
+// Problem setup shared by every entry point: the option transform to three data
+// types (src/hybrid_pose_estimator.cpp:13-23) and, for SF/TF, pp-centring plus
+// PoseLib normalize_points(..., true, false, true) (..shared..cpp:14-25).
+struct Problem {
+    PairConst C;
+    HostPair H;
+    double norm_scale = 1.0;
+};
+
+Problem make_problem(const PairInput &in, const RansacOptions &o, const EstimatorConfig &cfg) {
+    Problem P;
+    const int n = (int)in.n;
+    PairConst &C = P.C;
+    std::memset(&C, 0, sizeof(C));
+    C.variant = in.variant;
+    C.n = n;
+    C.score_type = cfg.score_type;
+    C.min_depth_constraint = cfg.min_depth_constraint ? 1 : 0;
+    C.use_shift = cfg.use_shift ? 1 : 0;
+    C.min_depth[0] = in.min_depth[0];
+    C.min_depth[1] = in.min_depth[1];
+    HostPair &H = P.H;
+    H.variant = in.variant;
+    H.n = n;
+    H.x0.resize(2 * n);
+    H.x1.resize(2 * n);
+    H.d0.assign(in.d0, in.d0 + n);
+    H.d1.assign(in.d1, in.d1 + n);
+    H.min_depth[0] = in.min_depth[0];
+    H.min_depth[1] = in.min_depth[1];
+    double thr0 = o.squared_inlier_thresholds[0], thr1 = o.squared_inlier_thresholds[1];
+    if (in.variant == kCal) {
+        std::memcpy(C.K0, in.cam0, sizeof(C.K0));
+        std::memcpy(C.K1, in.cam1, sizeof(C.K1));
+        inv3(C.K0, C.K0i);
+        inv3(C.K1, C.K1i);
+        std::memcpy(H.x0.data(), in.x0, sizeof(double) * 2 * n);
+        std::memcpy(H.x1.data(), in.x1, sizeof(double) * 2 * n);
+        const double s = 1.0 / (C.K0[0] + C.K0[4]) + 1.0 / (C.K1[0] + C.K1[4]);
+        C.loss_scale = 1.0 / (s * s);
+    } else {
+        double scale = 0.0;
+        for (int i = 0; i < n; ++i) {
+            const double a0 = in.x0[2 * i] - in.cam0[0], a1 = in.x0[2 * i + 1] - in.cam0[1];
+            const double b0 = in.x1[2 * i] - in.cam1[0], b1 = in.x1[2 * i + 1] - in.cam1[1];
+            H.x0[2 * i] = a0;
+            H.x0[2 * i + 1] = a1;
+            H.x1[2 * i] = b0;
+            H.x1[2 * i + 1] = b1;
+            scale += std::sqrt(a0 * a0 + a1 * a1) + std::sqrt(b0 * b0 + b1 * b1);
+        }
+        scale = (n > 0) ? scale / (std::sqrt(2.0) * n) : 1.0;
+        for (int i = 0; i < 2 * n; ++i) {
+            H.x0[i] /= scale;
+            H.x1[i] /= scale;
+        }
+        P.norm_scale = scale;
+        thr0 /= scale * scale;
+        thr1 /= scale * scale;
+        for (int i = 0; i < 9; ++i) C.K0[i] = C.K1[i] = C.K0i[i] = C.K1i[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        C.loss_scale = 1.0;
+    }
+    std::memcpy(H.K0, C.K0, sizeof(H.K0));
+    std::memcpy(H.K1, C.K1, sizeof(H.K1));
+    std::memcpy(H.K0i, C.K0i, sizeof(H.K0i));
+    std::memcpy(H.K1i, C.K1i, sizeof(H.K1i));
+    const double w0 = o.data_type_weights[0];
+    const double ws = o.data_type_weights[1] * 2.0 * thr0 / thr1;
+    H.sampson_squared_weight = ws;
+    C.thr[0] = C.thr[1] = thr0;
+    C.thr[2] = thr1;
+    C.w[0] = C.w[1] = w0;
+    C.w[2] = ws;
+    return P;
+}
+
+void upload_pair(DeviceCtx &X, const Problem &P, PairData *D) {
+    const int64_t n = P.C.n;
+    double *base = X.d_pair;
+    const int64_t cn = X.cap_n;
+    std::vector<double> soa(6 * (size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        soa[i] = P.H.x0[2 * i];
+        soa[n + i] = P.H.x0[2 * i + 1];
+        soa[2 * n + i] = P.H.x1[2 * i];
+        soa[3 * n + i] = P.H.x1[2 * i + 1];
+        soa[4 * n + i] = P.H.d0[i];
+        soa[5 * n + i] = P.H.d1[i];
+    }
+    for (int a = 0; a < 6; ++a)
+        MP_HIP(hipMemcpyAsync(base + a * cn, soa.data() + a * n, sizeof(double) * n, hipMemcpyHostToDevice, X.stream));
+    D->x0u = base;
+    D->x0v = base + cn;
+    D->x1u = base + 2 * cn;
+    D->x1v = base + 3 * cn;
+    D->d0 = base + 4 * cn;
+    D->d1 = base + 5 * cn;
+    D->r0 = base + 6 * cn;
+    D->r1 = base + 7 * cn;
+    MP_HIP(launch_prep_pair(X.stream, P.C, *D, base + 6 * cn, base + 7 * cn));
+    // the staging vector dies here: make the copies complete first
+    MP_HIP(hipStreamSynchronize(X.stream));
+}
+
+// ---------------------------------------------------------------------------
+// The estimator run (one pair)
+class Run {
+  public:
+    Run(DeviceCtx &X, const Problem &P, const RansacOptions &o, const EstimatorConfig &cfg)
+        : X_(X), P_(P), o_(o), cfg_(cfg), n_(P.C.n), variant_(P.C.variant), maxm_(max_models(P.C.variant)) {
+        const int kmd = variant_ == kCal ? 3 : 4;
+        const int kpt = variant_ == kCal ? 5 : (variant_ == kSF ? 6 : 7);
+        ss_[0][0] = kmd;
+        ss_[0][1] = kmd;
+        ss_[0][2] = 0;
+        ss_[1][0] = 0;
+        ss_[1][1] = 0;
+        ss_[1][2] = kpt;
+        min_sample_size_ = kpt;
+        non_min_sample_size_ = variant_ == kCal ? 35 : 36;
+        thr_[0] = P.C.thr[0];
+        thr_[1] = P.C.thr[1];
+        thr_[2] = P.C.thr[2];
+        w_[0] = P.C.w[0];
+        w_[1] = P.C.w[1];
+        w_[2] = P.C.w[2];
+        const char *env = std::getenv("MADPOSE_MAX_BATCH");
+        max_batch_ = env ? std::max(1, std::atoi(env)) : 8192;
+        const char *env2 = std::getenv("MADPOSE_MIN_BATCH");
+        min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 128;
+        min_batch_ = std::min(min_batch_, max_batch_);
+    }
+
+    void run(Model *best, Stats *S);
+
+  private:
+    DeviceCtx &X_;
+    const Problem &P_;
+    const RansacOptions &o_;
+    const EstimatorConfig &cfg_;
+    const int n_, variant_, maxm_;
+    int ss_[2][3];
+    int min_sample_size_, non_min_sample_size_;
+    double thr_[3], w_[3];
+    int max_batch_, min_batch_;
+    PairData D_;
+    Stats *S_ = nullptr;
+    IterationStream rs_; // sampler + selection/LO streams
+    // single-model sweep cache
+    Model cache_model_;
+    bool cache_valid_ = false;
+    double cache_score_ = 0.0;
+    std::vector<double> err_;
+
+    // --- GPU sweeps ---
+    const double *sweep(const Model &m, double *score) {
+        if (cache_valid_ && std::memcmp(&m, &cache_model_, sizeof(Model)) == 0) {
+            *score = cache_score_;
+            return err_.data();
+        }
+        prepare_score_rec(P_.C, m, X_.h_rec1[0]);
+        MP_HIP(hipMemcpyAsync(X_.d_rec1, X_.h_rec1, sizeof(ScoreRec), hipMemcpyHostToDevice, X_.stream));
+        MP_HIP(launch_sweep(X_.stream, D_, P_.C, X_.d_rec1, X_.d_err, X_.d_score1));
+        MP_HIP(hipMemcpyAsync(X_.h_err, X_.d_err, sizeof(double) * 3 * n_, hipMemcpyDeviceToHost, X_.stream));
+        MP_HIP(hipMemcpyAsync(X_.h_score1, X_.d_score1, sizeof(double), hipMemcpyDeviceToHost, X_.stream));
+        MP_HIP(hipStreamSynchronize(X_.stream));
+        err_.assign(X_.h_err, X_.h_err + 3 * n_);
+        cache_model_ = m;
+        cache_score_ = X_.h_score1[0];
+        cache_valid_ = true;
+        S_->num_lo_sweeps++;
+        *score = cache_score_;
+        return err_.data();
+    }
+    double score(const Model &m) {
+        double s;
+        sweep(m, &s);
+        return s;
+    }
+    int inliers(const Model &m, const double *thr, std::vector<int> out[3]) {
+        double s;
+        const double *e = sweep(m, &s);
+        int c = 0;
+        for (int t = 0; t < 3; ++t) {
+            out[t].clear();
+            for (int i = 0; i < n_; ++i)
+                if (e[(size_t)t * n_ + i] < thr[t]) {
+                    out[t].push_back(i);
+                    ++c;
+                }
+        }
+        return c;
+    }
+
+    static void update_best(double sc, const Model &m, int st, double *best_sc, Model *best, int *best_st) {
+        if (sc < *best_sc) {
+            *best_sc = sc;
+            *best = m;
+            *best_st = st;
+        }
+    }
+
+    uint32_t num_required(int s) const {
+        double p_all = 1.0;
+        for (int t = 0; t < 3; ++t) p_all *= std::pow(S_->inlier_ratios[t], (double)ss_[s][t]);
+        if (p_all <= 0.0) return o_.max_num_iterations_per_solver;
+        if (p_all >= 1.0) return o_.min_num_iterations;
+        const double p_bad = 1.0 - p_all;
+        if (p_bad >= 0.99999999999999) return o_.max_num_iterations_per_solver;
+        const double it = std::ceil(std::log(1.0 - o_.success_probability) / std::log(p_bad) + 0.5);
+        uint32_t r = std::min((uint32_t)it, o_.max_num_iterations_per_solver);
+        return std::max(o_.min_num_iterations, r);
+    }
+
+    // UpdateRANSACTerminationCriteria (src/hybrid_ransac.h:351-378)
+    void termination(const Model &m, uint32_t *max_per) {
+        S_->best_num_inliers = inliers(m, thr_, S_->inlier_indices);
+        for (int t = 0; t < 3; ++t)
+            S_->inlier_ratios[t] = n_ > 0 ? (double)S_->inlier_indices[t].size() / (double)n_ : 0.0;
+        for (int s = 0; s < 2; ++s) max_per[s] = num_required(s);
+    }
+
+    // --- LO (src/hybrid_ransac.h:383-538) ---
+    void least_squares(const std::vector<int> sample[3], Model *m, bool nonminimal) {
+        const int kmd = variant_ == kCal ? 3 : 4;
+        if (((int)sample[0].size() < kmd && (int)sample[1].size() < kmd) || (int)sample[2].size() < min_sample_size_)
+            return;
+        LMSettings S;
+        S.use_reproj = cfg_.lo_type != 1;
+        S.use_sampson = cfg_.lo_type != 2;
+        // use_shift is forwarded by the calibrated estimator (NonMinimalSolver and
+        // LeastSquares) and by the shared-focal NonMinimalSolver only.
+        S.use_shift = (variant_ == kCal || (variant_ == kSF && nonminimal)) ? cfg_.use_shift : true;
+        S.min_depth_constraint = cfg_.min_depth_constraint;
+        S.w_sampson = variant_ == kCal ? std::sqrt(P_.H.sampson_squared_weight) /
+                                             (1.0 / (P_.C.K0[0] + P_.C.K0[4]) + 1.0 / (P_.C.K1[0] + P_.C.K1[4]))
+                                       : std::sqrt(P_.H.sampson_squared_weight);
+        S.ftol = cfg_.ftol;
+        S.gtol = cfg_.gtol;
+        S.ptol = cfg_.ptol;
+        S.max_iter = (int)cfg_.max_iter;
+        lm_refine(P_.H, sample, S, m);
+    }
+
+    static void split(const std::vector<int> &all, int n, std::vector<int> out[3]) {
+        for (int t = 0; t < 3; ++t) out[t].clear();
+        for (int idx : all) {
+            int t = 0;
+            while (idx >= n) {
+                idx -= n;
+                ++t;
+            }
+            out[t].push_back(idx);
+        }
+    }
+    void shuffle_resize(int k, std::vector<int> *v) {
+        const int n = (int)v->size();
+        if (n <= k) return;
+        for (int i = 0; i < k; ++i) std::swap((*v)[i], (*v)[uniform_int(rs_.sel, i, n - 1)]);
+        v->resize(k);
+    }
+
+    void lsq_fit(const double *thr, int st, Model *m, bool use_all) {
+        std::vector<int> inl[3];
+        inliers(*m, thr, inl);
+        int k[3];
+        for (int t = 0; t < 3; ++t) {
+            if ((int)inl[t].size() < ss_[st][t]) return;
+            k[t] = std::min(ss_[st][t] * o_.min_sample_multiplicator, (int)inl[t].size());
+        }
+        if (use_all) {
+            least_squares(inl, m, false);
+            return;
+        }
+        const int total = (k[0] + k[1] + k[2]) * o_.min_sample_multiplicator;
+        std::vector<int> all;
+        for (int t = 0; t < 3; ++t)
+            for (int idx : inl[t]) all.push_back(idx + t * n_);
+        shuffle_resize(total, &all);
+        std::vector<int> smp[3];
+        split(all, n_, smp);
+        least_squares(smp, m, false);
+    }
+
+    void local_opt(int st, Model *best_min, double *best_min_score, int *best_st) {
+        auto t0 = Clock::now();
+        double thr[3], upd[3];
+        for (int t = 0; t < 3; ++t) {
+            upd[t] = (o_.threshold_multiplier - 1.0) * thr_[t] / (int)(o_.num_lsq_iterations - 1);
+            thr[t] = thr_[t] * o_.threshold_multiplier;
+        }
+        Model m_init = *best_min;
+        lsq_fit(thr, st, &m_init, true);
+        double sc = score(m_init);
+        update_best(sc, m_init, st, best_min_score, best_min, best_st);
+        std::vector<int> base[3];
+        inliers(m_init, thr_, base);
+        std::vector<int> base_all;
+        for (int t = 0; t < 3; ++t)
+            for (int idx : base[t]) base_all.push_back(idx + t * n_);
+        const int k_nonmin = std::max(non_min_sample_size_,
+                                      std::min(min_sample_size_ * o_.non_min_sample_multiplier, (int)base_all.size() / 2));
+        for (int r = 0; r < o_.num_lo_steps; ++r) {
+            std::vector<int> sample_all = base_all; // copied before the shuffle (:439-440)
+            shuffle_resize(k_nonmin, &base_all);
+            Model m = m_init;
+            std::vector<int> smp[3];
+            split(sample_all, n_, smp);
+            {
+                const int kmd = variant_ == kCal ? 3 : 4;
+                if (((int)smp[0].size() < kmd && (int)smp[1].size() < kmd) || (int)smp[2].size() < min_sample_size_)
+                    continue; // NonMinimalSolver returns 0
+                const size_t nres = (cfg_.lo_type != 1 ? smp[0].size() + smp[1].size() : 0) +
+                                    (cfg_.lo_type != 2 ? smp[2].size() : 0);
+                if (nres == 0) continue; // Solve() == false
+                least_squares(smp, &m, true);
+            }
+            sc = score(m);
+            update_best(sc, m, st, best_min_score, best_min, best_st);
+            lsq_fit(thr_, st, &m, false);
+            double cur[3] = {thr[0], thr[1], thr[2]};
+            for (int i = 0; i < o_.num_lsq_iterations; ++i) {
+                lsq_fit(cur, st, &m, false);
+                sc = score(m);
+                update_best(sc, m, st, best_min_score, best_min, best_st);
+                for (int t = 0; t < 3; ++t) cur[t] -= upd[t];
+            }
+        }
+        S_->seconds_lo += secs(t0);
+    }
+
+    Model fetch_model(int b, int slot) {
+        MP_HIP(hipMemcpyAsync(X_.h_model1, X_.d_models + (size_t)b * maxm_ + slot, sizeof(Model),
+                              hipMemcpyDeviceToHost, X_.stream));
+        MP_HIP(hipStreamSynchronize(X_.stream));
+        return X_.h_model1[0];
+    }
+};
+
+void Run::run(Model *best, Stats *S) {
+    auto t_start = Clock::now();
+    S_ = S;
+    *S = Stats();
+    S->best_model_score = kMax;
+    std::memset(best, 0, sizeof(Model));
+    best->scale = 1.0;
+    best->focal0 = best->focal1 = 1.0;
+    double *prior = rs_.prior;
+    if (cfg_.solver_type == 1) prior[0] = 0.0;
+    if (cfg_.solver_type == 2) prior[1] = 0.0;
+    for (int s = 0; s < 2; ++s)
+        for (int t = 0; t < 3; ++t) {
+            rs_.ss[s][t] = ss_[s][t];
+            if (ss_[s][t] > n_) prior[s] = 0.0;
+        }
+    if (prior[0] <= 0.0 && prior[1] <= 0.0) { // VerifyData failed
+        S->seconds_total = secs(t_start);
+        return;
+    }
+    X_.ensure(n_, max_batch_, maxm_);
+    upload_pair(X_, P_, &D_);
+    rs_.n = n_;
+    rs_.seed(o_.random_seed);
+
+    const uint32_t max_total = std::max(o_.max_num_iterations, o_.min_num_iterations);
+    uint32_t max_per[2];
+    max_per[0] = max_per[1] = std::max(o_.max_num_iterations_per_solver, o_.min_num_iterations);
+    const uint32_t lo_start = (uint32_t)o_.lo_starting_iterations;
+    Model best_min;
+    std::memset(&best_min, 0, sizeof(best_min));
+    double best_min_score = kMax;
+
+    uint32_t it = 0;
+    bool done = false;
+    int bcur = min_batch_;
+    std::vector<uint8_t> types(max_batch_);
+    while (it < max_total && !done) {
+        if (it == lo_start && best_min_score < kMax) {
+            ++S->number_lo_iterations;
+            local_opt(S->best_solver_type, best, &S->best_model_score, &S->best_solver_type);
+            termination(*best, max_per);
+        }
+        uint32_t B = std::min<uint32_t>((uint32_t)bcur, max_total - it);
+        if (it < lo_start) B = std::min<uint32_t>(B, lo_start - it);
+        const IterationStream rs0 = rs_;
+        int nmd = 0, npt = 0;
+        for (uint32_t j = 0; j < B; ++j) {
+            const int st = rs_.next(X_.h_samples + 8 * j);
+            types[j] = (uint8_t)st;
+            if (st == 0)
+                X_.h_md_list[nmd++] = (int)j;
+            else
+                X_.h_pt_list[npt++] = (int)j;
+        }
+        hipStream_t s = X_.stream;
+        MP_HIP(hipMemcpyAsync(X_.d_samples, X_.h_samples, sizeof(int) * 8 * B, hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(X_.d_md_list, X_.h_md_list, sizeof(int) * std::max(nmd, 1), hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
+        MP_HIP(launch_md_solve(s, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs, X_.d_counts, maxm_));
+        MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, X_.d_models, X_.d_recs, X_.d_counts, maxm_));
+        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_best,
+                                  X_.d_best_slot));
+        MP_HIP(hipMemcpyAsync(X_.h_best, X_.d_best, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+        MP_HIP(hipMemcpyAsync(X_.h_best_slot, X_.d_best_slot, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        MP_HIP(hipMemcpyAsync(X_.h_counts, X_.d_counts, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        auto tw = Clock::now();
+        MP_HIP(hipStreamSynchronize(s));
+        S->seconds_gpu_wait += secs(tw);
+        S->num_batches++;
+
+        bool invalidated = false;
+        uint32_t j = 0;
+        for (; j < B; ++j) {
+            const uint32_t iter = it + j;
+            const int st = types[j];
+            S->num_iterations_per_solver[st] += 1;
+            const int nm = X_.h_counts[j];
+            S->num_hypotheses += (uint64_t)nm;
+            bool lo_here = false;
+            if (nm > 0) {
+                const double bl = X_.h_best[j];
+                if (bl < best_min_score || iter == lo_start) {
+                    const bool new_best = bl < best_min_score;
+                    if (new_best) {
+                        best_min_score = bl;
+                        best_min = fetch_model((int)j, X_.h_best_slot[j]);
+                        update_best(best_min_score, best_min, st, &S->best_model_score, best, &S->best_solver_type);
+                    }
+                    const bool run_lo = iter >= lo_start && best_min_score < kMax;
+                    if (new_best || run_lo) {
+                        if (run_lo) {
+                            // rewind both streams to the end of iteration `iter`
+                            rs_ = rs0;
+                            int scratch[8];
+                            for (uint32_t r = 0; r <= j; ++r) rs_.next(scratch);
+                            ++S->number_lo_iterations;
+                            double sc = best_min_score;
+                            local_opt(S->best_solver_type, &best_min, &sc, &S->best_solver_type);
+                            update_best(sc, best_min, st, &S->best_model_score, best, &S->best_solver_type);
+                            lo_here = true;
+                            invalidated = true;
+                        }
+                        termination(*best, max_per);
+                    }
+                }
+            }
+            if (S->num_iterations_per_solver[st] >= max_per[st]) {
+                // `break` in the reference skips the loop increment
+                S->num_iterations_total = iter;
+                done = true;
+                if (!lo_here) {
+                    rs_ = rs0;
+                    int scratch[8];
+                    for (uint32_t r = 0; r <= j; ++r) rs_.next(scratch);
+                }
+                break;
+            }
+            if (invalidated) {
+                it = iter + 1;
+                break;
+            }
+        }
+        if (!done && !invalidated) it += B;
+        // batch-size schedule: grow while batches survive, shrink after a cut
+        if (invalidated)
+            bcur = std::max(min_batch_, bcur / 2);
+        else
+            bcur = std::min(max_batch_, bcur * 2);
+    }
+    if (!done) S->num_iterations_total = it;
+
+    if (S->num_iterations_total <= lo_start && S->best_model_score < kMax) {
+        ++S->number_lo_iterations;
+        local_opt(S->best_solver_type, best, &S->best_model_score, &S->best_solver_type);
+        termination(*best, max_per);
+    }
+    if (o_.final_least_squares) {
+        auto t0 = Clock::now();
+        Model refined = *best;
+        least_squares(S->inlier_indices, &refined, false);
+        const double sc = score(refined);
+        if (sc < S->best_model_score) {
+            S->best_model_score = sc;
+            *best = refined;
+            termination(*best, max_per);
+        }
+        S->seconds_lo += secs(t0);
+    }
+    S->seconds_total = secs(t_start);
+}
+
+void validate(const PairInput &in, const RansacOptions &o) {
+    if (in.variant < 0 || in.variant > 2) throw std::invalid_argument("variant must be 0 (calibrated), 1 or 2");
+    if (in.n < 0 || in.n > (int64_t)1 << 30) throw std::invalid_argument("bad number of correspondences");
+    if (in.n > 0 && (!in.x0 || !in.x1 || !in.d0 || !in.d1)) throw std::invalid_argument("null input array");
+    if (!(o.squared_inlier_thresholds[0] > 0) || !(o.squared_inlier_thresholds[1] > 0))
+        throw std::invalid_argument("squared_inlier_thresholds must hold two positive values");
+    if (o.use_ours || o.use_4p4d)
+        throw std::invalid_argument("use_ours / use_4p4d solvers are not implemented in this build");
+}
+
+} // namespace
+
+void estimate_pair(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int device, Model *out,
+                   Stats *stats) {
+    validate(in, opts);
+    CtxLease lease(device);
+    Problem P = make_problem(in, opts, cfg);
+    Run r(*lease.c, P, opts, cfg);
+    r.run(out, stats);
+    if (in.variant == kSF) {
+        out->focal0 *= P.norm_scale;
+        out->focal1 = out->focal0;
+    } else if (in.variant == kTF) {
+        out->focal0 *= P.norm_scale;
+        out->focal1 *= P.norm_scale;
+    }
+}
+
+void score_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
+                  int nm, double *scores, double *errors, int device, double *norm_scale) {
+    validate(in, opts);
+    CtxLease lease(device);
+    DeviceCtx &X = *lease.c;
+    Problem P = make_problem(in, opts, cfg);
+    if (norm_scale) *norm_scale = P.norm_scale;
+    X.ensure(in.n, 64, max_models(in.variant));
+    PairData D;
+    upload_pair(X, P, &D);
+    std::vector<ScoreRec> recs(std::max(nm, 1));
+    for (int m = 0; m < nm; ++m) prepare_score_rec(P.C, models[m], recs[m]);
+    ScoreRec *d_recs = nullptr;
+    double *d_sc = nullptr;
+    MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * recs.size()));
+    MP_HIP(hipMalloc(&d_sc, sizeof(double) * recs.size()));
+    MP_HIP(hipMemcpyAsync(d_recs, recs.data(), sizeof(ScoreRec) * nm, hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_score_models(X.stream, D, P.C, d_recs, nm, d_sc));
+    MP_HIP(hipMemcpyAsync(scores, d_sc, sizeof(double) * nm, hipMemcpyDeviceToHost, X.stream));
+    if (errors) {
+        for (int m = 0; m < nm; ++m) {
+            MP_HIP(launch_sweep(X.stream, D, P.C, d_recs + m, X.d_err, X.d_score1));
+            MP_HIP(hipMemcpyAsync(errors + (size_t)m * 3 * in.n, X.d_err, sizeof(double) * 3 * in.n,
+                                  hipMemcpyDeviceToHost, X.stream));
+        }
+    }
+    MP_HIP(hipStreamSynchronize(X.stream));
+    hipFree(d_recs);
+    hipFree(d_sc);
+}
+
+int solve_md_direct(int variant, const double *x, const double *y, const double *dx, const double *dy, double *sols,
+                    int max_sols, Model *poses, int max_poses, int *nposes, int device) {
+    CtxLease lease(device);
+    DeviceCtx &X = *lease.c;
+    const int k = variant == kCal ? 3 : 4;
+    std::vector<double> in(8 * k);
+    std::memcpy(in.data(), x, sizeof(double) * 3 * k);
+    std::memcpy(in.data() + 3 * k, y, sizeof(double) * 3 * k);
+    std::memcpy(in.data() + 6 * k, dx, sizeof(double) * k);
+    std::memcpy(in.data() + 7 * k, dy, sizeof(double) * k);
+    double *d_in, *d_sols;
+    int *d_n;
+    Model *d_poses;
+    MP_HIP(hipMalloc(&d_in, sizeof(double) * in.size()));
+    MP_HIP(hipMalloc(&d_sols, sizeof(double) * 8 * 6));
+    MP_HIP(hipMalloc(&d_n, sizeof(int) * 2));
+    MP_HIP(hipMalloc(&d_poses, sizeof(Model) * 8));
+    MP_HIP(hipMemcpyAsync(d_in, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_md_direct(X.stream, variant, d_in, d_sols, d_n, d_poses, d_n + 1));
+    double hs[48];
+    int hn[2];
+    Model hp[8];
+    MP_HIP(hipMemcpyAsync(hs, d_sols, sizeof(hs), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(hn, d_n, sizeof(hn), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(hp, d_poses, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipStreamSynchronize(X.stream));
+    hipFree(d_in);
+    hipFree(d_sols);
+    hipFree(d_n);
+    hipFree(d_poses);
+    const int w = variant == kCal ? 4 : (variant == kSF ? 5 : 6);
+    for (int i = 0; i < std::min(hn[0], max_sols); ++i)
+        for (int c = 0; c < w; ++c) sols[i * w + c] = hs[i * w + c];
+    for (int i = 0; i < std::min(hn[1], max_poses); ++i) poses[i] = hp[i];
+    if (nposes) *nposes = hn[1];
+    return hn[0];
+}
+
+int solve_5pt_direct(const double *b1, const double *b2, Model *poses, int max_poses, int device) {
+    CtxLease lease(device);
+    DeviceCtx &X = *lease.c;
+    double in[30];
+    std::memcpy(in, b1, sizeof(double) * 15);
+    std::memcpy(in + 15, b2, sizeof(double) * 15);
+    double *d_in;
+    int *d_n;
+    Model *d_poses;
+    MP_HIP(hipMalloc(&d_in, sizeof(in)));
+    MP_HIP(hipMalloc(&d_n, sizeof(int)));
+    MP_HIP(hipMalloc(&d_poses, sizeof(Model) * kMaxModelsCal));
+    MP_HIP(hipMemcpyAsync(d_in, in, sizeof(in), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_5pt_direct(X.stream, d_in, d_poses, d_n));
+    int hn = 0;
+    Model hp[kMaxModelsCal];
+    MP_HIP(hipMemcpyAsync(&hn, d_n, sizeof(int), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(hp, d_poses, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipStreamSynchronize(X.stream));
+    hipFree(d_in);
+    hipFree(d_n);
+    hipFree(d_poses);
+    for (int i = 0; i < std::min(hn, max_poses); ++i) poses[i] = hp[i];
+    return hn;
+}
+
+int device_count() {
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess) return 0;
+    return cnt;
+}
+
+} // namespace mp

@@ -1,0 +1,70 @@
+// Host controller of the MI355X hybrid LO-MSAC estimator.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../include/mp_types.h"
+#include "lm.h"
+
+namespace mp {
+
+struct RansacOptions {
+    uint32_t min_num_iterations = 100, max_num_iterations = 10000, max_num_iterations_per_solver = 10000;
+    double success_probability = 0.99;
+    double squared_inlier_thresholds[2] = {1.0, 1.0};
+    double data_type_weights[2] = {1.0, 1.0};
+    uint32_t random_seed = 0;
+    int num_lo_steps = 10;
+    double threshold_multiplier = 1.4142135623730951;
+    int num_lsq_iterations = 4, min_sample_multiplicator = 7, non_min_sample_multiplier = 3;
+    int lo_starting_iterations = 50;
+    bool final_least_squares = false, use_ours = false, use_4p4d = false;
+};
+
+struct EstimatorConfig {
+    int solver_type = 0, score_type = 0, lo_type = 0;
+    bool min_depth_constraint = true, use_shift = true;
+    double ftol = 1e-6, gtol = 1e-8, ptol = 1e-6, max_iter = 25;
+};
+
+struct Stats {
+    uint32_t num_iterations_total = 0;
+    uint32_t num_iterations_per_solver[2] = {0, 0};
+    int best_num_inliers = 0;
+    int best_solver_type = -1;
+    double best_model_score = 0.0;
+    double inlier_ratios[3] = {0, 0, 0};
+    std::vector<int> inlier_indices[3];
+    int number_lo_iterations = 0;
+    uint64_t num_hypotheses = 0, num_lo_sweeps = 0;
+    int num_batches = 0;
+    double seconds_total = 0, seconds_lo = 0, seconds_gpu_wait = 0;
+};
+
+struct PairInput {
+    int variant = kCal;
+    int64_t n = 0;
+    const double *x0 = nullptr, *x1 = nullptr, *d0 = nullptr, *d1 = nullptr;
+    double min_depth[2] = {0, 0};
+    double cam0[9] = {0}, cam1[9] = {0}; // K (CAL) or principal point (SF/TF)
+};
+
+// Runs the full estimator on one pair on `device`; throws std::runtime_error on HIP
+// errors and std::invalid_argument on bad input.  The returned model is in user
+// units (SF/TF focals multiplied back by the normalisation scale).
+void estimate_pair(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int device, Model *out,
+                   Stats *stats);
+
+// Scores explicit models (problem units) on the device (mp_score_models).
+void score_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
+                  int nm, double *scores, double *errors, int device, double *norm_scale);
+
+// Standalone solvers on the device (mp_solve_* / mp_relpose_5pt).
+int solve_md_direct(int variant, const double *x, const double *y, const double *dx, const double *dy, double *sols,
+                    int max_sols, Model *poses, int max_poses, int *nposes, int device);
+int solve_5pt_direct(const double *b1, const double *b2, Model *poses, int max_poses, int device);
+
+int device_count();
+
+} // namespace mp

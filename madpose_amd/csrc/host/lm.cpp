@@ -1,0 +1,541 @@
+// Host LM for LO -- see lm.h.
+#include "lm.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace mp {
+
+namespace {
+
+enum Full { kD0 = 0, kD1, kD2, kT0, kT1, kT2, kS, kO0, kO1, kF0, kF1, kNFull };
+
+inline void skew(const double *v, double *S) {
+    S[0] = 0;
+    S[1] = -v[2];
+    S[2] = v[1];
+    S[3] = v[2];
+    S[4] = 0;
+    S[5] = -v[0];
+    S[6] = -v[1];
+    S[7] = v[0];
+    S[8] = 0;
+}
+inline void mm3(const double *A, const double *B, double *C) {
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) C[3 * r + c] = A[3 * r] * B[c] + A[3 * r + 1] * B[3 + c] + A[3 * r + 2] * B[6 + c];
+}
+inline void mv3(const double *A, const double *v, double *o) {
+    for (int r = 0; r < 3; ++r) o[r] = A[3 * r] * v[0] + A[3 * r + 1] * v[1] + A[3 * r + 2] * v[2];
+}
+inline void mtv3(const double *A, const double *v, double *o) { // A^T v
+    for (int r = 0; r < 3; ++r) o[r] = A[r] * v[0] + A[3 + r] * v[1] + A[6 + r] * v[2];
+}
+
+struct Params {
+    double q[4], R[9], t[3], s, o0, o1, f0, f1;
+};
+
+struct Ctx {
+    const HostPair *P;
+    const std::vector<int> *sample;
+    LMSettings S;
+    bool has_o0, has_s_o1;
+    int col[kNFull]; // full -> active column (-1 inactive)
+    int n;
+};
+
+// Accumulates one residual row r with full-layout gradient gfull into H, g, cost.
+inline void acc_row(const Ctx &C, double r, const double *gfull, double *H, double *g, double *cost) {
+    double j[kNFull];
+    int idx[kNFull], m = 0;
+    for (int k = 0; k < kNFull; ++k)
+        if (C.col[k] >= 0) {
+            idx[m] = C.col[k];
+            j[m] = gfull[k];
+            ++m;
+        }
+    *cost += 0.5 * r * r;
+    for (int a = 0; a < m; ++a) {
+        g[idx[a]] += j[a] * r;
+        for (int b = 0; b < m; ++b) H[idx[a] * C.n + idx[b]] += j[a] * j[b];
+    }
+}
+
+// Evaluates cost (and, when H != nullptr, normal equations) at parameters p.
+double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
+    const HostPair &P = *C.P;
+    const bool cal = P.variant == kCal;
+    const bool sf = P.variant == kSF;
+    const double f0 = p.f0, f1 = sf ? p.f0 : p.f1;
+    double cost = 0.0;
+    if (H) {
+        std::memset(H, 0, sizeof(double) * C.n * C.n);
+        std::memset(g, 0, sizeof(double) * C.n);
+    }
+    const double *R = p.R, *t = p.t;
+    if (C.S.use_reproj) {
+        // LiftProjectionFunctor0 and variants: x1_hat = K1 (R c0 (d0 + o0) + t)
+        for (int i : C.sample[0]) {
+            double c[3];
+            const double xh[3] = {P.x0[2 * i], P.x0[2 * i + 1], 1.0};
+            if (cal)
+                mv3(P.K0i, xh, c);
+            else {
+                c[0] = xh[0] / f0;
+                c[1] = xh[1] / f0;
+                c[2] = 1.0;
+            }
+            const double a = P.d0[i] + p.o0;
+            const double pp[3] = {c[0] * a, c[1] * a, c[2] * a};
+            double v[3], y[3], h[3];
+            mv3(R, pp, v);
+            for (int k = 0; k < 3; ++k) y[k] = v[k] + t[k];
+            if (cal)
+                mv3(P.K1, y, h);
+            else {
+                h[0] = f1 * y[0];
+                h[1] = f1 * y[1];
+                h[2] = y[2];
+            }
+            const double iz = 1.0 / h[2];
+            const double r0 = h[0] * iz - P.x1[2 * i], r1 = h[1] * iz - P.x1[2 * i + 1];
+            if (!H) {
+                cost += 0.5 * (r0 * r0 + r1 * r1);
+                continue;
+            }
+            // dr/dh
+            const double Dh[2][3] = {{iz, 0, -h[0] * iz * iz}, {0, iz, -h[1] * iz * iz}};
+            double G[2][3]; // dr/dy
+            for (int rr = 0; rr < 2; ++rr)
+                for (int k = 0; k < 3; ++k) {
+                    if (cal)
+                        G[rr][k] = Dh[rr][0] * P.K1[k] + Dh[rr][1] * P.K1[3 + k] + Dh[rr][2] * P.K1[6 + k];
+                    else
+                        G[rr][k] = Dh[rr][k] * (k < 2 ? f1 : 1.0);
+                }
+            double Sv[9];
+            skew(v, Sv);
+            double Rc[3];
+            mv3(R, c, Rc);
+            double dcf[3] = {0, 0, 0}, Rdcf[3] = {0, 0, 0};
+            if (!cal) {
+                dcf[0] = -xh[0] / (f0 * f0) * a;
+                dcf[1] = -xh[1] / (f0 * f0) * a;
+                mv3(R, dcf, Rdcf);
+            }
+            for (int rr = 0; rr < 2; ++rr) {
+                double gf[kNFull] = {0};
+                for (int k = 0; k < 3; ++k) {
+                    // dy/ddelta = -2 [v]x
+                    gf[kD0 + k] = -2.0 * (G[rr][0] * Sv[k] + G[rr][1] * Sv[3 + k] + G[rr][2] * Sv[6 + k]);
+                    gf[kT0 + k] = G[rr][k];
+                }
+                gf[kO0] = G[rr][0] * Rc[0] + G[rr][1] * Rc[1] + G[rr][2] * Rc[2];
+                if (!cal) {
+                    const double dyf0 = G[rr][0] * Rdcf[0] + G[rr][1] * Rdcf[1] + G[rr][2] * Rdcf[2];
+                    const double dhf1 = Dh[rr][0] * y[0] + Dh[rr][1] * y[1];
+                    if (sf)
+                        gf[kF0] = dyf0 + dhf1;
+                    else {
+                        gf[kF0] = dyf0;
+                        gf[kF1] = dhf1;
+                    }
+                }
+                acc_row(C, rr == 0 ? r0 : r1, gf, H, g, &cost);
+            }
+        }
+        // LiftProjectionFunctor1: x0_hat = K0 R^T (c1 (d1 + o1) s - t)
+        for (int i : C.sample[1]) {
+            double c[3];
+            const double xh[3] = {P.x1[2 * i], P.x1[2 * i + 1], 1.0};
+            if (cal)
+                mv3(P.K1i, xh, c);
+            else {
+                c[0] = xh[0] / f1;
+                c[1] = xh[1] / f1;
+                c[2] = 1.0;
+            }
+            const double dep = P.d1[i] + p.o1;
+            const double a = dep * p.s;
+            const double u[3] = {c[0] * a - t[0], c[1] * a - t[1], c[2] * a - t[2]};
+            double y[3], h[3];
+            mtv3(R, u, y);
+            if (cal)
+                mv3(P.K0, y, h);
+            else {
+                h[0] = f0 * y[0];
+                h[1] = f0 * y[1];
+                h[2] = y[2];
+            }
+            const double iz = 1.0 / h[2];
+            const double r0 = h[0] * iz - P.x0[2 * i], r1 = h[1] * iz - P.x0[2 * i + 1];
+            if (!H) {
+                cost += 0.5 * (r0 * r0 + r1 * r1);
+                continue;
+            }
+            const double Dh[2][3] = {{iz, 0, -h[0] * iz * iz}, {0, iz, -h[1] * iz * iz}};
+            double G[2][3];
+            for (int rr = 0; rr < 2; ++rr)
+                for (int k = 0; k < 3; ++k) {
+                    if (cal)
+                        G[rr][k] = Dh[rr][0] * P.K0[k] + Dh[rr][1] * P.K0[3 + k] + Dh[rr][2] * P.K0[6 + k];
+                    else
+                        G[rr][k] = Dh[rr][k] * (k < 2 ? f0 : 1.0);
+                }
+            // dy/ddelta = 2 R^T [u]x ; dy/dt = -R^T ; dy/ds = R^T c dep ; dy/do1 = R^T c s
+            double Su[9], RtSu[9];
+            skew(u, Su);
+            for (int r = 0; r < 3; ++r)
+                for (int cc = 0; cc < 3; ++cc)
+                    RtSu[3 * r + cc] = R[r] * Su[cc] + R[3 + r] * Su[3 + cc] + R[6 + r] * Su[6 + cc];
+            double Rtc[3];
+            mtv3(R, c, Rtc);
+            double Rtdcf[3] = {0, 0, 0};
+            if (!cal) {
+                const double dcf[3] = {-xh[0] / (f1 * f1) * a, -xh[1] / (f1 * f1) * a, 0.0};
+                mtv3(R, dcf, Rtdcf);
+            }
+            for (int rr = 0; rr < 2; ++rr) {
+                double gf[kNFull] = {0};
+                for (int k = 0; k < 3; ++k) {
+                    gf[kD0 + k] =
+                        2.0 * (G[rr][0] * RtSu[k] + G[rr][1] * RtSu[3 + k] + G[rr][2] * RtSu[6 + k]);
+                    gf[kT0 + k] = -(G[rr][0] * R[3 * k] + G[rr][1] * R[3 * k + 1] + G[rr][2] * R[3 * k + 2]);
+                }
+                const double gRtc = G[rr][0] * Rtc[0] + G[rr][1] * Rtc[1] + G[rr][2] * Rtc[2];
+                gf[kS] = gRtc * dep;
+                gf[kO1] = gRtc * p.s;
+                if (!cal) {
+                    const double dyf1 = G[rr][0] * Rtdcf[0] + G[rr][1] * Rtdcf[1] + G[rr][2] * Rtdcf[2];
+                    const double dhf0 = Dh[rr][0] * y[0] + Dh[rr][1] * y[1];
+                    if (sf)
+                        gf[kF0] = dyf1 + dhf0;
+                    else {
+                        gf[kF0] = dhf0;
+                        gf[kF1] = dyf1;
+                    }
+                }
+                acc_row(C, rr == 0 ? r0 : r1, gf, H, g, &cost);
+            }
+        }
+    }
+    if (C.S.use_sampson) {
+        // SampsonError*Functor: r = w C / |(e0, e1, g0, g1)|
+        double Tx[9], E[9];
+        skew(t, Tx);
+        mm3(Tx, R, E);
+        double s0[3] = {1, 1, 1}, s1[3] = {1, 1, 1};
+        if (!cal) {
+            s0[0] = s0[1] = 1.0 / f0;
+            s1[0] = s1[1] = 1.0 / f1;
+        }
+        double F[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) F[3 * r + c] = E[3 * r + c] * s1[r] * s0[c];
+        // derivative building blocks: dE/dt_k = [e_k]x R, dE/ddelta_k = 2 [t]x [e_k]x R
+        double dEt[3][9], dEd[3][9];
+        if (H) {
+            for (int k = 0; k < 3; ++k) {
+                double ek[3] = {0, 0, 0};
+                ek[k] = 1.0;
+                double Sk[9];
+                skew(ek, Sk);
+                mm3(Sk, R, dEt[k]);
+                mm3(Tx, dEt[k], dEd[k]);
+                for (int e = 0; e < 9; ++e) dEd[k][e] *= 2.0;
+            }
+        }
+        for (int i : C.sample[2]) {
+            double a[3], b[3];
+            if (cal) {
+                const double xa[3] = {P.x0[2 * i], P.x0[2 * i + 1], 1.0}, xb[3] = {P.x1[2 * i], P.x1[2 * i + 1], 1.0};
+                mv3(P.K0i, xa, a);
+                mv3(P.K1i, xb, b);
+            } else {
+                a[0] = P.x0[2 * i];
+                a[1] = P.x0[2 * i + 1];
+                b[0] = P.x1[2 * i];
+                b[1] = P.x1[2 * i + 1];
+            }
+            a[2] = b[2] = 1.0; // the functor uses the first two coordinates and an implicit 1
+            const double e0 = F[0] * a[0] + F[1] * a[1] + F[2];
+            const double e1 = F[3] * a[0] + F[4] * a[1] + F[5];
+            const double e2 = F[6] * a[0] + F[7] * a[1] + F[8];
+            const double g0 = F[0] * b[0] + F[3] * b[1] + F[6];
+            const double g1 = F[1] * b[0] + F[4] * b[1] + F[7];
+            const double Cc = b[0] * e0 + b[1] * e1 + e2;
+            const double D = e0 * e0 + e1 * e1 + g0 * g0 + g1 * g1;
+            const double sD = std::sqrt(D);
+            const double r = C.S.w_sampson * Cc / sD;
+            if (!H) {
+                cost += 0.5 * r * r;
+                continue;
+            }
+            const double ev[3] = {e0, e1, e2}, gv[3] = {g0, g1, 0.0};
+            double W[9]; // dr/dF
+            const double k1 = C.S.w_sampson / sD, k2 = C.S.w_sampson * Cc / (D * sD);
+            for (int ii = 0; ii < 3; ++ii)
+                for (int jj = 0; jj < 3; ++jj) {
+                    const double dD = (ii < 2 ? ev[ii] * a[jj] : 0.0) + (jj < 2 ? gv[jj] * b[ii] : 0.0);
+                    W[3 * ii + jj] = k1 * b[ii] * a[jj] - k2 * dD;
+                }
+            double WE[9]; // dr/dE
+            for (int ii = 0; ii < 3; ++ii)
+                for (int jj = 0; jj < 3; ++jj) WE[3 * ii + jj] = W[3 * ii + jj] * s1[ii] * s0[jj];
+            double gf[kNFull] = {0};
+            for (int k = 0; k < 3; ++k) {
+                double dt = 0, dd = 0;
+                for (int e = 0; e < 9; ++e) {
+                    dt += WE[e] * dEt[k][e];
+                    dd += WE[e] * dEd[k][e];
+                }
+                gf[kT0 + k] = dt;
+                gf[kD0 + k] = dd;
+            }
+            if (!cal) {
+                const double ds0[3] = {-1.0 / (f0 * f0), -1.0 / (f0 * f0), 0.0};
+                const double ds1[3] = {-1.0 / (f1 * f1), -1.0 / (f1 * f1), 0.0};
+                double df0 = 0, df1 = 0;
+                for (int ii = 0; ii < 3; ++ii)
+                    for (int jj = 0; jj < 3; ++jj) {
+                        df0 += W[3 * ii + jj] * E[3 * ii + jj] * s1[ii] * ds0[jj];
+                        df1 += W[3 * ii + jj] * E[3 * ii + jj] * ds1[ii] * s0[jj];
+                    }
+                if (sf)
+                    gf[kF0] = df0 + df1;
+                else {
+                    gf[kF0] = df0;
+                    gf[kF1] = df1;
+                }
+            }
+            acc_row(C, r, gf, H, g, &cost);
+        }
+    }
+    return cost;
+}
+
+bool chol_solve(std::vector<double> A, int n, std::vector<double> b, std::vector<double> *x) {
+    for (int j = 0; j < n; ++j) {
+        double d = A[j * n + j];
+        for (int k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
+        if (!(d > 0)) return false;
+        d = std::sqrt(d);
+        A[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double s = A[i * n + j];
+            for (int k = 0; k < j; ++k) s -= A[i * n + k] * A[j * n + k];
+            A[i * n + j] = s / d;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= A[i * n + k] * b[k];
+        b[i] = s / A[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = b[i];
+        for (int k = i + 1; k < n; ++k) s -= A[k * n + i] * b[k];
+        b[i] = s / A[i * n + i];
+    }
+    *x = b;
+    return true;
+}
+
+void set_rotation(Params &p) { quat_to_rot(p.q, p.R); }
+
+} // namespace
+
+void rot_to_quat(const double *R, double *q) {
+    const double tr = R[0] + R[4] + R[8];
+    if (tr > 0) {
+        double s = std::sqrt(tr + 1.0);
+        q[0] = 0.5 * s;
+        s = 0.5 / s;
+        q[1] = (R[7] - R[5]) * s;
+        q[2] = (R[2] - R[6]) * s;
+        q[3] = (R[3] - R[1]) * s;
+    } else {
+        int i = 0;
+        if (R[4] > R[0]) i = 1;
+        if (R[8] > R[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double s = std::sqrt(R[4 * i] - R[4 * j] - R[4 * k] + 1.0);
+        double v[3];
+        v[i] = 0.5 * s;
+        s = 0.5 / s;
+        q[0] = (R[3 * k + j] - R[3 * j + k]) * s;
+        v[j] = (R[3 * j + i] + R[3 * i + j]) * s;
+        v[k] = (R[3 * k + i] + R[3 * i + k]) * s;
+        q[1] = v[0];
+        q[2] = v[1];
+        q[3] = v[2];
+    }
+}
+
+void quat_to_rot(const double *q0, double *R) {
+    const double n = std::sqrt(q0[0] * q0[0] + q0[1] * q0[1] + q0[2] * q0[2] + q0[3] * q0[3]);
+    const double w = q0[0] / n, x = q0[1] / n, y = q0[2] / n, z = q0[3] / n;
+    R[0] = 1 - 2 * (y * y + z * z);
+    R[1] = 2 * (x * y - w * z);
+    R[2] = 2 * (x * z + w * y);
+    R[3] = 2 * (x * y + w * z);
+    R[4] = 1 - 2 * (x * x + z * z);
+    R[5] = 2 * (y * z - w * x);
+    R[6] = 2 * (x * z - w * y);
+    R[7] = 2 * (y * z + w * x);
+    R[8] = 1 - 2 * (x * x + y * y);
+}
+
+bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettings &S, Model *m) {
+    Ctx C;
+    C.P = &P;
+    C.sample = sample;
+    C.S = S;
+    size_t nres = 0;
+    if (S.use_reproj) nres += sample[0].size() + sample[1].size();
+    if (S.use_sampson) nres += sample[2].size();
+    if (nres == 0) return false;
+    C.has_o0 = S.use_reproj && !sample[0].empty();
+    C.has_s_o1 = S.use_reproj && !sample[1].empty();
+    for (int k = 0; k < kNFull; ++k) C.col[k] = -1;
+    int n = 0;
+    for (int k = 0; k < 6; ++k) C.col[k] = n++;
+    bool has_lo[kNFull] = {false};
+    double lo[kNFull] = {0};
+    if (C.has_s_o1) {
+        C.col[kS] = n++;
+        has_lo[kS] = true;
+        lo[kS] = 1e-2;
+    }
+    if (C.has_o0 && S.use_shift) C.col[kO0] = n++;
+    if (C.has_s_o1 && S.use_shift) C.col[kO1] = n++;
+    if (S.min_depth_constraint) {
+        has_lo[kO0] = has_lo[kO1] = true;
+        lo[kO0] = -P.min_depth[0] + 1e-2;
+        lo[kO1] = -P.min_depth[1] + 1e-2;
+    }
+    if (P.variant == kSF) C.col[kF0] = n++;
+    if (P.variant == kTF) {
+        C.col[kF0] = n++;
+        C.col[kF1] = n++;
+        has_lo[kF0] = has_lo[kF1] = true;
+        lo[kF0] = lo[kF1] = 1e-6;
+    }
+    C.n = n;
+    Params x;
+    rot_to_quat(m->R, x.q);
+    set_rotation(x);
+    std::memcpy(x.t, m->t, sizeof(x.t));
+    x.s = m->scale;
+    x.o0 = m->offset0;
+    x.o1 = m->offset1;
+    x.f0 = m->focal0;
+    x.f1 = m->focal1;
+    // constant bounded blocks must start feasible (Ceres Program::IsFeasible)
+    if (!S.use_shift && S.min_depth_constraint) {
+        if (C.has_o0 && x.o0 < lo[kO0]) return true;
+        if (C.has_s_o1 && x.o1 < lo[kO1]) return true;
+    }
+    auto amb_norm2 = [](const Params &p) {
+        return p.q[0] * p.q[0] + p.q[1] * p.q[1] + p.q[2] * p.q[2] + p.q[3] * p.q[3] + p.t[0] * p.t[0] +
+               p.t[1] * p.t[1] + p.t[2] * p.t[2] + p.s * p.s + p.o0 * p.o0 + p.o1 * p.o1 + p.f0 * p.f0 + p.f1 * p.f1;
+    };
+    std::vector<double> H(n * n), g(n);
+    double cost = evaluate(C, x, H.data(), g.data());
+    auto gmax = [&]() {
+        double v = 0;
+        for (double e : g) v = std::max(v, std::fabs(e));
+        return v;
+    };
+    double radius = 1e4, decrease = 2.0;
+    if (!(gmax() <= S.gtol)) {
+        for (int iter = 0; iter < S.max_iter; ++iter) {
+            std::vector<double> sc(n), A(n * n), rhs(n), y;
+            for (int j = 0; j < n; ++j) sc[j] = 1.0 / (1.0 + std::sqrt(H[j * n + j]));
+            for (int a = 0; a < n; ++a) {
+                rhs[a] = -g[a] * sc[a];
+                for (int b = 0; b < n; ++b) A[a * n + b] = H[a * n + b] * sc[a] * sc[b];
+            }
+            for (int j = 0; j < n; ++j) {
+                const double dg = std::min(std::max(A[j * n + j], 1e-6), 1e32);
+                A[j * n + j] += dg / radius;
+            }
+            if (!chol_solve(A, n, rhs, &y)) {
+                radius /= decrease;
+                decrease *= 2.0;
+                if (radius < 1e-32) break;
+                continue;
+            }
+            std::vector<double> d(n);
+            for (int j = 0; j < n; ++j) d[j] = y[j] * sc[j];
+            // candidate = Plus(x, d), projected onto the bounds
+            Params c = x;
+            {
+                const double dv[3] = {d[0], d[1], d[2]};
+                const double nd = std::sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+                if (nd > 0) {
+                    const double sn = std::sin(nd) / nd;
+                    const double qd[4] = {std::cos(nd), sn * dv[0], sn * dv[1], sn * dv[2]};
+                    const double *q = x.q;
+                    c.q[0] = qd[0] * q[0] - qd[1] * q[1] - qd[2] * q[2] - qd[3] * q[3];
+                    c.q[1] = qd[0] * q[1] + qd[1] * q[0] + qd[2] * q[3] - qd[3] * q[2];
+                    c.q[2] = qd[0] * q[2] - qd[1] * q[3] + qd[2] * q[0] + qd[3] * q[1];
+                    c.q[3] = qd[0] * q[3] + qd[1] * q[2] - qd[2] * q[1] + qd[3] * q[0];
+                }
+                for (int k = 0; k < 3; ++k) c.t[k] = x.t[k] + d[3 + k];
+                auto upd = [&](int slot, double &v) {
+                    if (C.col[slot] < 0) return;
+                    v += d[C.col[slot]];
+                    if (has_lo[slot] && v < lo[slot]) v = lo[slot];
+                };
+                upd(kS, c.s);
+                upd(kO0, c.o0);
+                upd(kO1, c.o1);
+                upd(kF0, c.f0);
+                upd(kF1, c.f1);
+                set_rotation(c);
+            }
+            double step2 = 0;
+            {
+                const double dd[12] = {c.q[0] - x.q[0], c.q[1] - x.q[1], c.q[2] - x.q[2], c.q[3] - x.q[3],
+                                       c.t[0] - x.t[0], c.t[1] - x.t[1], c.t[2] - x.t[2], c.s - x.s,
+                                       c.o0 - x.o0,     c.o1 - x.o1,     c.f0 - x.f0,     c.f1 - x.f1};
+                for (double e : dd) step2 += e * e;
+            }
+            const double step_norm = std::sqrt(step2), xnorm = std::sqrt(amb_norm2(x));
+            const double cand_cost = evaluate(C, c, nullptr, nullptr);
+            if (step_norm <= S.ptol * (xnorm + S.ptol)) break;
+            if (std::fabs(cost - cand_cost) <= S.ftol * cost) break;
+            double gd = 0, jd2 = 0;
+            for (int a = 0; a < n; ++a) {
+                gd += g[a] * d[a];
+                for (int b = 0; b < n; ++b) jd2 += d[a] * H[a * n + b] * d[b];
+            }
+            const double mcc = -(gd + 0.5 * jd2);
+            const double rho = (mcc > 0 && std::isfinite(cand_cost)) ? (cost - cand_cost) / mcc : -1.0;
+            if (rho > 1e-3) {
+                x = c;
+                cost = evaluate(C, x, H.data(), g.data());
+                radius = std::min(1e16, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3)));
+                decrease = 2.0;
+                if (gmax() <= S.gtol) break;
+            } else {
+                radius /= decrease;
+                decrease *= 2.0;
+                if (radius < 1e-32) break;
+            }
+        }
+    }
+    quat_to_rot(x.q, m->R);
+    std::memcpy(m->t, x.t, sizeof(x.t));
+    m->scale = x.s;
+    m->offset0 = x.o0;
+    m->offset1 = x.o1;
+    m->focal0 = x.f0;
+    m->focal1 = (P.variant == kSF) ? x.f0 : x.f1;
+    return true;
+}
+
+} // namespace mp

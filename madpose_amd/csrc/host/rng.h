@@ -1,0 +1,126 @@
+// Random streams of the reference's RANSAC loop, restated so they do not depend on
+// the host toolchain's libstdc++ version:
+//   * MT19937 (Matsumoto & Nishimura 1998), default seeding of std::mt19937;
+//   * uniform_int_distribution<int>(a, b) as implemented by GCC >= 11 for a 32-bit
+//     engine: Lemire's nearly-divisionless downscaling ("_S_nd");
+//   * uniform_real_distribution<double>(a, b) = a + (b - a) * generate_canonical<double,53>
+//     with two 32-bit draws: (g1 + g2 * 2^32) / 2^64, clamped below 1.
+// tests/test_rng.py pins all three against tests/golden/rng_gcc11.json, which was
+// produced with this container's g++ 11.4 (std::mt19937 + std distributions), i.e.
+// the streams the reference consumes in src/hybrid_ransac.h:64,79-80,226-229.
+#pragma once
+#include <cmath>
+#include <cstdint>
+
+namespace mp {
+
+class Mt19937 {
+  public:
+    explicit Mt19937(uint32_t seed = 5489u) { seed_with(seed); }
+    void seed_with(uint32_t seed) {
+        mt_[0] = seed;
+        for (int i = 1; i < 624; ++i) mt_[i] = 1812433253u * (mt_[i - 1] ^ (mt_[i - 1] >> 30)) + (uint32_t)i;
+        idx_ = 624;
+    }
+    uint32_t operator()() {
+        if (idx_ >= 624) twist();
+        uint32_t y = mt_[idx_++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+
+  private:
+    void twist() {
+        for (int i = 0; i < 624; ++i) {
+            const uint32_t y = (mt_[i] & 0x80000000u) | (mt_[(i + 1) % 624] & 0x7fffffffu);
+            mt_[i] = mt_[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        idx_ = 0;
+    }
+    uint32_t mt_[624];
+    int idx_;
+};
+
+// uniform integer in [a, b]
+inline int uniform_int(Mt19937 &g, int a, int b) {
+    const uint32_t urange = (uint32_t)b - (uint32_t)a;
+    if (urange == 0xffffffffu) return (int)((uint32_t)a + g());
+    const uint32_t range = urange + 1u;
+    uint64_t product = (uint64_t)g() * (uint64_t)range;
+    uint32_t low = (uint32_t)product;
+    if (low < range) {
+        const uint32_t threshold = (uint32_t)(-range) % range;
+        while (low < threshold) {
+            product = (uint64_t)g() * (uint64_t)range;
+            low = (uint32_t)product;
+        }
+    }
+    return (int)((uint32_t)a + (uint32_t)(product >> 32));
+}
+
+// uniform real in [a, b)
+inline double uniform_real(Mt19937 &g, double a, double b) {
+    const double r = 4294967296.0; // 2^32
+    double sum = (double)g();
+    sum += (double)g() * r;
+    double c = sum / (r * r);
+    if (c >= 1.0) c = std::nextafter(1.0, 0.0);
+    return (b - a) * c + a;
+}
+
+// The per-iteration random decisions of HybridLOMSAC::EstimateModel:
+// SelectMinimalSolver (src/hybrid_ransac.h:210-243, selection/LO stream `sel`) then
+// HybridUniformSampling::Sample (RansacLib, sampler stream `samp`): for each data
+// type t, ss[s][t] distinct draws of uniform_int(0, n-1), redrawing duplicates.
+// Only the indices of the type the solver consumes are kept (type 0 for the MD
+// solver, type 2 for the point solver); the type-1 draws of an MD iteration are
+// consumed and discarded exactly as in the reference.
+struct IterationStream {
+    Mt19937 sel, samp;
+    double prior[2] = {1.0, 1.0};
+    int ss[2][3] = {{3, 3, 0}, {0, 0, 5}};
+    int n = 0;
+
+    void seed(uint32_t s) {
+        sel.seed_with(s);
+        samp.seed_with(s);
+    }
+    int next(int *idx) {
+        const double u = uniform_real(sel, 0.0, prior[0] + prior[1]);
+        int st = -1;
+        double acc = 0.0;
+        for (int s = 0; s < 2; ++s) {
+            if (prior[s] == 0.0) continue;
+            acc += prior[s];
+            if (u <= acc) {
+                st = s;
+                break;
+            }
+        }
+        if (st < 0) st = prior[1] > 0 ? 1 : 0; // unreachable: u < prior sum
+        int tmp[8];
+        for (int t = 0; t < 3; ++t) {
+            const int k = ss[st][t];
+            for (int i = 0; i < k; ++i) {
+                bool dup = true;
+                while (dup) {
+                    tmp[i] = uniform_int(samp, 0, n - 1);
+                    dup = false;
+                    for (int j = 0; j < i; ++j)
+                        if (tmp[j] == tmp[i]) {
+                            dup = true;
+                            break;
+                        }
+                }
+            }
+            if ((st == 0 && t == 0) || (st == 1 && t == 2))
+                for (int j = 0; j < k; ++j) idx[j] = tmp[j];
+        }
+        return st;
+    }
+};
+
+} // namespace mp

@@ -1,0 +1,444 @@
+// Register-resident small dense math for the per-sample solvers.
+// Everything here is fixed-size and fully unrollable so hipcc keeps it in VGPRs
+// (no dynamically indexed private arrays -> no scratch traffic).
+#pragma once
+#include <cmath>
+
+#include "mp_types.h"
+
+namespace mp {
+
+MP_HD double sq(double x) { return x * x; }
+
+MP_HD void cross3(const double *a, const double *b, double *c) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+MP_HD double dot3(const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+MP_HD void matmul3(const double *A, const double *B, double *C) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) C[3 * r + c] = A[3 * r] * B[c] + A[3 * r + 1] * B[3 + c] + A[3 * r + 2] * B[6 + c];
+}
+MP_HD void matvec3(const double *A, const double *v, double *o) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) o[r] = A[3 * r] * v[0] + A[3 * r + 1] * v[1] + A[3 * r + 2] * v[2];
+}
+
+// PoseLib check_cheirality (src/solver.cpp:1188-1206); x1, x2 unit vectors
+MP_HD bool check_cheirality(const double *R, const double *t, const double *x1, const double *x2, double min_depth) {
+    double Rx1[3];
+    matvec3(R, x1, Rx1);
+    const double a = -dot3(Rx1, x2);
+    const double b1 = -dot3(Rx1, t);
+    const double b2 = dot3(x2, t);
+    const double l1 = b1 - a * b2;
+    const double l2 = -a * b1 + b2;
+    min_depth = min_depth * (1 - a * a);
+    return l1 > min_depth && l2 > min_depth;
+}
+
+// Solve A X = B (N x N, N x M) in place by Gaussian elimination with partial
+// pivoting.  Row exchanges are done with predicated selects so all indices are
+// compile-time constants.  Returns false on a zero pivot.
+template <int N, int M> MP_HD bool gauss_solve(double (&A)[N][N], double (&B)[N][M]) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        // pivot search
+        int p = k;
+        double best = fabs(A[k][k]);
+#pragma unroll
+        for (int r = k + 1; r < N; ++r) {
+            double v = fabs(A[r][k]);
+            if (v > best) {
+                best = v;
+                p = r;
+            }
+        }
+#pragma unroll
+        for (int r = k + 1; r < N; ++r) {
+            if (r == p) {
+#pragma unroll
+                for (int c = 0; c < N; ++c) {
+                    double t = A[k][c];
+                    A[k][c] = A[r][c];
+                    A[r][c] = t;
+                }
+#pragma unroll
+                for (int c = 0; c < M; ++c) {
+                    double t = B[k][c];
+                    B[k][c] = B[r][c];
+                    B[r][c] = t;
+                }
+            }
+        }
+        if (best == 0.0) ok = false;
+        const double inv = 1.0 / A[k][k];
+#pragma unroll
+        for (int r = k + 1; r < N; ++r) {
+            const double l = A[r][k] * inv;
+#pragma unroll
+            for (int c = k + 1; c < N; ++c) A[r][c] -= l * A[k][c];
+#pragma unroll
+            for (int c = 0; c < M; ++c) B[r][c] -= l * B[k][c];
+        }
+    }
+    // back substitution
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) {
+        const double inv = 1.0 / A[k][k];
+#pragma unroll
+        for (int c = 0; c < M; ++c) {
+            double s = B[k][c];
+#pragma unroll
+            for (int j = k + 1; j < N; ++j) s -= A[k][j] * B[j][c];
+            B[k][c] = s * inv;
+        }
+    }
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// Real roots of a univariate polynomial by Sturm sequences (root isolation by
+// bisection of sign-change counts, then safeguarded Newton/bisection refinement).
+// c: ascending coefficients of degree N (c[N] != 0 expected).  Returns the number
+// of roots written to roots[] in ascending order.
+template <int N> struct SturmChain {
+    double s[N + 1][N + 1]; // poly k has degree N-k (ascending coefficients)
+    int len;
+};
+
+template <int N> MP_HD double horner(const double (&p)[N + 1], int deg, double x) {
+    double v = 0.0;
+#pragma unroll
+    for (int j = N; j >= 0; --j)
+        if (j <= deg) v = v * x + p[j];
+    return v;
+}
+
+template <int N> MP_HD void sturm_build(const double *c, SturmChain<N> &S) {
+    double mx = 0.0;
+#pragma unroll
+    for (int j = 0; j <= N; ++j) mx = fmax(mx, fabs(c[j]));
+    const double sc0 = mx > 0 ? 1.0 / mx : 1.0;
+#pragma unroll
+    for (int j = 0; j <= N; ++j) {
+        S.s[0][j] = c[j] * sc0;
+        S.s[1][j] = 0.0;
+    }
+    // derivative (positive scaling)
+    mx = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        S.s[1][j] = (j + 1) * S.s[0][j + 1];
+        mx = fmax(mx, fabs(S.s[1][j]));
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) S.s[1][j] /= mx;
+    S.len = 2;
+    bool alive = true;
+#pragma unroll
+    for (int k = 1; k < N; ++k) {
+        // a = s[k-1] (deg d+1), b = s[k] (deg d), d = N-k;  next = -(a mod b)
+        const int d = N - k;
+        double nxt[N + 1];
+#pragma unroll
+        for (int j = 0; j <= N; ++j) nxt[j] = 0.0;
+        const double bd = S.s[k][d];
+        double bmax = 0.0;
+#pragma unroll
+        for (int j = 0; j <= d; ++j) bmax = fmax(bmax, fabs(S.s[k][j]));
+        if (!(fabs(bd) > 1e-14 * bmax)) alive = false;
+        if (alive) {
+            const double q1 = S.s[k - 1][d + 1] / bd;
+            const double q0 = (S.s[k - 1][d] - q1 * S.s[k][d - 1]) / bd;
+            double rmax = 0.0;
+#pragma unroll
+            for (int j = 0; j < d; ++j) {
+                double bm1 = (j > 0) ? S.s[k][j - 1] : 0.0;
+                nxt[j] = -(S.s[k - 1][j] - q1 * bm1 - q0 * S.s[k][j]);
+                rmax = fmax(rmax, fabs(nxt[j]));
+            }
+            double amax = 0.0;
+#pragma unroll
+            for (int j = 0; j <= d + 1; ++j) amax = fmax(amax, fabs(S.s[k - 1][j]));
+            if (!(rmax > 1e-15 * amax)) {
+                alive = false; // exact division: gcd found (multiple roots); chain ends here
+            } else {
+#pragma unroll
+                for (int j = 0; j < d; ++j) S.s[k + 1][j] = nxt[j] / rmax;
+#pragma unroll
+                for (int j = d; j <= N; ++j) S.s[k + 1][j] = 0.0;
+                S.len = k + 2;
+            }
+        }
+    }
+}
+
+// number of sign changes of the chain at x
+template <int N> MP_HD int sturm_count(const SturmChain<N> &S, double x) {
+    int changes = 0;
+    double prev = 0.0;
+#pragma unroll
+    for (int k = 0; k <= N; ++k) {
+        if (k < S.len) {
+            double v = 0.0;
+#pragma unroll
+            for (int j = N - k; j >= 0; --j) v = v * x + S.s[k][j];
+            if (v != 0.0) {
+                if (prev != 0.0 && ((v < 0) != (prev < 0))) ++changes;
+                prev = v;
+            }
+        }
+    }
+    return changes;
+}
+
+template <int N> MP_HD double refine_root(const double *c, double lo, double hi) {
+    double flo = 0.0, fhi = 0.0;
+    for (int j = N; j >= 0; --j) {
+        flo = flo * lo + c[j];
+        fhi = fhi * hi + c[j];
+    }
+    if (flo == 0.0) return lo;
+    if (fhi == 0.0) return hi;
+    if ((flo < 0) == (fhi < 0)) return 0.5 * (lo + hi); // even multiplicity: midpoint
+    double x = 0.5 * (lo + hi);
+    for (int it = 0; it < 100; ++it) {
+        double f = 0.0, df = 0.0;
+        for (int j = N; j >= 0; --j) {
+            df = df * x + f;
+            f = f * x + c[j];
+        }
+        if (f == 0.0) return x;
+        if ((f < 0) == (flo < 0))
+            lo = x;
+        else
+            hi = x;
+        double xn = x - f / df;
+        if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
+        if (fabs(xn - x) <= 1e-16 * fabs(xn) || hi - lo <= 1e-16 * fmax(fabs(lo), fabs(hi))) return xn;
+        x = xn;
+    }
+    return x;
+}
+
+template <int N> MP_HD int sturm_real_roots(const double *c_in, double *roots) {
+    // trim leading zeros is the caller's job; normalise to avoid overflow
+    double c[N + 1], cs[N + 1];
+    double mx = 0.0;
+    for (int j = 0; j <= N; ++j) mx = fmax(mx, fabs(c_in[j]));
+    if (!(mx > 0.0) || !(fabs(c_in[N]) > 1e-300)) return 0;
+    for (int j = 0; j <= N; ++j) c[j] = c_in[j] / c_in[N]; // monic
+    // rescale x = sigma * y so the roots are O(1) (Fujiwara-type root-size estimate);
+    // the chain is built and bisected on the scaled polynomial, roots are refined on c.
+    double sigma = 0.0;
+    for (int j = 0; j < N; ++j)
+        if (c[j] != 0.0) sigma = fmax(sigma, pow(fabs(c[j]), 1.0 / (N - j)));
+    if (!(sigma > 0.0) || !(sigma < 1e300)) sigma = 1.0;
+    {
+        double p = 1.0;
+        for (int j = 0; j <= N; ++j) {
+            cs[j] = c[j] * p / pow(sigma, (double)N);
+            p *= sigma;
+        }
+        cs[N] = 1.0;
+    }
+    const double B = 3.0; // all roots of the scaled monic polynomial satisfy |y| <= 2
+    SturmChain<N> S;
+    sturm_build<N>(cs, S);
+    // Isolation: keep walking down the lower half of the current interval and park
+    // the upper halves that still hold roots.  Parked intervals are disjoint and each
+    // holds >= 1 root, so at most N are pending; output is ascending.
+    double st_lo[N + 1], st_hi[N + 1];
+    int st_clo[N + 1], st_chi[N + 1];
+    int sp = 1, nr = 0;
+    st_lo[0] = -B;
+    st_hi[0] = B;
+    st_clo[0] = sturm_count<N>(S, -B);
+    st_chi[0] = sturm_count<N>(S, B);
+    while (sp > 0) {
+        --sp;
+        double lo = st_lo[sp], hi = st_hi[sp];
+        int clo = st_clo[sp], chi = st_chi[sp];
+        for (int depth = 0; depth < 200; ++depth) {
+            const int k = clo - chi;
+            if (k <= 0) break;
+            if (k == 1 || hi - lo <= 1e-14 * fmax(1.0, fmax(fabs(lo), fabs(hi)))) {
+                if (nr < N) roots[nr++] = refine_root<N>(c, sigma * lo, sigma * hi);
+                break;
+            }
+            const double mid = 0.5 * (lo + hi);
+            const int cm = sturm_count<N>(S, mid);
+            if (cm - chi > 0 && sp <= N) {
+                st_lo[sp] = mid;
+                st_hi[sp] = hi;
+                st_clo[sp] = cm;
+                st_chi[sp] = chi;
+                ++sp;
+            }
+            hi = mid;
+            chi = cm;
+        }
+    }
+    return nr;
+}
+
+// ---------------------------------------------------------------------------
+// Cyclic Jacobi eigen-decomposition of a symmetric 4x4 matrix (in place, A becomes
+// diagonal, V accumulates eigenvectors as columns).
+MP_HD void jacobi_eig4(double (&A)[4][4], double (&V)[4][4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 12; ++sweep) {
+        double off = 0.0, dn = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            dn += A[i][i] * A[i][i];
+#pragma unroll
+            for (int j = i + 1; j < 4; ++j) off += A[i][j] * A[i][j];
+        }
+        if (!(off > 1e-32 * dn)) break;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int q = p + 1; q < 4; ++q) {
+                const double apq = A[p][q];
+                if (apq != 0.0) {
+                    const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+                    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const double akp = A[k][p], akq = A[k][q];
+                        A[k][p] = c * akp - s * akq;
+                        A[k][q] = s * akp + c * akq;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const double apk = A[p][k], aqk = A[q][k];
+                        A[p][k] = c * apk - s * aqk;
+                        A[q][k] = s * apk + c * aqk;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const double vkp = V[k][p], vkq = V[k][q];
+                        V[k][p] = c * vkp - s * vkq;
+                        V[k][q] = s * vkp + c * vkq;
+                    }
+                }
+            }
+    }
+}
+
+// Rotation minimising sum |Y_i - R X_i|^2 for centred point sets, via Horn's
+// unit-quaternion method: q = dominant eigenvector of the 4x4 matrix built from
+// M = sum X_i Y_i^T.  Equivalent to the SVD (Kabsch) solution with the det fix
+// used by the reference (src/solver.cpp:515-525).
+MP_HD void horn_rotation(const double (&M)[3][3], double *R) {
+    const double Sxx = M[0][0], Sxy = M[0][1], Sxz = M[0][2];
+    const double Syx = M[1][0], Syy = M[1][1], Syz = M[1][2];
+    const double Szx = M[2][0], Szy = M[2][1], Szz = M[2][2];
+    double N[4][4] = {{Sxx + Syy + Szz, Syz - Szy, Szx - Sxz, Sxy - Syx},
+                      {Syz - Szy, Sxx - Syy - Szz, Sxy + Syx, Szx + Sxz},
+                      {Szx - Sxz, Sxy + Syx, -Sxx + Syy - Szz, Syz + Szy},
+                      {Sxy - Syx, Szx + Sxz, Syz + Szy, -Sxx - Syy + Szz}};
+    double V[4][4];
+    jacobi_eig4(N, V);
+    int best = 0;
+    double bv = N[0][0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if (N[i][i] > bv) {
+            bv = N[i][i];
+            best = i;
+        }
+    double q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double v = V[i][0];
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+            if (best == j) v = V[i][j];
+        q[i] = v;
+    }
+    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double w = q[0] / n, x = q[1] / n, y = q[2] / n, z = q[3] / n;
+    R[0] = 1 - 2 * (y * y + z * z);
+    R[1] = 2 * (x * y - w * z);
+    R[2] = 2 * (x * z + w * y);
+    R[3] = 2 * (x * y + w * z);
+    R[4] = 1 - 2 * (x * x + z * z);
+    R[5] = 2 * (y * z - w * x);
+    R[6] = 2 * (x * z - w * y);
+    R[7] = 2 * (y * z + w * x);
+    R[8] = 1 - 2 * (x * x + y * y);
+}
+
+// Right singular vector of the smallest singular value of a 4x4 matrix
+// (one-sided Jacobi), used by DLT triangulation (src/utils.h:24-38).
+MP_HD void smallest_right_sv4(const double (&A0)[4][4], double *v) {
+    double A[4][4], V[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            A[i][j] = A0[i][j];
+            V[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    for (int sweep = 0; sweep < 20; ++sweep) {
+        double off = 0.0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int q = p + 1; q < 4; ++q) {
+                double al = 0, be = 0, ga = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    al += A[i][p] * A[i][p];
+                    be += A[i][q] * A[i][q];
+                    ga += A[i][p] * A[i][q];
+                }
+                const double rel = (ga != 0.0) ? fabs(ga) / sqrt(al * be) : 0.0;
+                off = fmax(off, rel);
+                if (rel > 1e-16) {
+                    const double zeta = (be - al) / (2.0 * ga);
+                    const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const double ap = A[i][p], aq = A[i][q];
+                        A[i][p] = c * ap - s * aq;
+                        A[i][q] = s * ap + c * aq;
+                        const double vp = V[i][p], vq = V[i][q];
+                        V[i][p] = c * vp - s * vq;
+                        V[i][q] = s * vp + c * vq;
+                    }
+                }
+            }
+        if (!(off > 1e-15)) break;
+    }
+    double nrm[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) nrm[j] = A[0][j] * A[0][j] + A[1][j] * A[1][j] + A[2][j] * A[2][j] + A[3][j] * A[3][j];
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+        if (nrm[j] < nrm[k]) k = j;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double val = V[i][0];
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+            if (k == j) val = V[i][j];
+        v[i] = val;
+    }
+}
+
+} // namespace mp

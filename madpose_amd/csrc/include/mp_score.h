@@ -1,0 +1,138 @@
+// Per-correspondence residuals of the three estimators, in the form the scoring
+// sweep evaluates them (one correspondence per lane, model constants uniform).
+//
+// Reference: EvaluateModelOnPoint (src/hybrid_pose_estimator.cpp:216-261,
+// src/hybrid_pose_shared_focal_estimator.cpp:160-202,
+// src/hybrid_pose_two_focal_estimator.cpp:213-257), compute_sampson_error
+// (src/utils.h:64-83), check_cheirality (src/solver.cpp:1188-1206), and the MSAC
+// term min(e, thr) * w of ScoreModel/ComputeScore (src/hybrid_ransac.h:265-287).
+// Sentinels follow the reference: DBL_MAX for z < 1e-2, failed cheirality or a
+// score-type-gated residual; min(NaN, thr) stays NaN (std::min semantics).
+#pragma once
+#include <cfloat>
+
+#include "mp_math.h"
+
+namespace mp {
+
+// Prepare the sweep constants of a model (host or device).
+MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r) {
+    double K0[9], K1[9], K0i[9], K1i[9];
+    if (C.variant == kCal) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            K0[i] = C.K0[i];
+            K1[i] = C.K1[i];
+            K0i[i] = C.K0i[i];
+            K1i[i] = C.K1i[i];
+        }
+    } else {
+        const double f0 = m.focal0, f1 = (C.variant == kSF) ? m.focal0 : m.focal1;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) K0[i] = K1[i] = K0i[i] = K1i[i] = 0.0;
+        K0[0] = K0[4] = f0;
+        K1[0] = K1[4] = f1;
+        K0i[0] = K0i[4] = 1.0 / f0;
+        K1i[0] = K1i[4] = 1.0 / f1;
+        K0[8] = K1[8] = K0i[8] = K1i[8] = 1.0;
+    }
+    const double *R = m.R, *t = m.t;
+    double T[9], Rt[9];
+    matmul3(R, K0i, T);
+    matmul3(K1, T, r.M0);
+    matvec3(K1, t, r.k0);
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) Rt[3 * a + b] = R[3 * b + a];
+    matmul3(Rt, K1i, T);
+    matmul3(K0, T, r.M1);
+    double rtt[3];
+    matvec3(Rt, t, rtt);
+    double k1[3];
+    matvec3(K0, rtt, k1);
+    r.k1[0] = -k1[0];
+    r.k1[1] = -k1[1];
+    r.k1[2] = -k1[2];
+    const double tx[9] = {0, -t[2], t[1], t[2], 0, -t[0], -t[1], t[0], 0};
+    double E[9];
+    matmul3(tx, R, E);
+    if (C.variant == kCal) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) r.G[i] = E[i];
+    } else {
+        // F = K1^-T E K0^-1 with diagonal K
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) r.G[3 * a + b] = E[3 * a + b] * K1i[4 * a] * K0i[4 * b];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.R[i] = R[i];
+    r.t[0] = t[0];
+    r.t[1] = t[1];
+    r.t[2] = t[2];
+    r.o0 = m.offset0;
+    r.s = m.scale;
+    r.o1s = m.offset1 * m.scale;
+    r.pad = 0.0;
+}
+
+struct Corr {
+    double x0u, x0v, x1u, x1v, d0, d1, r0, r1;
+};
+
+MP_HD double reproj_err(const double *M, const double *k, double u, double v, double a, double tu, double tv) {
+    const double px = (M[0] * u + M[1] * v + M[2]) * a + k[0];
+    const double py = (M[3] * u + M[4] * v + M[5]) * a + k[1];
+    const double pz = (M[6] * u + M[7] * v + M[8]) * a + k[2];
+    if (pz < 1e-2) return DBL_MAX;
+    const double iz = 1.0 / pz;
+    const double ex = px * iz - tu, ey = py * iz - tv;
+    return ex * ex + ey * ey;
+}
+
+MP_HD double sampson_err(const double *G, double au, double av, double bu, double bv) {
+    const double e0 = G[0] * au + G[1] * av + G[2];
+    const double e1 = G[3] * au + G[4] * av + G[5];
+    const double e2 = G[6] * au + G[7] * av + G[8];
+    const double f0 = G[0] * bu + G[3] * bv + G[6];
+    const double f1 = G[1] * bu + G[4] * bv + G[7];
+    const double c = bu * e0 + bv * e1 + e2;
+    return c * c / (e0 * e0 + e1 * e1 + f0 * f0 + f1 * f1);
+}
+
+// Squared errors of the three data types for one correspondence.
+// gate: apply the score_type gating of EvaluateModelOnPoint (is_for_inlier == false).
+template <int V>
+MP_HD void eval_corr(const PairConst &C, const ScoreRec &r, const Corr &p, bool gate, double &e0, double &e1,
+                     double &e2) {
+    const bool skip_md = gate && C.score_type == 1;  // EPI_ONLY: reprojection gated
+    const bool skip_epi = gate && C.score_type == 2; // MD_ONLY: Sampson gated
+    e0 = skip_md ? DBL_MAX : reproj_err(r.M0, r.k0, p.x0u, p.x0v, p.d0 + r.o0, p.x1u, p.x1v);
+    e1 = skip_md ? DBL_MAX : reproj_err(r.M1, r.k1, p.x1u, p.x1v, p.d1 * r.s + r.o1s, p.x0u, p.x0v);
+    if (skip_epi) {
+        e2 = DBL_MAX;
+        return;
+    }
+    if (V == kCal) {
+        // calibrated rays and unit bearings
+        const double *Ki = C.K0i, *Kj = C.K1i;
+        const double a0 = Ki[0] * p.x0u + Ki[1] * p.x0v + Ki[2];
+        const double a1 = Ki[3] * p.x0u + Ki[4] * p.x0v + Ki[5];
+        const double a2 = Ki[6] * p.x0u + Ki[7] * p.x0v + Ki[8];
+        const double b0 = Kj[0] * p.x1u + Kj[1] * p.x1v + Kj[2];
+        const double b1 = Kj[3] * p.x1u + Kj[4] * p.x1v + Kj[5];
+        const double b2 = Kj[6] * p.x1u + Kj[7] * p.x1v + Kj[8];
+        const double n0[3] = {a0 * p.r0, a1 * p.r0, a2 * p.r0}, n1[3] = {b0 * p.r1, b1 * p.r1, b2 * p.r1};
+        if (!check_cheirality(r.R, r.t, n0, n1, 1e-2)) {
+            e2 = DBL_MAX;
+            return;
+        }
+        e2 = sampson_err(r.G, a0, a1, b0, b1) * C.loss_scale;
+    } else {
+        e2 = sampson_err(r.G, p.x0u, p.x0v, p.x1u, p.x1v);
+    }
+}
+
+} // namespace mp

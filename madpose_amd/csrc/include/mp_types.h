@@ -1,0 +1,62 @@
+// Shared types of the MI355X hybrid-RANSAC engine (device kernels + host controller).
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MP_HD __host__ __device__ inline
+#define MP_DEV __device__ inline
+#else
+#define MP_HD inline
+#define MP_DEV inline
+#endif
+
+namespace mp {
+
+enum Variant : int { kCal = 0, kSF = 1, kTF = 2 };
+
+// Model layout == mp_model of include/madpose_mi355x.h (src/pose.h:7-56).
+// R row-major, x1 = R x0 + t.
+struct Model {
+    double R[9];
+    double t[3];
+    double scale, offset0, offset1, focal0, focal1;
+};
+
+// Per-model constants for the scoring sweep, prepared once per hypothesis so the
+// per-correspondence work is a handful of FMAs (see DESIGN.md "score_sweep").
+//   t=0:  p = M0 (x0,y0,1) * (d0 + o0) + k0      (M0 = K1 R K0^-1, k0 = K1 t)
+//   t=1:  p = M1 (x1,y1,1) * (d1*s + o1s) + k1   (M1 = K0 R^T K1^-1, k1 = -K0 R^T t)
+//   t=2:  Sampson with G (E for calibrated rays, F for normalized pixels),
+//         cheirality with R, t on unit bearings (calibrated variant only).
+struct ScoreRec {
+    double M0[9], k0[3], M1[9], k1[3], G[9], R[9], t[3];
+    double o0, s, o1s, pad;
+};
+
+// Per-pair constants (uniform over a launch).
+struct PairConst {
+    int variant;
+    int n;
+    int score_type; // 0 hybrid, 1 epi-only, 2 md-only (EstimatorConfig::score_type)
+    int min_depth_constraint;
+    int use_shift;
+    int pad0;
+    double K0[9], K1[9], K0i[9], K1i[9]; // identity for SF/TF (focal lives in the model)
+    double thr[3], w[3];                 // squared thresholds / weights after the option transform
+    double loss_scale;                   // calibrated Sampson scale (src/hybrid_pose_estimator.h:35-36)
+    double min_depth[2];
+};
+
+// Device-resident correspondence arrays of one pair (structure of arrays, doubles).
+struct PairData {
+    const double *x0u, *x0v, *x1u, *x1v, *d0, *d1; // pixels (CAL) or normalized pixels (SF/TF)
+    const double *r0, *r1;                          // 1/|K^-1 x| (CAL bearings), else unused
+};
+
+constexpr int kMaxModelsCal = 10; // MD <= 4, 5pt <= 10
+constexpr int kMaxModelsSF = 16;  // MD <= 8, 6pt <= 15
+constexpr int kMaxModelsTF = 4;   // MD <= 4, 7pt <= 3
+MP_HD int max_models(int v) { return v == kCal ? kMaxModelsCal : (v == kSF ? kMaxModelsSF : kMaxModelsTF); }
+
+} // namespace mp

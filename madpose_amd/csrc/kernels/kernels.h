@@ -1,0 +1,36 @@
+// Host-side launch wrappers of the HIP kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../include/mp_types.h"
+
+namespace mp {
+
+constexpr int kSampleStride = 8; // sample indices per iteration slot (max minimal sample = 7)
+
+// r0/r1 = 1 / |K^-1 x| for the calibrated bearings
+hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1);
+
+// MD minimal solver over the listed iterations (one thread per iteration).
+hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                           const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm);
+// point minimal solver over the listed iterations.
+hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                           const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm);
+// scoring sweep: one workgroup per iteration, every model of the iteration scored
+// over all correspondences; per-iteration argmin (first minimum wins).
+hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
+                              const int *counts, int nb, int maxm, double *scores, double *best, int *best_slot);
+// single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
+hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
+                        double *score);
+// scores of many explicit models (one workgroup per model) -- used by mp_score_models
+hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
+                               double *scores);
+
+// standalone solvers (mp_solve_* C API): one sample, one thread
+hipError_t launch_md_direct(hipStream_t s, int variant, const double *in /* x(3K) y(3K) dx(K) dy(K) */,
+                            double *sols, int *nsols, Model *poses, int *nposes);
+hipError_t launch_5pt_direct(hipStream_t s, const double *in /* b1(15) b2(15) */, Model *poses, int *nposes);
+
+} // namespace mp

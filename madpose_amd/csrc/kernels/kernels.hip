@@ -1,0 +1,434 @@
+// HIP kernels of the MI355X hybrid-RANSAC engine (gfx950, wave64).
+//
+//  prep_pair      per-pair bearing norms (once per pair)
+//  md_solve<V>    MD minimal solver, one iteration per thread (registers)
+//  pt_solve<V>    point minimal solver, one iteration per thread
+//  score_batch<V> THE hot loop: one workgroup per RANSAC iteration; each lane owns
+//                 correspondences i = lane, lane+256, ...; all models of the
+//                 iteration are scored from registers with model constants read
+//                 through the scalar cache; MSAC sums reduced in-wave (DPP shuffles)
+//                 and across the 4 waves in LDS in a fixed order (deterministic);
+//                 the workgroup also performs GetBestEstimatedModelId's argmin.
+//  sweep<V>       one model, all points: errors for GetInliers + gated score
+#include <cfloat>
+
+#include "../include/mp_pt.h"
+#include "../include/mp_score.h"
+#include "kernels.h"
+
+namespace mp {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ inline Corr load_corr(const PairData &D, int i, bool cal) {
+    Corr p;
+    p.x0u = D.x0u[i];
+    p.x0v = D.x0v[i];
+    p.x1u = D.x1u[i];
+    p.x1v = D.x1v[i];
+    p.d0 = D.d0[i];
+    p.d1 = D.d1[i];
+    p.r0 = cal ? D.r0[i] : 0.0;
+    p.r1 = cal ? D.r1[i] : 0.0;
+    return p;
+}
+
+__device__ inline double msac(double e, double thr, double w) { return ((thr < e) ? thr : e) * w; }
+
+__global__ void prep_pair_kernel(PairConst C, PairData D, double *r0, double *r1) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C.n) return;
+    const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+    double a[3], b[3];
+    matvec3(C.K0i, xa, a);
+    matvec3(C.K1i, xb, b);
+    r0[i] = 1.0 / sqrt(dot3(a, a));
+    r1[i] = 1.0 / sqrt(dot3(b, b));
+}
+
+__device__ inline void write_models(const PairConst &C, const Model *out, int n, int b, int maxm, Model *models,
+                                    ScoreRec *recs, int *counts) {
+    for (int k = 0; k < n; ++k) {
+        models[(size_t)b * maxm + k] = out[k];
+        ScoreRec r;
+        prepare_score_rec(C, out[k], r);
+        recs[(size_t)b * maxm + k] = r;
+    }
+    counts[b] = n;
+}
+
+// estimator-level min-depth filter of the MD branch (src/hybrid_pose_estimator.cpp:80-85)
+__device__ inline bool md_accept(const PairConst &C, Model &m) {
+    if (!C.min_depth_constraint || (m.offset0 > -C.min_depth[0] && m.offset1 > -C.min_depth[1] * m.scale)) {
+        m.offset1 /= m.scale;
+        return true;
+    }
+    return false;
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                      const int *samples, Model *models, ScoreRec *recs, int *counts,
+                                                      int maxm) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nlist) return;
+    const int b = list[idx];
+    const int *s = samples + (size_t)b * kSampleStride;
+    Model out[8];
+    int n = 0;
+    if (V == kCal) {
+        double x[3][3], y[3][3], dx[3], dy[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int i = s[j];
+            const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+            matvec3(C.K0i, xa, x[j]);
+            matvec3(C.K1i, xb, y[j]);
+            dx[j] = D.d0[i];
+            dy[j] = D.d1[i];
+        }
+        if (!C.use_shift) {
+            Model m;
+            m.focal0 = m.focal1 = 1.0;
+            md_pose_noshift_cal(x, y, dx, dy, m);
+            out[n++] = m;
+        } else {
+            double sols[4][6];
+            const int ns = md_sols_cal(x, y, dx, dy, sols);
+            for (int k = 0; k < ns; ++k) {
+                Model m;
+                m.focal0 = m.focal1 = 1.0;
+                if (md_pose_from_sol<3>(x, y, dx, dy, sols[k], 1.0, 1.0, m) && md_accept(C, m)) out[n++] = m;
+            }
+        }
+    } else {
+        double x[4][3], y[4][3], dx[4], dy[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = s[j];
+            x[j][0] = D.x0u[i];
+            x[j][1] = D.x0v[i];
+            x[j][2] = 1.0;
+            y[j][0] = D.x1u[i];
+            y[j][1] = D.x1v[i];
+            y[j][2] = 1.0;
+            dx[j] = D.d0[i];
+            dy[j] = D.d1[i];
+        }
+        double sols[8][6];
+        int ns;
+        if (V == kSF)
+            ns = md_sols_sf(x, y, dx, dy, sols);
+        else
+            ns = md_sols_tf(x, y, dx, dy, *reinterpret_cast<double(*)[4][6]>(&sols[0][0]));
+        for (int k = 0; k < ns; ++k) {
+            Model m;
+            const double fa = sols[k][4], fb = (V == kSF) ? sols[k][4] : sols[k][5];
+            m.focal0 = fa;
+            m.focal1 = fb;
+            if (md_pose_from_sol<4>(x, y, dx, dy, sols[k], fa, fb, m) && md_accept(C, m)) out[n++] = m;
+        }
+    }
+    write_models(C, out, n, b, maxm, models, recs, counts);
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) pt_solve_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                      const int *samples, Model *models, ScoreRec *recs, int *counts,
+                                                      int maxm) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nlist) return;
+    const int b = list[idx];
+    const int *s = samples + (size_t)b * kSampleStride;
+    int n = 0;
+    Model out[kMaxModelsCal];
+    if (V == kCal) {
+        double b1[5][3], b2[5][3], p0[5][2], p1[5][2], dd0[5], dd1[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int i = s[j];
+            const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+            double a[3], c[3];
+            matvec3(C.K0i, xa, a);
+            matvec3(C.K1i, xb, c);
+            const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                b1[j][q] = a[q] * na;
+                b2[j][q] = c[q] * nc;
+            }
+            p0[j][0] = a[0];
+            p0[j][1] = a[1];
+            p1[j][0] = c[0];
+            p1[j][1] = c[1];
+            dd0[j] = D.d0[i];
+            dd1[j] = D.d1[i];
+        }
+        Model poses[kMaxModelsCal];
+        const int np = relpose_5pt(b1, b2, poses, kMaxModelsCal);
+        for (int k = 0; k < np; ++k) {
+            Model m = poses[k];
+            if (point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, C.use_shift != 0, C.min_depth_constraint != 0,
+                                    C.min_depth, m))
+                out[n++] = m;
+        }
+    }
+    // SF (6-point) / TF (7-point) point solvers: not yet available on device
+    write_models(C, out, n, b, maxm, models, recs, counts);
+}
+
+template <int V, int MAXM>
+__global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairConst C,
+                                                             const ScoreRec *__restrict__ recs,
+                                                             const int *__restrict__ counts, double *scores,
+                                                             double *best, int *best_slot) {
+    const int b = blockIdx.x;
+    const int nm = counts[b];
+    if (nm == 0) {
+        if (threadIdx.x == 0) {
+            best[b] = DBL_MAX;
+            best_slot[b] = 0;
+        }
+        return;
+    }
+    const ScoreRec *R = recs + (size_t)b * MAXM;
+    double acc[MAXM];
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) acc[m] = 0.0;
+    const double t0 = C.thr[0], t1 = C.thr[1], t2 = C.thr[2];
+    const double w0 = C.w[0], w1 = C.w[1], w2 = C.w[2];
+    for (int i = threadIdx.x; i < C.n; i += kBlock) {
+        const Corr p = load_corr(D, i, V == kCal);
+#pragma unroll
+        for (int m = 0; m < MAXM; ++m) {
+            if (m < nm) {
+                double e0, e1, e2;
+                eval_corr<V>(C, R[m], p, true, e0, e1, e2);
+                acc[m] += msac(e0, t0, w0) + msac(e1, t1, w1) + msac(e2, t2, w2);
+            }
+        }
+    }
+    __shared__ double part[kBlock / 64][MAXM];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) {
+        if (m < nm) {
+            const double v = wave_sum(acc[m]);
+            if (lane == 0) part[wave][m] = v;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double bs = DBL_MAX;
+        int bi = 0;
+        for (int m = 0; m < nm; ++m) {
+            double v = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) v += part[w][m];
+            scores[(size_t)b * MAXM + m] = v;
+            if (v < bs) { // strict '<': first minimum wins (src/hybrid_ransac.h:258)
+                bs = v;
+                bi = m;
+            }
+        }
+        best[b] = bs;
+        best_slot[b] = bi;
+    }
+}
+
+template <int V>
+__global__ void __launch_bounds__(1024) sweep_kernel(PairData D, PairConst C, const ScoreRec *rec, double *err,
+                                                     double *score) {
+    const ScoreRec r = *rec;
+    double acc = 0.0;
+    const bool gate_md = C.score_type == 1, gate_epi = C.score_type == 2;
+    for (int i = threadIdx.x; i < C.n; i += blockDim.x) {
+        const Corr p = load_corr(D, i, V == kCal);
+        double e0, e1, e2;
+        eval_corr<V>(C, r, p, false, e0, e1, e2);
+        err[i] = e0;
+        err[C.n + i] = e1;
+        err[2 * C.n + i] = e2;
+        acc += gate_md ? C.thr[0] * C.w[0] + C.thr[1] * C.w[1] : msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]);
+        acc += gate_epi ? C.thr[2] * C.w[2] : msac(e2, C.thr[2], C.w[2]);
+    }
+    __shared__ double part[16];
+    const double v = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+        *score = s;
+    }
+}
+
+template <int V>
+__global__ void __launch_bounds__(kBlock) score_models_kernel(PairData D, PairConst C, const ScoreRec *recs,
+                                                              double *scores) {
+    const ScoreRec r = recs[blockIdx.x];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < C.n; i += kBlock) {
+        const Corr p = load_corr(D, i, V == kCal);
+        double e0, e1, e2;
+        eval_corr<V>(C, r, p, true, e0, e1, e2);
+        acc += msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]) + msac(e2, C.thr[2], C.w[2]);
+    }
+    __shared__ double part[kBlock / 64];
+    const double v = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int w = 0; w < kBlock / 64; ++w) s += part[w];
+        scores[blockIdx.x] = s;
+    }
+}
+
+__global__ void md_direct_kernel(int variant, const double *in, double *sols_out, int *nsols, Model *poses,
+                                 int *nposes) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (variant == kCal) {
+        double x[3][3], y[3][3], dx[3], dy[3];
+        for (int j = 0; j < 3; ++j) {
+            for (int c = 0; c < 3; ++c) {
+                x[j][c] = in[3 * j + c];
+                y[j][c] = in[9 + 3 * j + c];
+            }
+            dx[j] = in[18 + j];
+            dy[j] = in[21 + j];
+        }
+        double sols[4][6];
+        const int ns = md_sols_cal(x, y, dx, dy, sols);
+        int np = 0;
+        for (int k = 0; k < ns; ++k) {
+            for (int c = 0; c < 4; ++c) sols_out[4 * k + c] = sols[k][c];
+            Model m;
+            m.focal0 = m.focal1 = 1.0;
+            if (md_pose_from_sol<3>(x, y, dx, dy, sols[k], 1.0, 1.0, m)) poses[np++] = m;
+        }
+        *nsols = ns;
+        *nposes = np;
+        return;
+    }
+    double x[4][3], y[4][3], dx[4], dy[4];
+    for (int j = 0; j < 4; ++j) {
+        for (int c = 0; c < 3; ++c) {
+            x[j][c] = in[3 * j + c];
+            y[j][c] = in[12 + 3 * j + c];
+        }
+        dx[j] = in[24 + j];
+        dy[j] = in[28 + j];
+    }
+    double sols[8][6];
+    const int ns = (variant == kSF) ? md_sols_sf(x, y, dx, dy, sols)
+                                    : md_sols_tf(x, y, dx, dy, *reinterpret_cast<double(*)[4][6]>(&sols[0][0]));
+    const int w = (variant == kSF) ? 5 : 6;
+    int np = 0;
+    for (int k = 0; k < ns; ++k) {
+        for (int c = 0; c < w; ++c) sols_out[w * k + c] = sols[k][c];
+        Model m;
+        const double fa = sols[k][4], fb = (variant == kSF) ? sols[k][4] : sols[k][5];
+        m.focal0 = fa;
+        m.focal1 = fb;
+        if (md_pose_from_sol<4>(x, y, dx, dy, sols[k], fa, fb, m)) poses[np++] = m;
+    }
+    *nsols = ns;
+    *nposes = np;
+}
+
+__global__ void five_pt_direct_kernel(const double *in, Model *poses, int *nposes) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double b1[5][3], b2[5][3];
+    for (int j = 0; j < 5; ++j)
+        for (int c = 0; c < 3; ++c) {
+            b1[j][c] = in[3 * j + c];
+            b2[j][c] = in[15 + 3 * j + c];
+        }
+    *nposes = relpose_5pt(b1, b2, poses, kMaxModelsCal);
+}
+
+template <class F> hipError_t by_variant(int v, F f) {
+    if (v == kCal) return f(std::integral_constant<int, kCal>());
+    if (v == kSF) return f(std::integral_constant<int, kSF>());
+    return f(std::integral_constant<int, kTF>());
+}
+
+} // namespace
+
+hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1) {
+    if (C.n <= 0) return hipSuccess;
+    prep_pair_kernel<<<(C.n + 255) / 256, 256, 0, s>>>(C, D, r0, r1);
+    return hipGetLastError();
+}
+
+hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                           const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm) {
+    if (nlist <= 0) return hipSuccess;
+    const int grid = (nlist + 63) / 64;
+    return by_variant(C.variant, [&](auto V) {
+        md_solve_kernel<decltype(V)::value><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                           const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm) {
+    if (nlist <= 0) return hipSuccess;
+    const int grid = (nlist + 63) / 64;
+    return by_variant(C.variant, [&](auto V) {
+        pt_solve_kernel<decltype(V)::value><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
+                              const int *counts, int nb, int maxm, double *scores, double *best, int *best_slot) {
+    if (nb <= 0) return hipSuccess;
+    if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
+    if (C.variant == kCal)
+        score_batch_kernel<kCal, kMaxModelsCal><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, best, best_slot);
+    else if (C.variant == kSF)
+        score_batch_kernel<kSF, kMaxModelsSF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, best, best_slot);
+    else
+        score_batch_kernel<kTF, kMaxModelsTF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, best, best_slot);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
+                        double *score) {
+    return by_variant(C.variant, [&](auto V) {
+        sweep_kernel<decltype(V)::value><<<1, 1024, 0, s>>>(D, C, rec, err, score);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
+                               double *scores) {
+    if (nm <= 0) return hipSuccess;
+    return by_variant(C.variant, [&](auto V) {
+        score_models_kernel<decltype(V)::value><<<nm, kBlock, 0, s>>>(D, C, recs, scores);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_md_direct(hipStream_t s, int variant, const double *in, double *sols, int *nsols, Model *poses,
+                            int *nposes) {
+    md_direct_kernel<<<1, 64, 0, s>>>(variant, in, sols, nsols, poses, nposes);
+    return hipGetLastError();
+}
+
+hipError_t launch_5pt_direct(hipStream_t s, const double *in, Model *poses, int *nposes) {
+    five_pt_direct_kernel<<<1, 64, 0, s>>>(in, poses, nposes);
+    return hipGetLastError();
+}
+
+} // namespace mp

@@ -1,0 +1,70 @@
+"""CPU tests of the oracle itself: pinned against the reference's golden vectors."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from madpose_amd import synthetic
+from tests.helpers import oracle_cfg, oracle_opts, rot_angle_deg, solution_sets_match
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("variant,name", [(0, "cal"), (1, "sf"), (2, "tf")])
+def test_oracle_md_matches_reference_goldens(variant, name):
+    g = np.load(os.path.join(GOLDEN, "md_solvers.npz"))
+    for i in range(len(g[f"{name}_x"])):
+        ref = g[f"{name}_sols"][i, : g[f"{name}_nsols"][i]]
+        ref = ref[np.all(np.isfinite(ref), axis=1)]
+        mine = oracle.md_scale_shift(variant, g[f"{name}_x"][i].T, g[f"{name}_y"][i].T, g[f"{name}_dx"][i],
+                                     g[f"{name}_dy"][i])
+        ok, err = solution_sets_match(ref, mine, 1e-6)
+        assert ok, (name, i, err)
+
+
+@pytest.mark.parametrize("variant,name", [(0, "cal"), (1, "sf"), (2, "tf")])
+def test_oracle_md_recovers_ground_truth(variant, name):
+    """Noise-free golden instances: one root equals the generating (b1, a2, b2, f)."""
+    g = np.load(os.path.join(GOLDEN, "md_solvers.npz"))
+    noise = g[f"{name}_noise"]
+    for i in np.flatnonzero(noise == 0)[:60]:
+        gt = g[f"{name}_gt"][i]
+        sols = oracle.md_scale_shift(variant, g[f"{name}_x"][i].T, g[f"{name}_y"][i].T, g[f"{name}_dx"][i],
+                                     g[f"{name}_dy"][i])
+        want = [gt[0], gt[1], gt[2]] + ([gt[3]] if variant == 1 else [gt[3], gt[4]] if variant == 2 else [])
+        errs = [np.max(np.abs(s[1:] - want) / (1 + np.abs(want))) for s in sols]
+        assert min(errs) < 1e-6, (i, errs)
+
+
+def test_oracle_5pt_recovers_ground_truth():
+    rng = np.random.default_rng(0)
+    for _ in range(40):
+        R = np.linalg.qr(rng.standard_normal((3, 3)))[0]
+        R *= np.linalg.det(R)
+        t = rng.standard_normal(3)
+        X = np.c_[rng.uniform(-1, 1, (5, 2)), rng.uniform(2, 6, 5)]
+        X2 = X @ R.T + t
+        if np.any(X2[:, 2] < 0.1):
+            continue
+        b1 = X / np.linalg.norm(X, axis=1, keepdims=True)
+        b2 = X2 / np.linalg.norm(X2, axis=1, keepdims=True)
+        poses = oracle.relpose_5pt(b1, b2)
+        tn = t / np.linalg.norm(t)
+        err = min(rot_angle_deg(p["R"], R) + np.abs(p["t"] / np.linalg.norm(p["t"]) - tn).max() for p in poses)
+        assert err < 1e-5  # degrees + unit-vector difference
+
+
+def test_oracle_estimator_recovers_pose():
+    p = synthetic.make_pair(0, n=400)
+    o, c = synthetic.example_options("calibrated", iterations=300)
+    m, st, inl = oracle.estimate(0, p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], p["K0"], p["K1"],
+                                 oracle_opts(o), oracle_cfg(c))
+    assert rot_angle_deg(m["R"], p["R"]) < 0.5
+    assert st.number_lo_iterations >= 1
+    # inlier lists are sorted, unique and within range
+    for t in range(3):
+        assert np.all(np.diff(inl[t]) > 0) and (len(inl[t]) == 0 or inl[t][-1] < 400)
+    # true inliers dominate the returned set
+    frac = np.mean(p["inlier_mask"][inl[2]])
+    assert frac > 0.9
