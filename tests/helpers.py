@@ -42,8 +42,9 @@ def oracle_cfg(c):
 
 
 def rot_angle_deg(Ra, Rb):
-    c = np.clip((np.trace(Ra.T @ Rb) - 1.0) / 2.0, -1.0, 1.0)
-    return np.rad2deg(np.arccos(c))
+    # chordal form: accurate near zero (arccos of the trace loses ~1e-6 deg there)
+    d = np.linalg.norm(np.asarray(Ra) - np.asarray(Rb)) / (2.0 * np.sqrt(2.0))
+    return np.rad2deg(2.0 * np.arcsin(min(d, 1.0)))
 
 
 def solution_sets_match(ref, mine, rtol):
