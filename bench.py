@@ -1,0 +1,198 @@
+"""Throughput bench of the MI355X hybrid-RANSAC engine (BASELINE.json metric).
+
+A step is one full HybridEstimatePoseScaleOffset run (solver batches, GPU scoring
+sweep, host LO, termination) over one synthetic pair of BASELINE.json configs[1]:
+calibrated, N = 2000 correspondences, 100k iterations (min = max = per-solver cap, so
+the adaptive bound never stops early).  Every rank runs its own pairs (weak scaling);
+the only collective is the final gather of per-rank counters.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cal|sf|tf]
+
+Prints ONE JSON line on rank 0.  `value` = hypotheses scored per second by the whole
+job; `roofline` prices the score_batch kernel at the algorithmic 48*N bytes per
+hypothesis against its HIP-event device time; `cpu_baseline` times the CPU oracle
+(test infrastructure, a scalar restatement of the reference) on a bounded sample of
+the same pair.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (HBM3E spec peak)
+BYTES_PER_CORR = 48    # x0u, x0v, x1u, x1v, d0, d1 in FP64
+
+WORKLOADS = {
+    "cal": dict(kind="calibrated", variant=0, config=2, n=2000, iterations=100000,
+                name="configs[1]: calibrated solver, 1 pair, 2000 synthetic correspondences, 100k hypotheses"),
+    "sf": dict(kind="shared_focal", variant=1, config=3, n=2000, iterations=100000,
+               name="configs[2]: shared-focal solver, 2000 synthetic correspondences, 100k hypotheses"),
+    "tf": dict(kind="two_focal", variant=2, config=4, n=4000, iterations=200000,
+               name="configs[3]: two-focal solver, 4000 synthetic correspondences, 200k hypotheses"),
+}
+
+
+def _pair_args(p, variant):
+    if variant == 0:
+        return (p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], p["K0"], p["K1"])
+    return (p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], p["K0"][:2, 2], p["K1"][:2, 2])
+
+
+def _estimate(madpose, variant, args, o, c, device):
+    fn = [madpose.HybridEstimatePoseScaleOffset, madpose.HybridEstimatePoseScaleOffsetSharedFocal,
+          madpose.HybridEstimatePoseScaleOffsetTwoFocal][variant]
+    return fn(*args, o, c, device=device)
+
+
+def cpu_baseline(wl, pair, budget_s=15.0):
+    """Scalar CPU oracle (kind "port") on a bounded iteration count of the same pair."""
+    try:
+        import oracle
+        from tests.helpers import oracle_cfg, oracle_opts
+        from madpose_amd import synthetic
+    except Exception as e:  # the oracle is test infrastructure; its absence must not break the bench
+        return {"value": None, "unit": "hypotheses/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+    args = _pair_args(pair, wl["variant"])
+    it = 500
+    while True:
+        o, c = synthetic.throughput_options(wl["kind"], iterations=it)
+        t0 = time.perf_counter()
+        _, st, _ = oracle.estimate(wl["variant"], *args, oracle_opts(o), oracle_cfg(c))
+        dt = time.perf_counter() - t0
+        if dt >= budget_s / 3 or it >= wl["iterations"]:
+            break
+        it = min(wl["iterations"], int(it * max(2.0, budget_s / max(dt, 1e-3))))
+    return {"value": st.num_hypotheses / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
+            "sample": f"same pair, {it} iterations (min=max=per-solver cap), single thread, {dt:.1f} s, "
+                      f"{st.num_hypotheses} hypotheses, {st.number_lo_iterations} LO runs"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cal")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (0 = skip)")
+    a = ap.parse_args()
+    wl = WORKLOADS[a.workload]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    import madpose_amd as madpose
+    from madpose_amd import synthetic
+
+    if world > 1:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+    dev = local_rank if torch.cuda.is_available() else 0
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    # per-rank pairs, generated before timing (weak scaling: one pair per rank per step)
+    n_pairs = a.warmup + a.steps
+    pairs = [synthetic.config_pair(wl["config"], seed=rank * 1000 + k) for k in range(n_pairs)]
+    o, c = synthetic.throughput_options(wl["kind"], iterations=wl["iterations"])
+
+    for k in range(a.warmup):
+        _estimate(madpose, wl["variant"], _pair_args(pairs[k], wl["variant"]), o, c, dev)
+
+    madpose.profile_reset()
+    madpose.profile_enable(True)
+    hyps = iters = lo = 0
+    t_lo = 0.0
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(a.warmup, n_pairs):
+        _, st = _estimate(madpose, wl["variant"], _pair_args(pairs[k], wl["variant"]), o, c, dev)
+        hyps += st.num_hypotheses
+        iters += st.num_iterations_total
+        lo += st.number_lo_iterations
+        t_lo += st.seconds_lo
+    barrier()
+    elapsed = time.perf_counter() - t0
+    madpose.profile_enable(False)
+    prof = madpose.profile_read()
+
+    local = torch.tensor([elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
+                          prof["correspondences"], prof["batches"], prof["sweeps"]], dtype=torch.float64)
+    if world > 1:
+        gathered = [torch.zeros_like(local) for _ in range(world)]
+        if dist.get_backend() == "nccl":
+            lc = local.cuda()
+            gl = [g.cuda() for g in gathered]
+            dist.all_gather(gl, lc)
+            gathered = [g.cpu() for g in gl]
+        else:
+            dist.all_gather(gathered, local)
+        allv = torch.stack(gathered).numpy()
+    else:
+        allv = local.numpy()[None]
+
+    if rank == 0:
+        t_max = float(allv[:, 0].max())
+        tot_h, tot_it, tot_lo = allv[:, 1].sum(), allv[:, 2].sum(), allv[:, 3].sum()
+        score_ms = allv[:, 5].sum()
+        corr = allv[:, 8].sum()
+        achieved = corr * BYTES_PER_CORR / (score_ms * 1e-3) / 1e9 if score_ms > 0 else 0.0
+        launches = int(allv[:, 9].sum())
+        res = {
+            "metric": "RANSAC hypotheses/sec + image-pairs/sec on 1xMI355X",
+            "value": tot_h / t_max,
+            "unit": "hypotheses/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": t_max / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded pairs per SURVEY.md §8d; no datasets on the box)",
+            "config": {"workload": wl["name"], "n_correspondences": wl["n"], "iterations": wl["iterations"],
+                       "pairs_per_step_per_gpu": 1, "parallelism": f"pairs sharded over {world} rank(s)"},
+            "pairs_per_s": world * a.steps / t_max,
+            "iterations_per_s": tot_it / t_max,
+            "lo_runs": int(tot_lo),
+            "lo_share": float(allv[:, 4].sum() / allv[:, 0].sum()),
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "score_batch_kernel",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "launches": launches,
+                "avg_launch_us": score_ms * 1e3 / max(launches, 1),
+                "bytes_per_hypothesis": BYTES_PER_CORR * wl["n"],
+                "solve_ms_per_launch": float(allv[:, 6].sum() / max(launches, 1)),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and a.cpu_budget > 0:
+            res["cpu_baseline"] = cpu_baseline(wl, pairs[a.warmup], a.cpu_budget)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

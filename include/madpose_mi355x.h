@@ -142,6 +142,22 @@ int mp_debug_random_stream(int kind, uint32_t seed, int32_t a, int32_t b, int32_
 int mp_debug_iteration_stream(int variant, int32_t n, uint32_t seed, int32_t solver_type, int32_t iterations,
                               int32_t *types, int32_t *idx);
 
+/* Device timing of the estimator's batch kernels (engine-internal; no reference
+ * counterpart).  Durations come from HIP events recorded on the engine's stream
+ * around each launch and are process-wide totals since the last reset. */
+typedef struct mp_kernel_profile {
+    uint64_t batches;         /* speculative batches timed                  */
+    uint64_t iterations;      /* minimal samples solved                     */
+    uint64_t hypotheses;      /* models scored by the score_batch kernel    */
+    uint64_t correspondences; /* sum of hypotheses x n over timed batches   */
+    uint64_t sweeps;          /* single-model LO / termination sweeps       */
+    double solve_ms;          /* md_solve + pt_solve kernels                */
+    double score_ms;          /* score_batch kernel                         */
+} mp_kernel_profile;
+int mp_profile_enable(int on);
+int mp_profile_reset(void);
+int mp_profile_read(mp_kernel_profile *out);
+
 const char *mp_last_error(void);
 int mp_device_count(void);
 const char *mp_version(void);

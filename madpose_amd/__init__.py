@@ -22,6 +22,9 @@ from .api import (  # noqa: F401
     RansacStats,
     device_count,
     estimate_batch,
+    profile_enable,
+    profile_read,
+    profile_reset,
     relpose_5pt,
     score_models,
     set_device,

@@ -87,6 +87,18 @@ class mp_stats(ctypes.Structure):
     ]
 
 
+class mp_kernel_profile(ctypes.Structure):
+    _fields_ = [
+        ("batches", ctypes.c_uint64),
+        ("iterations", ctypes.c_uint64),
+        ("hypotheses", ctypes.c_uint64),
+        ("correspondences", ctypes.c_uint64),
+        ("sweeps", ctypes.c_uint64),
+        ("solve_ms", ctypes.c_double),
+        ("score_ms", ctypes.c_double),
+    ]
+
+
 EXPORTS = {
     "mp_estimate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p, c_double_p,
                                    c_double_p, c_double_p, c_double_p, ctypes.POINTER(mp_ransac_options),
@@ -110,6 +122,9 @@ EXPORTS = {
                                               ctypes.c_int32, c_double_p]),
     "mp_debug_iteration_stream": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32,
                                                  ctypes.c_int32, c_int32_p, c_int32_p]),
+    "mp_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "mp_profile_reset": (ctypes.c_int, []),
+    "mp_profile_read": (ctypes.c_int, [ctypes.POINTER(mp_kernel_profile)]),
     "mp_last_error": (ctypes.c_char_p, []),
     "mp_device_count": (ctypes.c_int, []),
     "mp_version": (ctypes.c_char_p, []),

@@ -501,3 +501,20 @@ def device_count():
 
 def version():
     return L.lib().mp_version().decode()
+
+
+def profile_enable(on=True):
+    """Turn on HIP-event timing of the estimator's batch kernels (process-wide)."""
+    L.check(L.lib().mp_profile_enable(1 if on else 0))
+
+
+def profile_reset():
+    L.check(L.lib().mp_profile_reset())
+
+
+def profile_read():
+    """Totals since the last reset: batches, iterations, hypotheses, correspondences,
+    sweeps, solve_ms, score_ms (device time from HIP events on the engine stream)."""
+    p = L.mp_kernel_profile()
+    L.check(L.lib().mp_profile_read(ctypes.byref(p)))
+    return {name: getattr(p, name) for name, _ in p._fields_}

@@ -277,6 +277,27 @@ int mp_debug_iteration_stream(int variant, int32_t n, uint32_t seed, int32_t sol
     return MP_OK;
 }
 
+int mp_profile_enable(int on) {
+    mp::profile_enable(on != 0);
+    return MP_OK;
+}
+int mp_profile_reset(void) {
+    mp::profile_reset();
+    return MP_OK;
+}
+int mp_profile_read(mp_kernel_profile *out) {
+    if (!out) return MP_EINVAL;
+    const mp::KernelProfile p = mp::profile_read();
+    out->batches = p.batches;
+    out->iterations = p.iterations;
+    out->hypotheses = p.hypotheses;
+    out->correspondences = p.correspondences;
+    out->sweeps = p.sweeps;
+    out->solve_ms = p.solve_ms;
+    out->score_ms = p.score_ms;
+    return MP_OK;
+}
+
 const char *mp_last_error(void) { return g_last_error.c_str(); }
 
 int mp_device_count(void) { return mp::device_count(); }

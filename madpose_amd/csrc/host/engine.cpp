@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -70,6 +71,7 @@ struct DeviceCtx {
     double *h_best = nullptr, *h_err = nullptr, *h_score1 = nullptr;
     ScoreRec *h_rec1 = nullptr;
     Model *h_model1 = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr}; // solve start / score start / score end
 
     void free_all() {
         hipSetDevice(device);
@@ -130,6 +132,10 @@ struct DeviceCtx {
 std::mutex g_pool_mu;
 std::vector<DeviceCtx *> g_pool;
 
+std::atomic<bool> g_prof_on{false};
+std::mutex g_prof_mu;
+KernelProfile g_prof;
+
 struct CtxLease {
     DeviceCtx *c = nullptr;
     explicit CtxLease(int device) {
@@ -151,6 +157,7 @@ struct CtxLease {
             c->device = device;
             MP_HIP(hipSetDevice(device));
             MP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            for (auto &e : c->ev) MP_HIP(hipEventCreate(&e));
         }
         MP_HIP(hipSetDevice(device));
     }
@@ -346,6 +353,10 @@ class Run {
         cache_score_ = X_.h_score1[0];
         cache_valid_ = true;
         S_->num_lo_sweeps++;
+        if (g_prof_on.load(std::memory_order_relaxed)) {
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            g_prof.sweeps += 1;
+        }
         *score = cache_score_;
         return err_.data();
     }
@@ -570,13 +581,17 @@ void Run::run(Model *best, Stats *S) {
                 X_.h_pt_list[npt++] = (int)j;
         }
         hipStream_t s = X_.stream;
+        const bool prof = g_prof_on.load(std::memory_order_relaxed);
         MP_HIP(hipMemcpyAsync(X_.d_samples, X_.h_samples, sizeof(int) * 8 * B, hipMemcpyHostToDevice, s));
         MP_HIP(hipMemcpyAsync(X_.d_md_list, X_.h_md_list, sizeof(int) * std::max(nmd, 1), hipMemcpyHostToDevice, s));
         MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
+        if (prof) MP_HIP(hipEventRecord(X_.ev[0], s));
         MP_HIP(launch_md_solve(s, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs, X_.d_counts, maxm_));
         MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, X_.d_models, X_.d_recs, X_.d_counts, maxm_));
+        if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
         MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_best,
                                   X_.d_best_slot));
+        if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
         MP_HIP(hipMemcpyAsync(X_.h_best, X_.d_best, sizeof(double) * B, hipMemcpyDeviceToHost, s));
         MP_HIP(hipMemcpyAsync(X_.h_best_slot, X_.d_best_slot, sizeof(int) * B, hipMemcpyDeviceToHost, s));
         MP_HIP(hipMemcpyAsync(X_.h_counts, X_.d_counts, sizeof(int) * B, hipMemcpyDeviceToHost, s));
@@ -584,6 +599,20 @@ void Run::run(Model *best, Stats *S) {
         MP_HIP(hipStreamSynchronize(s));
         S->seconds_gpu_wait += secs(tw);
         S->num_batches++;
+        if (prof) {
+            float ms_solve = 0.f, ms_score = 0.f;
+            MP_HIP(hipEventElapsedTime(&ms_solve, X_.ev[0], X_.ev[1]));
+            MP_HIP(hipEventElapsedTime(&ms_score, X_.ev[1], X_.ev[2]));
+            uint64_t h = 0;
+            for (uint32_t q = 0; q < B; ++q) h += (uint64_t)X_.h_counts[q];
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            g_prof.batches += 1;
+            g_prof.iterations += B;
+            g_prof.hypotheses += h;
+            g_prof.correspondences += h * (uint64_t)n_;
+            g_prof.solve_ms += ms_solve;
+            g_prof.score_ms += ms_score;
+        }
 
         bool invalidated = false;
         uint32_t j = 0;
@@ -677,6 +706,16 @@ void validate(const PairInput &in, const RansacOptions &o) {
 }
 
 } // namespace
+
+void profile_enable(bool on) { g_prof_on.store(on); }
+void profile_reset() {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof = KernelProfile();
+}
+KernelProfile profile_read() {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    return g_prof;
+}
 
 void estimate_pair(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int device, Model *out,
                    Stats *stats) {

@@ -67,4 +67,19 @@ int solve_5pt_direct(const double *b1, const double *b2, Model *poses, int max_p
 
 int device_count();
 
+// Per-kernel device timing of the estimator's batch launches, measured with HIP
+// events on the engine's own stream (mp_profile_* C API).  Process-wide totals.
+struct KernelProfile {
+    uint64_t batches = 0;          // speculative batches timed
+    uint64_t iterations = 0;       // minimal samples solved
+    uint64_t hypotheses = 0;       // models scored by score_batch
+    uint64_t correspondences = 0;  // sum over batches of (hypotheses x n)
+    uint64_t sweeps = 0;           // single-model LO / termination sweeps
+    double solve_ms = 0.0;         // md_solve + pt_solve
+    double score_ms = 0.0;         // score_batch
+};
+void profile_enable(bool on);
+void profile_reset();
+KernelProfile profile_read();
+
 } // namespace mp
