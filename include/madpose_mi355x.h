@@ -132,6 +132,16 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
  * (5 points, point-major 3 doubles each).  Returns count or -code. */
 int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device);
 
+/* Point minimal solvers of the uncalibrated estimators on 2-D points in the
+ * estimators' normalized pixel frame ((x - pp) / s, point-major, 2 doubles each),
+ * bearings formed as at src/hybrid_pose_shared_focal_estimator.cpp:79-84:
+ *   6pt: PoseLib relpose_6pt_shared_focal (:87); out.focal0 = out.focal1 = f.
+ *   7pt: PoseLib relpose_7pt + bougnoux_focals + cv::recoverPose
+ *        (src/hybrid_pose_two_focal_estimator.cpp:116-146); out.focal0/1 = f0/f1.
+ * Models are returned before the depth fit (scale 1, offsets 0).  Returns count or -code. */
+int mp_relpose_6pt_shared_focal(const double *x0, const double *x1, mp_model *out, int max_out, int device);
+int mp_relpose_7pt_two_focal(const double *x0, const double *x1, mp_model *out, int max_out, int device);
+
 /* Test hooks for the host-side random streams (no device needed).
  * mp_debug_random_stream: kind 0 raw mt19937 words, 1 uniform_int(a, b),
  * 2 uniform_real(0, b), 3 uniform_int(i % 300, 300 + i % 17) for i = 0..count-1.

@@ -26,6 +26,8 @@ from .api import (  # noqa: F401
     profile_read,
     profile_reset,
     relpose_5pt,
+    relpose_6pt_shared_focal,
+    relpose_7pt_two_focal,
     score_models,
     set_device,
     solve_scale_and_shift,

@@ -118,6 +118,10 @@ EXPORTS = {
                                        ctypes.POINTER(mp_estimator_config), ctypes.POINTER(mp_model), ctypes.c_int32,
                                        c_double_p, c_double_p, ctypes.c_int]),
     "mp_relpose_5pt": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int, ctypes.c_int]),
+    "mp_relpose_6pt_shared_focal": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int,
+                                                   ctypes.c_int]),
+    "mp_relpose_7pt_two_focal": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int,
+                                                ctypes.c_int]),
     "mp_debug_random_stream": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
                                               ctypes.c_int32, c_double_p]),
     "mp_debug_iteration_stream": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32,

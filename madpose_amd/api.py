@@ -473,6 +473,28 @@ def relpose_5pt(x1, x2):
     return [_model_from_c(out[i], L.CALIBRATED) for i in range(min(n, 16))]
 
 
+def _point_direct(fn, k, variant, x0, x1):
+    a = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).reshape(k, 2))
+    b = np.ascontiguousarray(np.asarray(x1, dtype=np.float64).reshape(k, 2))
+    out = (L.mp_model * 16)()
+    n = fn(_dp(a), _dp(b), out, 16, _DEFAULT_DEVICE)
+    if n < 0:
+        L.check(-n)
+    return [_model_from_c(out[i], variant) for i in range(min(n, 16))]
+
+
+def relpose_6pt_shared_focal(x0, x1):
+    """Device shared-focal 6-point solver on normalized 2-D points (6 x 2 each):
+    PoseScaleOffsetSharedFocal candidates before the depth fit."""
+    return _point_direct(L.lib().mp_relpose_6pt_shared_focal, 6, L.SHARED_FOCAL, x0, x1)
+
+
+def relpose_7pt_two_focal(x0, x1):
+    """Device 7-point + Bougnoux + recoverPose on normalized 2-D points (7 x 2 each):
+    PoseScaleOffsetTwoFocal candidates before the depth fit."""
+    return _point_direct(L.lib().mp_relpose_7pt_two_focal, 7, L.TWO_FOCAL, x0, x1)
+
+
 def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, models, with_errors=False):
     """Device ScoreModel over explicit models given in problem units (tests / diagnostics)."""
     x0 = _pts(x0, "x0")

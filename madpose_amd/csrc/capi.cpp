@@ -224,14 +224,27 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
     });
 }
 
-int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device) {
+static int point_direct(int kind, const double *x1, const double *x2, mp_model *out, int max_out, int device) {
+    if (!x1 || !x2 || (max_out > 0 && !out)) return -fail(MP_EINVAL, "null argument");
     int r = guarded([&]() {
         mp::Model poses[16];
-        int np = mp::solve_5pt_direct(x1, x2, poses, 16, device);
+        int np = mp::solve_point_direct(kind, x1, x2, poses, 16, device);
         for (int i = 0; i < std::min(np, max_out); ++i) to_model(poses[i], &out[i]);
         return -(np + 1000);
     });
     return r <= -1000 ? -(r + 1000) : -r;
+}
+
+int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device) {
+    return point_direct(0, x1, x2, out, max_out, device);
+}
+
+int mp_relpose_6pt_shared_focal(const double *x0, const double *x1, mp_model *out, int max_out, int device) {
+    return point_direct(1, x0, x1, out, max_out, device);
+}
+
+int mp_relpose_7pt_two_focal(const double *x0, const double *x1, mp_model *out, int max_out, int device) {
+    return point_direct(2, x0, x1, out, max_out, device);
 }
 
 int mp_debug_random_stream(int kind, uint32_t seed, int32_t a, int32_t b, int32_t count, double *out) {

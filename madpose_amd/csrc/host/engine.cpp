@@ -309,7 +309,7 @@ class Run {
         w_[1] = P.C.w[1];
         w_[2] = P.C.w[2];
         const char *env = std::getenv("MADPOSE_MAX_BATCH");
-        max_batch_ = env ? std::max(1, std::atoi(env)) : 8192;
+        max_batch_ = env ? std::max(1, std::atoi(env)) : 65536;
         const char *env2 = std::getenv("MADPOSE_MIN_BATCH");
         min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 128;
         min_batch_ = std::min(min_batch_, max_batch_);
@@ -667,11 +667,11 @@ void Run::run(Model *best, Stats *S) {
             }
         }
         if (!done && !invalidated) it += B;
-        // batch-size schedule: grow while batches survive, shrink after a cut
-        if (invalidated)
-            bcur = std::max(min_batch_, bcur / 2);
-        else
-            bcur = std::min(max_batch_, bcur * 2);
+        // batch-size schedule: the solver kernels are latency-bound (cost ~flat up to
+        // tens of thousands of samples) and new bests -- the only thing that cuts a
+        // batch -- thin out like records of an iid sequence, so speculate on a window
+        // proportional to the position in the stream.
+        bcur = (int)std::min<uint64_t>((uint64_t)max_batch_, std::max<uint64_t>((uint64_t)min_batch_, 4ull * it));
     }
     if (!done) S->num_iterations_total = it;
 
@@ -802,29 +802,32 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
     return hn[0];
 }
 
-int solve_5pt_direct(const double *b1, const double *b2, Model *poses, int max_poses, int device) {
+int solve_point_direct(int kind, const double *x1, const double *x2, Model *poses, int max_poses, int device) {
+    if (kind < 0 || kind > 2) throw std::invalid_argument("point solver kind must be 0, 1 or 2");
     CtxLease lease(device);
     DeviceCtx &X = *lease.c;
+    const int per = kind == 0 ? 15 : (kind == 1 ? 12 : 14);
     double in[30];
-    std::memcpy(in, b1, sizeof(double) * 15);
-    std::memcpy(in + 15, b2, sizeof(double) * 15);
+    std::memcpy(in, x1, sizeof(double) * per);
+    std::memcpy(in + per, x2, sizeof(double) * per);
     double *d_in;
     int *d_n;
     Model *d_poses;
+    constexpr int kCap = 16;
     MP_HIP(hipMalloc(&d_in, sizeof(in)));
     MP_HIP(hipMalloc(&d_n, sizeof(int)));
-    MP_HIP(hipMalloc(&d_poses, sizeof(Model) * kMaxModelsCal));
+    MP_HIP(hipMalloc(&d_poses, sizeof(Model) * kCap));
     MP_HIP(hipMemcpyAsync(d_in, in, sizeof(in), hipMemcpyHostToDevice, X.stream));
-    MP_HIP(launch_5pt_direct(X.stream, d_in, d_poses, d_n));
+    MP_HIP(launch_point_direct(X.stream, kind, d_in, d_poses, d_n));
     int hn = 0;
-    Model hp[kMaxModelsCal];
+    Model hp[kCap];
     MP_HIP(hipMemcpyAsync(&hn, d_n, sizeof(int), hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipMemcpyAsync(hp, d_poses, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));
     hipFree(d_in);
     hipFree(d_n);
     hipFree(d_poses);
-    for (int i = 0; i < std::min(hn, max_poses); ++i) poses[i] = hp[i];
+    for (int i = 0; i < std::min(std::min(hn, kCap), max_poses); ++i) poses[i] = hp[i];
     return hn;
 }
 

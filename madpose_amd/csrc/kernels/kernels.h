@@ -31,6 +31,6 @@ hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst
 // standalone solvers (mp_solve_* C API): one sample, one thread
 hipError_t launch_md_direct(hipStream_t s, int variant, const double *in /* x(3K) y(3K) dx(K) dy(K) */,
                             double *sols, int *nsols, Model *poses, int *nposes);
-hipError_t launch_5pt_direct(hipStream_t s, const double *in /* b1(15) b2(15) */, Model *poses, int *nposes);
+hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes);
 
 } // namespace mp

@@ -12,7 +12,7 @@
 //  sweep<V>       one model, all points: errors for GetInliers + gated score
 #include <cfloat>
 
-#include "../include/mp_pt.h"
+#include "../include/mp_pt67.h"
 #include "../include/mp_score.h"
 #include "kernels.h"
 
@@ -140,6 +140,36 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
     write_models(C, out, n, b, maxm, models, recs, counts);
 }
 
+__device__ inline void put_model(const PairConst &C, const Model &m, int b, int slot, int maxm, Model *models,
+                                 ScoreRec *recs) {
+    models[(size_t)b * maxm + slot] = m;
+    ScoreRec r;
+    prepare_score_rec(C, m, r);
+    recs[(size_t)b * maxm + slot] = r;
+}
+
+template <int K>
+__device__ inline void load_uncal_sample(const PairData &D, const int *s, double (&b0)[K][3], double (&b1)[K][3],
+                                         double (&p0)[K][2], double (&p1)[K][2], double (&dd0)[K], double (&dd1)[K]) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const int i = s[j];
+        const double a[3] = {D.x0u[i], D.x0v[i], 1.0}, c[3] = {D.x1u[i], D.x1v[i], 1.0};
+        const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            b0[j][q] = a[q] * na;
+            b1[j][q] = c[q] * nc;
+        }
+        p0[j][0] = a[0];
+        p0[j][1] = a[1];
+        p1[j][0] = c[0];
+        p1[j][1] = c[1];
+        dd0[j] = D.d0[i];
+        dd1[j] = D.d1[i];
+    }
+}
+
 template <int V>
 __global__ void __launch_bounds__(64) pt_solve_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                       const int *samples, Model *models, ScoreRec *recs, int *counts,
@@ -149,8 +179,9 @@ __global__ void __launch_bounds__(64) pt_solve_kernel(PairData D, PairConst C, c
     const int b = list[idx];
     const int *s = samples + (size_t)b * kSampleStride;
     int n = 0;
-    Model out[kMaxModelsCal];
+    const bool shift = C.use_shift != 0, mdc = C.min_depth_constraint != 0;
     if (V == kCal) {
+        // src/hybrid_pose_estimator.cpp:121-185
         double b1[5][3], b2[5][3], p0[5][2], p1[5][2], dd0[5], dd1[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -176,13 +207,48 @@ __global__ void __launch_bounds__(64) pt_solve_kernel(PairData D, PairConst C, c
         const int np = relpose_5pt(b1, b2, poses, kMaxModelsCal);
         for (int k = 0; k < np; ++k) {
             Model m = poses[k];
-            if (point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, C.use_shift != 0, C.min_depth_constraint != 0,
-                                    C.min_depth, m))
-                out[n++] = m;
+            if (point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, shift, mdc, C.min_depth, m))
+                put_model(C, m, b, n++, maxm, models, recs);
+        }
+    } else if (V == kSF) {
+        // src/hybrid_pose_shared_focal_estimator.cpp:74-128
+        double b0[6][3], b1[6][3], p0[6][2], p1[6][2], dd0[6], dd1[6];
+        load_uncal_sample<6>(D, s, b0, b1, p0, p1, dd0, dd1);
+        Model poses[kMaxModelsSF];
+        const int np = relpose_6pt_sf(b0, b1, poses, kMaxModelsSF);
+        for (int k = 0; k < np; ++k) {
+            Model m = poses[k];
+            const double f = m.focal0;
+            if (point_model_tail<6>(p0, p1, dd0, dd1, f, f, shift, mdc, C.min_depth, m))
+                put_model(C, m, b, n++, maxm, models, recs);
+        }
+    } else {
+        // src/hybrid_pose_two_focal_estimator.cpp:103-182
+        double b0[7][3], b1[7][3], p0[7][2], p1[7][2], dd0[7], dd1[7];
+        load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
+        double F[3][9];
+        const int nf = relpose_7pt_F(b0, b1, F);
+        for (int k = 0; k < nf; ++k) {
+            double f0, f1;
+            bougnoux_sq(F[k], &f0, &f1);
+            f0 = sqrt(fabs(f0));
+            f1 = sqrt(fabs(f1));
+            double E[9];
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) E[3 * r + c] = (r < 2 ? f1 : 1.0) * F[k][3 * r + c] * (c < 2 ? f0 : 1.0);
+            Model m;
+            recover_pose_cv<7>(E, p0, p1, 1e9, m.R, m.t);
+            m.scale = 1.0;
+            m.offset0 = m.offset1 = 0.0;
+            m.focal0 = f0;
+            m.focal1 = f1;
+            if (point_model_tail<7>(p0, p1, dd0, dd1, f0, f1, shift, mdc, C.min_depth, m))
+                put_model(C, m, b, n++, maxm, models, recs);
         }
     }
-    // SF (6-point) / TF (7-point) point solvers: not yet available on device
-    write_models(C, out, n, b, maxm, models, recs, counts);
+    counts[b] = n;
 }
 
 template <int V, int MAXM>
@@ -345,15 +411,65 @@ __global__ void md_direct_kernel(int variant, const double *in, double *sols_out
     *nposes = np;
 }
 
-__global__ void five_pt_direct_kernel(const double *in, Model *poses, int *nposes) {
+// standalone point solvers (test hooks): kind 0 = 5pt on unit bearings (5 + 5 x 3
+// doubles); kind 1 = shared-focal 6pt, kind 2 = two-focal 7pt + Bougnoux +
+// recoverPose, both on normalized 2-D points (K + K x 2 doubles) turned into
+// bearings exactly as the estimator does.  Models are returned before the depth fit.
+__global__ void point_direct_kernel(int kind, const double *in, Model *poses, int *nposes) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double b1[5][3], b2[5][3];
-    for (int j = 0; j < 5; ++j)
-        for (int c = 0; c < 3; ++c) {
-            b1[j][c] = in[3 * j + c];
-            b2[j][c] = in[15 + 3 * j + c];
+    if (kind == 0) {
+        double b1[5][3], b2[5][3];
+        for (int j = 0; j < 5; ++j)
+            for (int c = 0; c < 3; ++c) {
+                b1[j][c] = in[3 * j + c];
+                b2[j][c] = in[15 + 3 * j + c];
+            }
+        *nposes = relpose_5pt(b1, b2, poses, kMaxModelsCal);
+    } else if (kind == 1) {
+        double b0[6][3], b1[6][3];
+        for (int j = 0; j < 6; ++j) {
+            const double a[3] = {in[2 * j], in[2 * j + 1], 1.0}, c[3] = {in[12 + 2 * j], in[12 + 2 * j + 1], 1.0};
+            const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+            for (int q = 0; q < 3; ++q) {
+                b0[j][q] = a[q] * na;
+                b1[j][q] = c[q] * nc;
+            }
         }
-    *nposes = relpose_5pt(b1, b2, poses, kMaxModelsCal);
+        *nposes = relpose_6pt_sf(b0, b1, poses, kMaxModelsSF);
+    } else {
+        double b0[7][3], b1[7][3], p0[7][2], p1[7][2];
+        for (int j = 0; j < 7; ++j) {
+            const double a[3] = {in[2 * j], in[2 * j + 1], 1.0}, c[3] = {in[14 + 2 * j], in[14 + 2 * j + 1], 1.0};
+            const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+            for (int q = 0; q < 3; ++q) {
+                b0[j][q] = a[q] * na;
+                b1[j][q] = c[q] * nc;
+            }
+            p0[j][0] = a[0];
+            p0[j][1] = a[1];
+            p1[j][0] = c[0];
+            p1[j][1] = c[1];
+        }
+        double F[3][9];
+        const int nf = relpose_7pt_F(b0, b1, F);
+        for (int k = 0; k < nf; ++k) {
+            double f0, f1;
+            bougnoux_sq(F[k], &f0, &f1);
+            f0 = sqrt(fabs(f0));
+            f1 = sqrt(fabs(f1));
+            double E[9];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) E[3 * r + c] = (r < 2 ? f1 : 1.0) * F[k][3 * r + c] * (c < 2 ? f0 : 1.0);
+            Model m;
+            recover_pose_cv<7>(E, p0, p1, 1e9, m.R, m.t);
+            m.scale = 1.0;
+            m.offset0 = m.offset1 = 0.0;
+            m.focal0 = f0;
+            m.focal1 = f1;
+            poses[k] = m;
+        }
+        *nposes = nf;
+    }
 }
 
 template <class F> hipError_t by_variant(int v, F f) {
@@ -426,8 +542,8 @@ hipError_t launch_md_direct(hipStream_t s, int variant, const double *in, double
     return hipGetLastError();
 }
 
-hipError_t launch_5pt_direct(hipStream_t s, const double *in, Model *poses, int *nposes) {
-    five_pt_direct_kernel<<<1, 64, 0, s>>>(in, poses, nposes);
+hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes) {
+    point_direct_kernel<<<1, 64, 0, s>>>(kind, in, poses, nposes);
     return hipGetLastError();
 }
 

@@ -134,6 +134,35 @@ def relpose_5pt(b1, b2):
     return [model_to_dict(out[i]) for i in range(min(n, 32))]
 
 
+def relpose_6pt_shared_focal(b1, b2):
+    """PoseLib relpose_6pt_shared_focal restatement: list of dicts (focal in focal0)."""
+    out = (OrModel * 64)()
+    n = lib().oracle_relpose_6pt(_dp(_c(b1)), _dp(_c(b2)), out, 64)
+    return [model_to_dict(out[i]) for i in range(min(n, 64))]
+
+
+def relpose_7pt(b1, b2):
+    """PoseLib relpose_7pt restatement: (k, 3, 3) fundamental matrices."""
+    out = np.zeros((8, 9))
+    n = lib().oracle_relpose_7pt(_dp(_c(b1)), _dp(_c(b2)), _dp(out), 8)
+    return out[:n].reshape(-1, 3, 3).copy()
+
+
+def bougnoux_focals(F):
+    out = np.zeros(2)
+    lib().oracle_bougnoux(_dp(_c(F)), _dp(out))
+    return out
+
+
+def recover_pose(E, p0, p1, thresh=1e9):
+    p0, p1 = _c(p0), _c(p1)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    lib().oracle_recover_pose.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_double] + [ctypes.c_void_p] * 2
+    good = lib().oracle_recover_pose(_dp(_c(E)), _dp(p0), _dp(p1), len(p0), thresh, _dp(R), _dp(t))
+    return R.reshape(3, 3), t, good
+
+
 def score_models(variant, x0, x1, d0, d1, cam0, cam1, opts, cfg, models):
     """models: list of OrModel (problem units).  Returns (scores, errors[m,3,n], norm_scale)."""
     n = len(d0)

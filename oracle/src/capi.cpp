@@ -119,6 +119,31 @@ int oracle_relpose_5pt(const double *x1, const double *x2, or_model *out, int ma
     return (int)sols.size();
 }
 
+int oracle_relpose_7pt(const double *x1, const double *x2, double *F_out, int max_out) {
+    auto sols = oracle::relpose_7pt(x1, x2);
+    int n = std::min((int)sols.size(), max_out);
+    for (int i = 0; i < n; ++i)
+        for (int e = 0; e < 9; ++e) F_out[9 * i + e] = sols[i][e];
+    return (int)sols.size();
+}
+
+int oracle_bougnoux(const double *F, double *f_sq) {
+    oracle::bougnoux_focals(F, &f_sq[0], &f_sq[1]);
+    return 0;
+}
+
+int oracle_recover_pose(const double *E, const double *p0, const double *p1, int n, double thresh, double *R,
+                        double *t) {
+    return oracle::recover_pose(E, p0, p1, n, thresh, R, t);
+}
+
+int oracle_relpose_6pt(const double *x1, const double *x2, or_model *out, int max_out) {
+    auto sols = oracle::relpose_6pt_shared_focal(x1, x2);
+    int n = std::min((int)sols.size(), max_out);
+    for (int i = 0; i < n; ++i) put_model(sols[i], &out[i]);
+    return (int)sols.size();
+}
+
 // Scores / per-point errors of given models (models in problem units, i.e. after
 // the SF/TF normalisation).  errors: num_models x 3 x n (is_for_inlier = true).
 int oracle_score_models(int variant, int64_t n, const double *x0, const double *x1, const double *d0,

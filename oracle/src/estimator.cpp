@@ -363,7 +363,38 @@ int minimal_solver(const Problem &P, const std::vector<std::vector<int>> &sample
             if (point_model_tail(P, idx, pose.R, pose.t, 1.0, 1.0, &m)) models->push_back(m);
         }
     }
-    // SF (6pt) and TF (7pt) point solvers: see relpose_6pt / relpose_7pt (not yet restated)
+    std::vector<double> p0(2 * k), p1(2 * k);
+    for (int j = 0; j < k; ++j) {
+        p0[2 * j] = P.x0[3 * idx[j]];
+        p0[2 * j + 1] = P.x0[3 * idx[j] + 1];
+        p1[2 * j] = P.x1[3 * idx[j]];
+        p1[2 * j + 1] = P.x1[3 * idx[j] + 1];
+    }
+    if (P.variant == SF) {
+        // src/hybrid_pose_shared_focal_estimator.cpp:74-128
+        for (const Model &ip : relpose_6pt_shared_focal(b0.data(), b1.data())) {
+            Model m;
+            m.focal0 = m.focal1 = ip.focal0;
+            if (point_model_tail(P, idx, ip.R, ip.t, ip.focal0, ip.focal0, &m)) models->push_back(m);
+        }
+    } else if (P.variant == TF) {
+        // src/hybrid_pose_two_focal_estimator.cpp:103-182
+        for (const auto &F : relpose_7pt(b0.data(), b1.data())) {
+            double f0, f1;
+            bougnoux_focals(F.data(), &f0, &f1);
+            f0 = std::sqrt(std::fabs(f0));
+            f1 = std::sqrt(std::fabs(f1));
+            double E[9];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) E[3 * r + c] = (r < 2 ? f1 : 1.0) * F[3 * r + c] * (c < 2 ? f0 : 1.0);
+            double R[9], t[3];
+            recover_pose(E, p0.data(), p1.data(), k, 1e9, R, t);
+            Model m;
+            m.focal0 = f0;
+            m.focal1 = f1;
+            if (point_model_tail(P, idx, R, t, f0, f1, &m)) models->push_back(m);
+        }
+    }
     return (int)models->size();
 }
 

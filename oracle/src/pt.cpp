@@ -62,6 +62,8 @@ void cross3(const double *a, const double *b, double *c) {
     c[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+} // namespace
+
 void motion_from_essential(const double E[9], const double *x1, const double *x2, int np, std::vector<Model> *out) {
     // columns of E
     double c0[3] = {E[0], E[3], E[6]}, c1[3] = {E[1], E[4], E[7]}, c2[3] = {E[2], E[5], E[8]};
@@ -134,8 +136,6 @@ void motion_from_essential(const double E[9], const double *x1, const double *x2
     try_pose(-1.0, -1.0);
     try_pose(-1.0, 1.0);
 }
-
-} // namespace
 
 bool check_cheirality(const double R[9], const double t[3], const double x1[3], const double x2[3], double min_depth) {
     double Rx1[3];
