@@ -26,6 +26,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -313,6 +314,7 @@ class Run {
         const char *env2 = std::getenv("MADPOSE_MIN_BATCH");
         min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 128;
         min_batch_ = std::min(min_batch_, max_batch_);
+        trace_ = std::getenv("MADPOSE_TRACE") != nullptr;
     }
 
     void run(Model *best, Stats *S);
@@ -327,6 +329,7 @@ class Run {
     int min_sample_size_, non_min_sample_size_;
     double thr_[3], w_[3];
     int max_batch_, min_batch_;
+    bool trace_ = false;
     PairData D_;
     Stats *S_ = nullptr;
     IterationStream rs_; // sampler + selection/LO streams
@@ -628,6 +631,7 @@ void Run::run(Model *best, Stats *S) {
                 if (bl < best_min_score || iter == lo_start) {
                     const bool new_best = bl < best_min_score;
                     if (new_best) {
+                        if (trace_) std::fprintf(stderr, "[engine] it=%u new best %.17g (solver %d, %d models)\n", iter, bl, st, nm);
                         best_min_score = bl;
                         best_min = fetch_model((int)j, X_.h_best_slot[j]);
                         update_best(best_min_score, best_min, st, &S->best_model_score, best, &S->best_solver_type);
@@ -642,6 +646,7 @@ void Run::run(Model *best, Stats *S) {
                             ++S->number_lo_iterations;
                             double sc = best_min_score;
                             local_opt(S->best_solver_type, &best_min, &sc, &S->best_solver_type);
+                            if (trace_) std::fprintf(stderr, "[engine] it=%u LO %.17g -> %.17g\n", iter, best_min_score, sc);
                             update_best(sc, best_min, st, &S->best_model_score, best, &S->best_solver_type);
                             lo_here = true;
                             invalidated = true;

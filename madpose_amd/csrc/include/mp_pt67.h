@@ -206,8 +206,16 @@ MP_HD void jacobi_eig3(double (&A)[3][3], double (&V)[3][3]) {
 // cv::recoverPose(E, p0, p1, I, R, t, dist) with the candidate order of OpenCV's
 // decomposeEssentialMat; returns the number of good points of the chosen pose.
 template <int K>
-MP_HD int recover_pose_cv(const double *E, const double (&p0)[K][2], const double (&p1)[K][2], double dist,
+MP_HD int recover_pose_cv(const double *E_in, const double (&p0)[K][2], const double (&p1)[K][2], double dist,
                           double *R, double *t) {
+    // canonical sign of E (largest-magnitude entry positive), as in the oracle
+    double emax = E_in[0];
+#pragma unroll
+    for (int e = 1; e < 9; ++e)
+        if (fabs(E_in[e]) > fabs(emax)) emax = E_in[e];
+    double E[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) E[e] = emax < 0 ? -E_in[e] : E_in[e];
     double S[3][3], V[3][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -227,33 +235,45 @@ MP_HD int recover_pose_cv(const double *E, const double (&p0)[K][2], const doubl
         i0 = 0;
         i1 = (l1 >= l2) ? 1 : 2;
     }
+    // canonical reflection of (v1, v2): v3 = v1 x v2 with its largest-magnitude entry
+    // positive (see oracle/src/pt67.cpp); u2 re-orthogonalised against u1
     double v[3][3], u[3][3];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int ik = k == 0 ? i0 : i1;
-        double col[3];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) col[r] = (ik == 0) ? V[r][0] : ((ik == 1) ? V[r][1] : V[r][2]);
-        int im = 0;
+        for (int r = 0; r < 3; ++r) v[k][r] = (ik == 0) ? V[r][0] : ((ik == 1) ? V[r][1] : V[r][2]);
+    }
+    cross3(v[0], v[1], v[2]);
+    {
+        double vm = v[2][0];
 #pragma unroll
         for (int r = 1; r < 3; ++r)
-            if (fabs(col[r]) > fabs(col[im])) im = r;
-        const double cm = (im == 0) ? col[0] : ((im == 1) ? col[1] : col[2]);
-        const double sg = cm < 0 ? -1.0 : 1.0;
+            if (fabs(v[2][r]) > fabs(vm)) vm = v[2][r];
+        if (vm < 0) {
 #pragma unroll
-        for (int r = 0; r < 3; ++r) v[k][r] = sg * col[r];
-        double nn = 0.0;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            u[k][r] = E[3 * r] * v[k][0] + E[3 * r + 1] * v[k][1] + E[3 * r + 2] * v[k][2];
-            nn += u[k][r] * u[k][r];
+            for (int r = 0; r < 3; ++r) {
+                v[1][r] = -v[1][r];
+                v[2][r] = -v[2][r];
+            }
         }
-        nn = 1.0 / sqrt(nn);
+    }
 #pragma unroll
-        for (int r = 0; r < 3; ++r) u[k][r] *= nn;
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) u[k][r] = E[3 * r] * v[k][0] + E[3 * r + 1] * v[k][1] + E[3 * r + 2] * v[k][2];
+    {
+        const double n0 = 1.0 / sqrt(dot3(u[0], u[0]));
+#pragma unroll
+        for (int r = 0; r < 3; ++r) u[0][r] *= n0;
+        const double d = dot3(u[0], u[1]);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) u[1][r] -= d * u[0][r];
+        const double n1 = 1.0 / sqrt(dot3(u[1], u[1]));
+#pragma unroll
+        for (int r = 0; r < 3; ++r) u[1][r] *= n1;
     }
     cross3(u[0], u[1], u[2]);
-    cross3(v[0], v[1], v[2]);
     double R1[9], R2[9];
 #pragma unroll
     for (int r = 0; r < 3; ++r)

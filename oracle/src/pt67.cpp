@@ -168,35 +168,52 @@ void bougnoux_focals(const double F[9], double *f0_sq, double *f1_sq) {
     *f1_sq = -T1[8] / T2[8];
 }
 
-int recover_pose(const double E[9], const double *p0, const double *p1, int n, double dist_thresh, double R[9],
+int recover_pose(const double E_in[9], const double *p0, const double *p1, int n, double dist_thresh, double R[9],
                  double t[3]) {
+    // The sign of E (inherited from the arbitrary sign of F) only relabels the four
+    // candidates; it is fixed canonically (largest-magnitude entry positive).
+    double E[9];
+    int emax = 0;
+    for (int e = 1; e < 9; ++e)
+        if (std::fabs(E_in[e]) > std::fabs(E_in[emax])) emax = e;
+    for (int e = 0; e < 9; ++e) E[e] = E_in[emax] < 0 ? -E_in[e] : E_in[e];
     Mat A(3, 3);
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) A(r, c) = E[3 * r + c];
     Mat U, V;
     std::vector<double> s;
     jacobi_svd(A, &U, &s, &V);
-    // OpenCV's SVD sign conventions are not reproducible without its source; the
-    // candidate order (and so tie-breaking) is fixed canonically instead: v1, v2 with
-    // their largest-magnitude entry positive, u_k = E v_k / s_k, u3 = u1 x u2,
-    // v3 = v1 x v2 (both rotations, so the det(U), det(Vt) flips are no-ops).
+    // OpenCV's SVD sign conventions are not reproducible without its source, and
+    // with Bougnoux focals E has two equal singular values, so (v1, v2) is only
+    // defined up to an in-plane rotation -- which leaves R1, R2 and u3 unchanged --
+    // and a reflection, which relabels the candidates.  The reflection is fixed
+    // canonically: v3 = v1 x v2 with its largest-magnitude entry positive (v2 is
+    // flipped otherwise); u_k = E v_k / |E v_k|, u2 re-orthogonalised, u3 = u1 x u2.
     double v[3][3], u[3][3];
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 2; ++k)
+        for (int r = 0; r < 3; ++r) v[k][r] = V(r, k);
+    cross3v(v[0], v[1], v[2]);
+    {
         int im = 0;
         for (int r = 1; r < 3; ++r)
-            if (std::fabs(V(r, k)) > std::fabs(V(im, k))) im = r;
-        const double sg = V(im, k) < 0 ? -1.0 : 1.0;
-        for (int r = 0; r < 3; ++r) v[k][r] = sg * V(r, k);
-        double nn = 0.0;
-        for (int r = 0; r < 3; ++r) {
-            u[k][r] = E[3 * r] * v[k][0] + E[3 * r + 1] * v[k][1] + E[3 * r + 2] * v[k][2];
-            nn += u[k][r] * u[k][r];
-        }
-        nn = std::sqrt(nn);
-        for (int r = 0; r < 3; ++r) u[k][r] /= nn;
+            if (std::fabs(v[2][r]) > std::fabs(v[2][im])) im = r;
+        if (v[2][im] < 0)
+            for (int r = 0; r < 3; ++r) {
+                v[1][r] = -v[1][r];
+                v[2][r] = -v[2][r];
+            }
+    }
+    for (int k = 0; k < 2; ++k)
+        for (int r = 0; r < 3; ++r) u[k][r] = E[3 * r] * v[k][0] + E[3 * r + 1] * v[k][1] + E[3 * r + 2] * v[k][2];
+    {
+        double n0 = std::sqrt(u[0][0] * u[0][0] + u[0][1] * u[0][1] + u[0][2] * u[0][2]);
+        for (int r = 0; r < 3; ++r) u[0][r] /= n0;
+        const double d = u[0][0] * u[1][0] + u[0][1] * u[1][1] + u[0][2] * u[1][2];
+        for (int r = 0; r < 3; ++r) u[1][r] -= d * u[0][r];
+        double n1 = std::sqrt(u[1][0] * u[1][0] + u[1][1] * u[1][1] + u[1][2] * u[1][2]);
+        for (int r = 0; r < 3; ++r) u[1][r] /= n1;
     }
     cross3v(u[0], u[1], u[2]);
-    cross3v(v[0], v[1], v[2]);
     double Um[9], Vt[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) {

@@ -11,6 +11,8 @@
 //                             for i < k, a no-op when k >= size.
 // The random streams are libstdc++'s (std::mt19937, std::uniform_*_distribution),
 // i.e. exactly what the reference consumes.
+#include <cstdlib>
+#include <cstdio>
 #include <algorithm>
 #include <cmath>
 #include <limits>
@@ -265,6 +267,7 @@ struct Engine {
                 if (bl < best_min_score || it == lo_start) {
                     const bool new_best = bl < best_min_score;
                     if (new_best) {
+                        if (std::getenv("ORACLE_TRACE")) std::fprintf(stderr, "[oracle] it=%u new best %.17g (solver %d, %d models)\n", it, bl, st, nm);
                         best_min_score = bl;
                         best_min = models[bid];
                         update_best(best_min_score, best_min, st, &S->best_model_score, best, &S->best_solver_type);
@@ -275,6 +278,7 @@ struct Engine {
                             ++S->number_lo_iterations;
                             double sc = best_min_score;
                             local_opt(S->best_solver_type, &rng, &best_min, &sc, &S->best_solver_type);
+                            if (std::getenv("ORACLE_TRACE")) std::fprintf(stderr, "[oracle] it=%u LO %.17g -> %.17g\n", it, best_min_score, sc);
                             update_best(sc, best_min, st, &S->best_model_score, best, &S->best_solver_type);
                         }
                         termination(*best, S, &max_per);
