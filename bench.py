@@ -73,6 +73,73 @@ def cpu_baseline(wl, pair, budget_s=15.0):
                       f"{st.num_hypotheses} hypotheses, {st.number_lo_iterations} LO runs"}
 
 
+COUNTERS = ["elapsed_s", "hypotheses", "iterations", "lo_runs", "lo_s", "score_ms", "solve_ms", "prof_hypotheses",
+            "prof_correspondences", "prof_batches", "prof_sweeps"]
+
+
+def gather_counters(local, world):
+    """All ranks' counter vectors (world x len(COUNTERS)) -- the only collective of the
+    bench: one all_gather of a few doubles per rank (RCCL on GPUs, gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(local, dtype=torch.float64)
+    if world == 1:
+        return t.numpy()[None]
+    out = [torch.zeros_like(t) for _ in range(world)]
+    if dist.get_backend() == "nccl":
+        gl = [g.cuda() for g in out]
+        dist.all_gather(gl, t.cuda())
+        out = [g.cpu() for g in gl]
+    else:
+        dist.all_gather(out, t)
+    return torch.stack(out).numpy()
+
+
+def summarize(allv, wl, steps, warmup, world):
+    """Whole-job JSON record from the gathered counters: value = all ranks' hypotheses
+    divided by the slowest rank's wall time (weak scaling)."""
+    c = {k: allv[:, i] for i, k in enumerate(COUNTERS)}
+    t_max = float(c["elapsed_s"].max())
+    score_ms = float(c["score_ms"].sum())
+    achieved = float(c["prof_correspondences"].sum()) * BYTES_PER_CORR / (score_ms * 1e-3) / 1e9 if score_ms > 0 else 0.0
+    launches = int(c["prof_batches"].sum())
+    return {
+        "metric": "RANSAC hypotheses/sec + image-pairs/sec on 1xMI355X",
+        "value": float(c["hypotheses"].sum()) / t_max,
+        "unit": "hypotheses/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": t_max / steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded pairs per SURVEY.md §8d; no datasets on the box)",
+        "config": {"workload": wl["name"], "n_correspondences": wl["n"], "iterations": wl["iterations"],
+                   "pairs_per_step_per_gpu": 1, "parallelism": f"pairs sharded over {world} rank(s)"},
+        "pairs_per_s": world * steps / t_max,
+        "iterations_per_s": float(c["iterations"].sum()) / t_max,
+        "lo_runs": int(c["lo_runs"].sum()),
+        "lo_share": float(c["lo_s"].sum() / c["elapsed_s"].sum()),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "score_batch_kernel",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "launches": launches,
+            "avg_launch_us": score_ms * 1e3 / max(launches, 1),
+            "bytes_per_hypothesis": BYTES_PER_CORR * wl["n"],
+            "solve_ms_per_launch": float(c["solve_ms"].sum()) / max(launches, 1),
+        },
+        "cpu_baseline": None,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,62 +198,11 @@ def main():
     madpose.profile_enable(False)
     prof = madpose.profile_read()
 
-    local = torch.tensor([elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
-                          prof["correspondences"], prof["batches"], prof["sweeps"]], dtype=torch.float64)
-    if world > 1:
-        gathered = [torch.zeros_like(local) for _ in range(world)]
-        if dist.get_backend() == "nccl":
-            lc = local.cuda()
-            gl = [g.cuda() for g in gathered]
-            dist.all_gather(gl, lc)
-            gathered = [g.cpu() for g in gl]
-        else:
-            dist.all_gather(gathered, local)
-        allv = torch.stack(gathered).numpy()
-    else:
-        allv = local.numpy()[None]
-
+    local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
+             prof["correspondences"], prof["batches"], prof["sweeps"]]
+    allv = gather_counters(local, world)
     if rank == 0:
-        t_max = float(allv[:, 0].max())
-        tot_h, tot_it, tot_lo = allv[:, 1].sum(), allv[:, 2].sum(), allv[:, 3].sum()
-        score_ms = allv[:, 5].sum()
-        corr = allv[:, 8].sum()
-        achieved = corr * BYTES_PER_CORR / (score_ms * 1e-3) / 1e9 if score_ms > 0 else 0.0
-        launches = int(allv[:, 9].sum())
-        res = {
-            "metric": "RANSAC hypotheses/sec + image-pairs/sec on 1xMI355X",
-            "value": tot_h / t_max,
-            "unit": "hypotheses/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": t_max / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (seeded pairs per SURVEY.md §8d; no datasets on the box)",
-            "config": {"workload": wl["name"], "n_correspondences": wl["n"], "iterations": wl["iterations"],
-                       "pairs_per_step_per_gpu": 1, "parallelism": f"pairs sharded over {world} rank(s)"},
-            "pairs_per_s": world * a.steps / t_max,
-            "iterations_per_s": tot_it / t_max,
-            "lo_runs": int(tot_lo),
-            "lo_share": float(allv[:, 4].sum() / allv[:, 0].sum()),
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "score_batch_kernel",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
-                "launches": launches,
-                "avg_launch_us": score_ms * 1e3 / max(launches, 1),
-                "bytes_per_hypothesis": BYTES_PER_CORR * wl["n"],
-                "solve_ms_per_launch": float(allv[:, 6].sum() / max(launches, 1)),
-            },
-            "cpu_baseline": None,
-        }
+        res = summarize(allv, wl, a.steps, a.warmup, world)
         if world == 1 and a.cpu_budget > 0:
             res["cpu_baseline"] = cpu_baseline(wl, pairs[a.warmup], a.cpu_budget)
         print(json.dumps(res), flush=True)
