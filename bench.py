@@ -74,7 +74,7 @@ def cpu_baseline(wl, pair, budget_s=15.0):
 
 
 COUNTERS = ["elapsed_s", "hypotheses", "iterations", "lo_runs", "lo_s", "score_ms", "solve_ms", "prof_hypotheses",
-            "prof_correspondences", "prof_batches", "prof_sweeps"]
+            "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms"]
 
 
 def gather_counters(local, world):
@@ -123,6 +123,8 @@ def summarize(allv, wl, steps, warmup, world):
         "iterations_per_s": float(c["iterations"].sum()) / t_max,
         "lo_runs": int(c["lo_runs"].sum()),
         "lo_share": float(c["lo_s"].sum() / c["elapsed_s"].sum()),
+        "lo_breakdown": {"lm_calls": int(c["lm_calls"].sum()), "lm_ms": float(c["lm_ms"].sum()),
+                         "sweeps": int(c["prof_sweeps"].sum()), "sweep_ms": float(c["sweep_ms"].sum())},
         "roofline": {
             "bound": "hbm",
             "kernel": "score_batch_kernel",
@@ -199,7 +201,8 @@ def main():
     prof = madpose.profile_read()
 
     local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
-             prof["correspondences"], prof["batches"], prof["sweeps"]]
+             prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
+             prof["sweep_wall_ms"]]
     allv = gather_counters(local, world)
     if rank == 0:
         res = summarize(allv, wl, a.steps, a.warmup, world)

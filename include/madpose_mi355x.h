@@ -163,6 +163,9 @@ typedef struct mp_kernel_profile {
     uint64_t sweeps;          /* single-model LO / termination sweeps       */
     double solve_ms;          /* md_solve + pt_solve kernels                */
     double score_ms;          /* score_batch kernel                         */
+    uint64_t lm_calls;        /* host LM solves inside LO                   */
+    double lm_wall_ms;        /* host wall time spent in the LM             */
+    double sweep_wall_ms;     /* host wall time of LO sweeps (incl. copies) */
 } mp_kernel_profile;
 int mp_profile_enable(int on);
 int mp_profile_reset(void);

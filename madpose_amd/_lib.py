@@ -96,6 +96,9 @@ class mp_kernel_profile(ctypes.Structure):
         ("sweeps", ctypes.c_uint64),
         ("solve_ms", ctypes.c_double),
         ("score_ms", ctypes.c_double),
+        ("lm_calls", ctypes.c_uint64),
+        ("lm_wall_ms", ctypes.c_double),
+        ("sweep_wall_ms", ctypes.c_double),
     ]
 
 

@@ -308,6 +308,9 @@ int mp_profile_read(mp_kernel_profile *out) {
     out->sweeps = p.sweeps;
     out->solve_ms = p.solve_ms;
     out->score_ms = p.score_ms;
+    out->lm_calls = p.lm_calls;
+    out->lm_wall_ms = p.lm_wall_ms;
+    out->sweep_wall_ms = p.sweep_wall_ms;
     return MP_OK;
 }
 

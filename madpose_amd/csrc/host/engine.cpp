@@ -345,6 +345,7 @@ class Run {
             *score = cache_score_;
             return err_.data();
         }
+        auto t_sw = Clock::now();
         prepare_score_rec(P_.C, m, X_.h_rec1[0]);
         MP_HIP(hipMemcpyAsync(X_.d_rec1, X_.h_rec1, sizeof(ScoreRec), hipMemcpyHostToDevice, X_.stream));
         MP_HIP(launch_sweep(X_.stream, D_, P_.C, X_.d_rec1, X_.d_err, X_.d_score1));
@@ -357,8 +358,10 @@ class Run {
         cache_valid_ = true;
         S_->num_lo_sweeps++;
         if (g_prof_on.load(std::memory_order_relaxed)) {
+            const double dt = secs(t_sw);
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.sweeps += 1;
+            g_prof.sweep_wall_ms += 1e3 * dt;
         }
         *score = cache_score_;
         return err_.data();
@@ -430,7 +433,14 @@ class Run {
         S.gtol = cfg_.gtol;
         S.ptol = cfg_.ptol;
         S.max_iter = (int)cfg_.max_iter;
+        auto t_lm = Clock::now();
         lm_refine(P_.H, sample, S, m);
+        if (g_prof_on.load(std::memory_order_relaxed)) {
+            const double dt = secs(t_lm);
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            g_prof.lm_calls += 1;
+            g_prof.lm_wall_ms += 1e3 * dt;
+        }
     }
 
     static void split(const std::vector<int> &all, int n, std::vector<int> out[3]) {

@@ -79,6 +79,9 @@ struct KernelProfile {
     uint64_t sweeps = 0;           // single-model LO / termination sweeps
     double solve_ms = 0.0;         // md_solve + pt_solve
     double score_ms = 0.0;         // score_batch
+    uint64_t lm_calls = 0;         // host LM solves inside LO
+    double lm_wall_ms = 0.0;       // host wall time in the LM
+    double sweep_wall_ms = 0.0;    // host wall time of single-model sweeps (incl. copies + sync)
 };
 void profile_enable(bool on);
 void profile_reset();

@@ -2,6 +2,12 @@
 #include "lm.h"
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstring>
 
@@ -46,38 +52,140 @@ struct Ctx {
     int n;
 };
 
-// Accumulates one residual row r with full-layout gradient gfull into H, g, cost.
-inline void acc_row(const Ctx &C, double r, const double *gfull, double *H, double *g, double *cost) {
-    double j[kNFull];
-    int idx[kNFull], m = 0;
-    for (int k = 0; k < kNFull; ++k)
-        if (C.col[k] >= 0) {
-            idx[m] = C.col[k];
-            j[m] = gfull[k];
-            ++m;
-        }
-    *cost += 0.5 * r * r;
-    for (int a = 0; a < m; ++a) {
-        g[idx[a]] += j[a] * r;
-        for (int b = 0; b < m; ++b) H[idx[a] * C.n + idx[b]] += j[a] * j[b];
+// Normal-equation accumulator in the full parameter layout (packed upper triangle).
+// Inactive parameters accumulate harmlessly and are dropped by scatter().
+constexpr int kNPack = kNFull * (kNFull + 1) / 2;
+struct Acc {
+    double H[kNPack];
+    double g[kNFull];
+    double cost;
+    void clear() {
+        std::memset(H, 0, sizeof(H));
+        std::memset(g, 0, sizeof(g));
+        cost = 0.0;
     }
-}
+    void add(double r, const double *gf) {
+        cost += 0.5 * r * r;
+        int q = 0;
+        for (int a = 0; a < kNFull; ++a) {
+            g[a] += gf[a] * r;
+            const double ja = gf[a];
+            for (int b = a; b < kNFull; ++b) H[q++] += ja * gf[b];
+        }
+    }
+    void merge(const Acc &o) {
+        for (int q = 0; q < kNPack; ++q) H[q] += o.H[q];
+        for (int a = 0; a < kNFull; ++a) g[a] += o.g[a];
+        cost += o.cost;
+    }
+    void scatter(const Ctx &C, double *Hn, double *gn) const {
+        std::memset(Hn, 0, sizeof(double) * C.n * C.n);
+        std::memset(gn, 0, sizeof(double) * C.n);
+        int q = 0;
+        for (int a = 0; a < kNFull; ++a) {
+            const int ca = C.col[a];
+            if (ca >= 0) gn[ca] = g[a];
+            for (int b = a; b < kNFull; ++b, ++q) {
+                const int cb = C.col[b];
+                if (ca >= 0 && cb >= 0) Hn[ca * C.n + cb] = Hn[cb * C.n + ca] = H[q];
+            }
+        }
+    }
+};
 
 // Evaluates cost (and, when H != nullptr, normal equations) at parameters p.
-double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
+// Small persistent pool for the residual loop of large LM problems (the LO's
+// all-inlier fits).  MADPOSE_LO_THREADS sets its size (default 1 = off: an LM
+// iteration is ~10-100 us of work, comparable to a thread wake-up).
+constexpr size_t kChunk = 256;
+class Pool {
+  public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n - 1; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    // runs f(k) for k in [0, n); the calling thread takes part
+    void run(size_t n, const std::function<void(size_t)> &f) {
+        if (th_.empty() || n < 2) {
+            for (size_t k = 0; k < n; ++k) f(k);
+            return;
+        }
+        std::lock_guard<std::mutex> job(job_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            f_ = &f;
+            n_ = n;
+            next_.store(0);
+            active_ = (int)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return active_ == 0; });
+        f_ = nullptr;
+    }
+
+  private:
+    void work() {
+        for (size_t k; (k = next_.fetch_add(1)) < n_;) (*f_)(k);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--active_ == 0) done_cv_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, job_mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t)> *f_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    int active_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+Pool &lo_pool() {
+    static Pool pool([] {
+        const char *e = std::getenv("MADPOSE_LO_THREADS");
+        const int n = e ? std::atoi(e) : 1;
+        return std::max(1, std::min(n, 64));
+    }());
+    return pool;
+}
+
+// Residual blocks [b0, b1) of the concatenated block list (reproj0, reproj1, Sampson)
+// into acc; with jac == false only the cost is accumulated (in the same order).
+void evaluate_range(const Ctx &C, const Params &p, bool jac, size_t b0, size_t b1, Acc &acc) {
     const HostPair &P = *C.P;
     const bool cal = P.variant == kCal;
     const bool sf = P.variant == kSF;
     const double f0 = p.f0, f1 = sf ? p.f0 : p.f1;
-    double cost = 0.0;
-    if (H) {
-        std::memset(H, 0, sizeof(double) * C.n * C.n);
-        std::memset(g, 0, sizeof(double) * C.n);
-    }
+    double &cost = acc.cost;
+    const size_t n0 = C.S.use_reproj ? C.sample[0].size() : 0, n1 = C.S.use_reproj ? C.sample[1].size() : 0;
+    const size_t n2 = C.S.use_sampson ? C.sample[2].size() : 0;
     const double *R = p.R, *t = p.t;
-    if (C.S.use_reproj) {
+    if (n0 > 0 && b0 < n0) {
         // LiftProjectionFunctor0 and variants: x1_hat = K1 (R c0 (d0 + o0) + t)
-        for (int i : C.sample[0]) {
+        for (size_t bi = b0; bi < std::min(b1, n0); ++bi) {
+            const int i = C.sample[0][bi];
             double c[3];
             const double xh[3] = {P.x0[2 * i], P.x0[2 * i + 1], 1.0};
             if (cal)
@@ -101,8 +209,9 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
             }
             const double iz = 1.0 / h[2];
             const double r0 = h[0] * iz - P.x1[2 * i], r1 = h[1] * iz - P.x1[2 * i + 1];
-            if (!H) {
-                cost += 0.5 * (r0 * r0 + r1 * r1);
+            if (!jac) {
+                cost += 0.5 * r0 * r0;
+                cost += 0.5 * r1 * r1;
                 continue;
             }
             // dr/dh
@@ -143,11 +252,14 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
                         gf[kF1] = dhf1;
                     }
                 }
-                acc_row(C, rr == 0 ? r0 : r1, gf, H, g, &cost);
+                acc.add(rr == 0 ? r0 : r1, gf);
             }
         }
+    }
+    if (n1 > 0 && b1 > n0 && b0 < n0 + n1) {
         // LiftProjectionFunctor1: x0_hat = K0 R^T (c1 (d1 + o1) s - t)
-        for (int i : C.sample[1]) {
+        for (size_t bi = std::max(b0, n0); bi < std::min(b1, n0 + n1); ++bi) {
+            const int i = C.sample[1][bi - n0];
             double c[3];
             const double xh[3] = {P.x1[2 * i], P.x1[2 * i + 1], 1.0};
             if (cal)
@@ -171,8 +283,9 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
             }
             const double iz = 1.0 / h[2];
             const double r0 = h[0] * iz - P.x0[2 * i], r1 = h[1] * iz - P.x0[2 * i + 1];
-            if (!H) {
-                cost += 0.5 * (r0 * r0 + r1 * r1);
+            if (!jac) {
+                cost += 0.5 * r0 * r0;
+                cost += 0.5 * r1 * r1;
                 continue;
             }
             const double Dh[2][3] = {{iz, 0, -h[0] * iz * iz}, {0, iz, -h[1] * iz * iz}};
@@ -217,11 +330,11 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
                         gf[kF1] = dyf1;
                     }
                 }
-                acc_row(C, rr == 0 ? r0 : r1, gf, H, g, &cost);
+                acc.add(rr == 0 ? r0 : r1, gf);
             }
         }
     }
-    if (C.S.use_sampson) {
+    if (n2 > 0 && b1 > n0 + n1) {
         // SampsonError*Functor: r = w C / |(e0, e1, g0, g1)|
         double Tx[9], E[9];
         skew(t, Tx);
@@ -236,7 +349,7 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
             for (int c = 0; c < 3; ++c) F[3 * r + c] = E[3 * r + c] * s1[r] * s0[c];
         // derivative building blocks: dE/dt_k = [e_k]x R, dE/ddelta_k = 2 [t]x [e_k]x R
         double dEt[3][9], dEd[3][9];
-        if (H) {
+        if (jac) {
             for (int k = 0; k < 3; ++k) {
                 double ek[3] = {0, 0, 0};
                 ek[k] = 1.0;
@@ -247,7 +360,8 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
                 for (int e = 0; e < 9; ++e) dEd[k][e] *= 2.0;
             }
         }
-        for (int i : C.sample[2]) {
+        for (size_t bi = std::max(b0, n0 + n1); bi < std::min(b1, n0 + n1 + n2); ++bi) {
+            const int i = C.sample[2][bi - n0 - n1];
             double a[3], b[3];
             if (cal) {
                 const double xa[3] = {P.x0[2 * i], P.x0[2 * i + 1], 1.0}, xb[3] = {P.x1[2 * i], P.x1[2 * i + 1], 1.0};
@@ -269,7 +383,7 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
             const double D = e0 * e0 + e1 * e1 + g0 * g0 + g1 * g1;
             const double sD = std::sqrt(D);
             const double r = C.S.w_sampson * Cc / sD;
-            if (!H) {
+            if (!jac) {
                 cost += 0.5 * r * r;
                 continue;
             }
@@ -310,10 +424,37 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
                     gf[kF1] = df1;
                 }
             }
-            acc_row(C, r, gf, H, g, &cost);
+            acc.add(r, gf);
         }
     }
-    return cost;
+}
+
+size_t num_blocks(const Ctx &C) {
+    return (C.S.use_reproj ? C.sample[0].size() + C.sample[1].size() : 0) +
+           (C.S.use_sampson ? C.sample[2].size() : 0);
+}
+
+// Evaluates cost (and, when H != nullptr, the active normal equations) at p.  Blocks
+// are reduced in fixed chunks in chunk order, so the result does not depend on how
+// many worker threads evaluate them.
+double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
+    const size_t nb = num_blocks(C);
+    const size_t nchunks = (nb + kChunk - 1) / kChunk;
+    const bool jac = H != nullptr;
+    Acc total;
+    total.clear();
+    if (nchunks <= 1) {
+        evaluate_range(C, p, jac, 0, nb, total);
+    } else {
+        std::vector<Acc> parts(nchunks);
+        lo_pool().run(nchunks, [&](size_t k) {
+            parts[k].clear();
+            evaluate_range(C, p, jac, k * kChunk, std::min(nb, (k + 1) * kChunk), parts[k]);
+        });
+        for (size_t k = 0; k < nchunks; ++k) total.merge(parts[k]);
+    }
+    if (jac) total.scatter(C, H, g);
+    return total.cost;
 }
 
 bool chol_solve(std::vector<double> A, int n, std::vector<double> b, std::vector<double> *x) {
@@ -442,7 +583,7 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
         return p.q[0] * p.q[0] + p.q[1] * p.q[1] + p.q[2] * p.q[2] + p.q[3] * p.q[3] + p.t[0] * p.t[0] +
                p.t[1] * p.t[1] + p.t[2] * p.t[2] + p.s * p.s + p.o0 * p.o0 + p.o1 * p.o1 + p.f0 * p.f0 + p.f1 * p.f1;
     };
-    std::vector<double> H(n * n), g(n);
+    std::vector<double> H(n * n), g(n), Hc(n * n), gc(n);
     double cost = evaluate(C, x, H.data(), g.data());
     auto gmax = [&]() {
         double v = 0;
@@ -505,7 +646,9 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
                 for (double e : dd) step2 += e * e;
             }
             const double step_norm = std::sqrt(step2), xnorm = std::sqrt(amb_norm2(x));
-            const double cand_cost = evaluate(C, c, nullptr, nullptr);
+            // the candidate is evaluated with its normal equations: accepted steps
+            // (the common case) then need no second pass
+            const double cand_cost = evaluate(C, c, Hc.data(), gc.data());
             if (step_norm <= S.ptol * (xnorm + S.ptol)) break;
             if (std::fabs(cost - cand_cost) <= S.ftol * cost) break;
             double gd = 0, jd2 = 0;
@@ -517,7 +660,9 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
             const double rho = (mcc > 0 && std::isfinite(cand_cost)) ? (cost - cand_cost) / mcc : -1.0;
             if (rho > 1e-3) {
                 x = c;
-                cost = evaluate(C, x, H.data(), g.data());
+                cost = cand_cost;
+                H.swap(Hc);
+                g.swap(gc);
                 radius = std::min(1e16, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3)));
                 decrease = 2.0;
                 if (gmax() <= S.gtol) break;
