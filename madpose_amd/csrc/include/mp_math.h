@@ -207,9 +207,27 @@ template <int N> MP_HD double refine_root(const double *c, double lo, double hi)
     if (flo == 0.0) return lo;
     if (fhi == 0.0) return hi;
     if ((flo < 0) == (fhi < 0)) return 0.5 * (lo + hi); // even multiplicity: midpoint
+    // a few plain bisection steps first (only the sign of p is needed), so that the
+    // Newton phase starts close to the root and rarely falls back to bisection
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        double fm = 0.0;
+#pragma unroll
+        for (int j = N; j >= 0; --j) fm = fm * mid + c[j];
+        if (fm == 0.0) return mid;
+        if ((fm < 0) == (flo < 0))
+            lo = mid;
+        else
+            hi = mid;
+    }
+    // safeguarded Newton: a Newton step that leaves the bracket is replaced by
+    // bisection; stop once the step is within a few ulps (Newton then oscillates
+    // between neighbouring doubles and a tighter test would never fire)
     double x = 0.5 * (lo + hi);
-    for (int it = 0; it < 100; ++it) {
+    for (int it = 0; it < 60; ++it) {
         double f = 0.0, df = 0.0;
+#pragma unroll
         for (int j = N; j >= 0; --j) {
             df = df * x + f;
             f = f * x + c[j];
@@ -221,71 +239,110 @@ template <int N> MP_HD double refine_root(const double *c, double lo, double hi)
             hi = x;
         double xn = x - f / df;
         if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
-        if (fabs(xn - x) <= 1e-16 * fabs(xn) || hi - lo <= 1e-16 * fmax(fabs(lo), fabs(hi))) return xn;
+        if (fabs(xn - x) <= 4e-16 * fabs(xn) || hi - lo <= 4e-16 * fmax(fabs(lo), fabs(hi))) return xn;
         x = xn;
     }
     return x;
+}
+
+// Isolating intervals collected per lane before any refinement, so that the
+// refinement loop of a wave runs max(#roots) times instead of once per grid cell
+// that holds a root on any lane.  Writes use static indices (registers).
+template <int N> struct RootIntervals {
+    double lo[N], hi[N];
+    int n = 0;
+    MP_HD void push(double a, double b) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (k == n) {
+                lo[k] = a;
+                hi[k] = b;
+            }
+        if (n < N) ++n;
+    }
+};
+
+// Roots in (lo, hi] (Sturm counts clo > chi) isolated left to right by bisection
+// without a stack: shrink onto the leftmost root, record it, continue to its right.
+// A cluster narrower than 1e-14 (relative) yields one root.  Used only for grid
+// cells that hold several roots.
+template <int N>
+MP_HD void sturm_isolate(const SturmChain<N> &S, double lo, double hi, int clo, int chi, RootIntervals<N> &I) {
+    for (int guard = 0; guard < N && clo > chi; ++guard) {
+        double a = lo, b = hi;
+        int ca = clo, cb = chi;
+        for (int depth = 0; depth < 100; ++depth) {
+            if (ca - cb == 1 || b - a <= 1e-14 * fmax(1.0, fmax(fabs(a), fabs(b)))) break;
+            const double m = 0.5 * (a + b);
+            const int cm = sturm_count<N>(S, m);
+            if (ca - cm >= 1) {
+                b = m;
+                cb = cm;
+            } else {
+                a = m;
+                ca = cm;
+            }
+        }
+        I.push(a, b);
+        lo = b;
+        clo = cb;
+    }
 }
 
 template <int N> MP_HD int sturm_real_roots(const double *c_in, double *roots) {
     // trim leading zeros is the caller's job; normalise to avoid overflow
     double c[N + 1], cs[N + 1];
     double mx = 0.0;
+#pragma unroll
     for (int j = 0; j <= N; ++j) mx = fmax(mx, fabs(c_in[j]));
     if (!(mx > 0.0) || !(fabs(c_in[N]) > 1e-300)) return 0;
-    for (int j = 0; j <= N; ++j) c[j] = c_in[j] / c_in[N]; // monic
+    const double lead = 1.0 / c_in[N];
+#pragma unroll
+    for (int j = 0; j <= N; ++j) c[j] = c_in[j] * lead; // monic
     // rescale x = sigma * y so the roots are O(1) (Fujiwara-type root-size estimate);
-    // the chain is built and bisected on the scaled polynomial, roots are refined on c.
+    // the chain is built and searched on the scaled polynomial, roots are refined on c.
     double sigma = 0.0;
+#pragma unroll
     for (int j = 0; j < N; ++j)
         if (c[j] != 0.0) sigma = fmax(sigma, pow(fabs(c[j]), 1.0 / (N - j)));
     if (!(sigma > 0.0) || !(sigma < 1e300)) sigma = 1.0;
     {
+        const double inv = 1.0 / sigma;
         double p = 1.0;
-        for (int j = 0; j <= N; ++j) {
-            cs[j] = c[j] * p / pow(sigma, (double)N);
-            p *= sigma;
-        }
         cs[N] = 1.0;
+#pragma unroll
+        for (int j = N - 1; j >= 0; --j) {
+            p *= inv;
+            cs[j] = c[j] * p;
+        }
     }
     const double B = 3.0; // all roots of the scaled monic polynomial satisfy |y| <= 2
     SturmChain<N> S;
     sturm_build<N>(cs, S);
-    // Isolation: keep walking down the lower half of the current interval and park
-    // the upper halves that still hold roots.  Parked intervals are disjoint and each
-    // holds >= 1 root, so at most N are pending; output is ascending.
-    double st_lo[N + 1], st_hi[N + 1];
-    int st_clo[N + 1], st_chi[N + 1];
-    int sp = 1, nr = 0;
-    st_lo[0] = -B;
-    st_hi[0] = B;
-    st_clo[0] = sturm_count<N>(S, -B);
-    st_chi[0] = sturm_count<N>(S, B);
-    while (sp > 0) {
-        --sp;
-        double lo = st_lo[sp], hi = st_hi[sp];
-        int clo = st_clo[sp], chi = st_chi[sp];
-        for (int depth = 0; depth < 200; ++depth) {
-            const int k = clo - chi;
-            if (k <= 0) break;
-            if (k == 1 || hi - lo <= 1e-14 * fmax(1.0, fmax(fabs(lo), fabs(hi)))) {
-                if (nr < N) roots[nr++] = refine_root<N>(c, sigma * lo, sigma * hi);
-                break;
-            }
-            const double mid = 0.5 * (lo + hi);
-            const int cm = sturm_count<N>(S, mid);
-            if (cm - chi > 0 && sp <= N) {
-                st_lo[sp] = mid;
-                st_hi[sp] = hi;
-                st_clo[sp] = cm;
-                st_chi[sp] = chi;
-                ++sp;
-            }
-            hi = mid;
-            chi = cm;
-        }
+    // Isolation on a uniform grid of kCells cells (the same work on every lane of a
+    // wave); cells with several roots are split by stackless bisection.  Then every
+    // isolated root is refined.  Output is ascending.
+    constexpr int kCells = 32;
+    const double h = 2.0 * B / kCells;
+    const int c_end = sturm_count<N>(S, B);
+    double x_lo = -B;
+    int v_lo = sturm_count<N>(S, -B);
+    RootIntervals<N> I;
+    for (int i = 0; i < kCells && v_lo > c_end; ++i) {
+        const double x_hi = (i + 1 == kCells) ? B : -B + (i + 1) * h;
+        const int v_hi = (i + 1 == kCells) ? c_end : sturm_count<N>(S, x_hi);
+        const int d = v_lo - v_hi;
+        if (d == 1)
+            I.push(x_lo, x_hi);
+        else if (d > 1)
+            sturm_isolate<N>(S, x_lo, x_hi, v_lo, v_hi, I);
+        x_lo = x_hi;
+        v_lo = v_hi;
     }
-    return nr;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if (k < I.n) roots[k] = refine_root<N>(c, sigma * I.lo[k], sigma * I.hi[k]);
+    return I.n;
 }
 
 // ---------------------------------------------------------------------------

@@ -211,8 +211,16 @@ MP_HD void nullspace_5x9(const double (&Q)[5][9], double (&N)[4][9]) {
     }
 }
 
-// relpose_5pt on unit bearings; returns number of poses written (<= kmax).
-MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model *out, int kmax) {
+// The 5-point system of one sample: null-space basis, the hidden-variable matrix
+// B(z) and its degree-10 determinant (ascending coefficients).
+struct FivePtSys {
+    double N[4][9];
+    double Bx[3][4], By[3][4], B1[3][5];
+    double d10[11];
+};
+
+// Builds the system; false when the 10x20 elimination hits a zero pivot.
+MP_HD bool fivept_system(const double (&x1)[5][3], const double (&x2)[5][3], FivePtSys &S) {
     double Q[5][9];
 #pragma unroll
     for (int i = 0; i < 5; ++i)
@@ -220,7 +228,7 @@ MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model 
         for (int r = 0; r < 3; ++r)
 #pragma unroll
             for (int c = 0; c < 3; ++c) Q[i][3 * r + c] = x2[i][r] * x1[i][c];
-    double N[4][9];
+    double (&N)[4][9] = S.N;
     nullspace_5x9(Q, N);
     Lin E[9];
 #pragma unroll
@@ -303,7 +311,7 @@ MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model 
                 best = fabs(M[r][k]);
                 p = r;
             }
-        if (!(best > 0.0)) return 0;
+        if (!(best > 0.0)) return false;
 #pragma unroll
         for (int r = k + 1; r < 10; ++r)
             if (r == p) {
@@ -327,7 +335,9 @@ MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model 
         }
     }
     // B(z): rows (e - z f), (g - z h), (i - z j)
-    double Bx[3][4], By[3][4], B1[3][5];
+    double (&Bx)[3][4] = S.Bx;
+    double (&By)[3][4] = S.By;
+    double (&B1)[3][5] = S.B1;
     const int ra[3] = {4, 6, 8}, rb[3] = {5, 7, 9};
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -347,7 +357,8 @@ MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model 
         B1[q][4] = -b[16];
     }
     // det = Bx0 (By1 B12 - B11 By2) - By0 (Bx1 B12 - B11 Bx2) + B10 (Bx1 By2 - By1 Bx2)
-    double t7a[8], t7b[8], t6a[7], t6b[7], d10[11];
+    double t7a[8], t7b[8], t6a[7], t6b[7];
+    double (&d10)[11] = S.d10;
 #pragma unroll
     for (int i = 0; i < 11; ++i) d10[i] = 0.0;
     double t10[11];
@@ -372,33 +383,44 @@ MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model 
     pmul<4, 6>(B1[0], t6a, t10);
 #pragma unroll
     for (int i = 0; i < 11; ++i) d10[i] += t10[i];
-    double roots[10];
-    const int nr = sturm_real_roots<10>(d10, roots);
-    int nout = 0;
-    for (int r = 0; r < nr; ++r) {
-        const double z = roots[r];
-        double Bm[3][3];
+    return true;
+}
+
+// Poses of one real root z of det B(z): (x, y) from the null vector of B(z), E, and
+// motion_from_essential with cheirality on the five points.  Appends at out[k..].
+MP_HD int fivept_poses_for_root(const FivePtSys &S, double z, const double (&x1)[5][3], const double (&x2)[5][3],
+                                Model *out, int k, int kmax) {
+    double Bm[3][3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            Bm[q][0] = peval<3>(Bx[q], z);
-            Bm[q][1] = peval<3>(By[q], z);
-            Bm[q][2] = peval<4>(B1[q], z);
-        }
-        double v01[3], v02[3], v12[3];
-        cross3(Bm[0], Bm[1], v01);
-        cross3(Bm[0], Bm[2], v02);
-        cross3(Bm[1], Bm[2], v12);
-        const double n01 = dot3(v01, v01), n02 = dot3(v02, v02), n12 = dot3(v12, v12);
-        double v[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) v[c] = (n01 >= n02 && n01 >= n12) ? v01[c] : (n02 >= n12 ? v02[c] : v12[c]);
-        if (v[2] == 0.0) continue;
-        const double x = v[0] / v[2], y = v[1] / v[2];
-        double Ee[9];
-#pragma unroll
-        for (int e = 0; e < 9; ++e) Ee[e] = x * N[0][e] + y * N[1][e] + z * N[2][e] + N[3][e];
-        nout += motion_from_essential<5>(Ee, x1, x2, out, nout, kmax);
+    for (int q = 0; q < 3; ++q) {
+        Bm[q][0] = peval<3>(S.Bx[q], z);
+        Bm[q][1] = peval<3>(S.By[q], z);
+        Bm[q][2] = peval<4>(S.B1[q], z);
     }
+    double v01[3], v02[3], v12[3];
+    cross3(Bm[0], Bm[1], v01);
+    cross3(Bm[0], Bm[2], v02);
+    cross3(Bm[1], Bm[2], v12);
+    const double n01 = dot3(v01, v01), n02 = dot3(v02, v02), n12 = dot3(v12, v12);
+    double v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = (n01 >= n02 && n01 >= n12) ? v01[c] : (n02 >= n12 ? v02[c] : v12[c]);
+    if (v[2] == 0.0) return 0;
+    const double x = v[0] / v[2], y = v[1] / v[2];
+    double Ee[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) Ee[e] = x * S.N[0][e] + y * S.N[1][e] + z * S.N[2][e] + S.N[3][e];
+    return motion_from_essential<5>(Ee, x1, x2, out, k, kmax);
+}
+
+// relpose_5pt on unit bearings; returns number of poses written (<= kmax).
+MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model *out, int kmax) {
+    FivePtSys S;
+    if (!fivept_system(x1, x2, S)) return 0;
+    double roots[10];
+    const int nr = sturm_real_roots<10>(S.d10, roots);
+    int nout = 0;
+    for (int r = 0; r < nr; ++r) nout += fivept_poses_for_root(S, roots[r], x1, x2, out, nout, kmax);
     return nout;
 }
 

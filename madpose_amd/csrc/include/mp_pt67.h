@@ -528,6 +528,8 @@ MP_HD bool null_vector10(double (&A)[10][10], double (&v)[10]) {
     return true;
 }
 
+// kStop < 4 truncates the solver after stage kStop (tools/solver_bench.hip timing).
+template <int kStop = 4>
 MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Model *out, int kmax) {
     double Q[6][9], N[3][9];
     epipolar_rows<6>(x1, x2, Q);
@@ -606,6 +608,7 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
                 }
             }
     }
+    if (kStop == 0) return (int)(M[1][3][4] > 0);
     // q(u): first pass on |u| = 1, then on the geometric mean of the root moduli
     double c[16];
     pencil_poly15(M, 1.0, c);
@@ -615,8 +618,10 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
         if (!(rho > 0.0) || !(rho < 1e300)) rho = 1.0;
     }
     if (rho != 1.0) pencil_poly15(M, rho, c);
+    if (kStop == 1) return (int)(c[7] > 0);
     double roots[15];
     const int nr = sturm_real_roots<15>(c, roots);
+    if (kStop == 2) return nr;
     int nout = 0;
     for (int k = 0; k < nr; ++k) {
         if (!(roots[k] > 0.0)) continue;
@@ -655,6 +660,10 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
             w -= Jtr[2][0];
         }
         if (!(w > 0.0)) continue;
+        if (kStop == 3) {
+            nout += (x > y);
+            continue;
+        }
         const double foc = 1.0 / sqrt(w);
         double Fm[9], nn = 0.0;
 #pragma unroll
