@@ -119,6 +119,13 @@ int mp_solve_scale_and_shift(int variant, const double *x_homo, const double *y_
 int mp_solve_scale_shift_pose(int variant, const double *x_homo, const double *y_homo, const double *depth_x,
                               const double *depth_y, mp_model *out, int max_out, int device);
 
+/* Option-gated alternates of the MD solvers (HybridLORansacOptions::use_ours / use_4p4d):
+ * alt 1 = solve_scale_shift_pose{,_shared_focal,_two_focal}_ours (src/solver.cpp:623-680,
+ * 818-984, 1045-1148), alt 2 = solve_scale_shift_pose_two_focal_4p4d (:1287-1406).
+ * Same point layout as mp_solve_scale_shift_pose.  Returns count or -code. */
+int mp_solve_scale_shift_pose_alt(int variant, int alt, const double *x_homo, const double *y_homo,
+                                  const double *depth_x, const double *depth_y, mp_model *out, int max_out, int device);
+
 /* Batched device sweep over one pair's correspondences (ScoreModel / GetInliers,
  * src/hybrid_ransac.h:265-349) for num_models models given in problem units.
  * Used by tests to check the scoring kernel directly.  scores: num_models;

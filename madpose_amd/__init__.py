@@ -35,7 +35,11 @@ from .api import (  # noqa: F401
     solve_scale_and_shift_two_focal,
     solve_scale_shift_pose,
     solve_scale_shift_pose_shared_focal,
+    solve_scale_shift_pose_ours,
+    solve_scale_shift_pose_shared_focal_ours,
     solve_scale_shift_pose_two_focal,
+    solve_scale_shift_pose_two_focal_4p4d,
+    solve_scale_shift_pose_two_focal_ours,
     version,
 )
 from . import utils  # noqa: F401

@@ -116,6 +116,8 @@ EXPORTS = {
                                                 c_double_p, ctypes.c_int, ctypes.c_int]),
     "mp_solve_scale_shift_pose": (ctypes.c_int, [ctypes.c_int, c_double_p, c_double_p, c_double_p, c_double_p,
                                                  ctypes.POINTER(mp_model), ctypes.c_int, ctypes.c_int]),
+    "mp_solve_scale_shift_pose_alt": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, c_double_p,
+                                                     c_double_p, ctypes.POINTER(mp_model), ctypes.c_int, ctypes.c_int]),
     "mp_score_models": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p, c_double_p,
                                        c_double_p, c_double_p, ctypes.POINTER(mp_ransac_options),
                                        ctypes.POINTER(mp_estimator_config), ctypes.POINTER(mp_model), ctypes.c_int32,

@@ -419,14 +419,18 @@ def _solve_ss(variant, x_homo, y_homo, depth_x, depth_y):
     return [out[i * w:(i + 1) * w].copy() for i in range(n)]
 
 
-def _solve_pose(variant, x_homo, y_homo, depth_x, depth_y):
+def _solve_pose(variant, x_homo, y_homo, depth_x, depth_y, alt=0):
     k = 3 if variant == L.CALIBRATED else 4
     x = _homog_pm(x_homo, k, "x_homo")
     y = _homog_pm(y_homo, k, "y_homo")
     dx = _vec(depth_x, k, "depth_x")
     dy = _vec(depth_y, k, "depth_y")
     out = (L.mp_model * 8)()
-    n = L.lib().mp_solve_scale_shift_pose(variant, _dp(x), _dp(y), _dp(dx), _dp(dy), out, 8, _DEFAULT_DEVICE)
+    if alt:
+        n = L.lib().mp_solve_scale_shift_pose_alt(variant, alt, _dp(x), _dp(y), _dp(dx), _dp(dy), out, 8,
+                                                  _DEFAULT_DEVICE)
+    else:
+        n = L.lib().mp_solve_scale_shift_pose(variant, _dp(x), _dp(y), _dp(dx), _dp(dy), out, 8, _DEFAULT_DEVICE)
     if n < 0:
         L.check(-n)
     return [_model_from_c(out[i], variant) for i in range(n)]
@@ -493,6 +497,26 @@ def relpose_7pt_two_focal(x0, x1):
     """Device 7-point + Bougnoux + recoverPose on normalized 2-D points (7 x 2 each):
     PoseScaleOffsetTwoFocal candidates before the depth fit."""
     return _point_direct(L.lib().mp_relpose_7pt_two_focal, 7, L.TWO_FOCAL, x0, x1)
+
+
+def solve_scale_shift_pose_ours(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:623-680 (the use_ours calibrated MD solver)."""
+    return _solve_pose(L.CALIBRATED, x_homo, y_homo, depth_x, depth_y, alt=1)
+
+
+def solve_scale_shift_pose_shared_focal_ours(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:818-984 (the use_ours shared-focal MD solver)."""
+    return _solve_pose(L.SHARED_FOCAL, x_homo, y_homo, depth_x, depth_y, alt=1)
+
+
+def solve_scale_shift_pose_two_focal_ours(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:1045-1148 (the use_ours two-focal MD solver)."""
+    return _solve_pose(L.TWO_FOCAL, x_homo, y_homo, depth_x, depth_y, alt=1)
+
+
+def solve_scale_shift_pose_two_focal_4p4d(x_homo, y_homo, depth_x, depth_y):
+    """src/solver.cpp:1287-1406 (the use_4p4d two-focal solver)."""
+    return _solve_pose(L.TWO_FOCAL, x_homo, y_homo, depth_x, depth_y, alt=2)
 
 
 def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, models, with_errors=False):

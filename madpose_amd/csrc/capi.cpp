@@ -209,6 +209,22 @@ int mp_solve_scale_shift_pose(int variant, const double *x_homo, const double *y
     return r <= -1000 ? -(r + 1000) : -r;
 }
 
+int mp_solve_scale_shift_pose_alt(int variant, int alt, const double *x_homo, const double *y_homo,
+                                  const double *depth_x, const double *depth_y, mp_model *out, int max_out, int device) {
+    int r = guarded([&]() {
+        if (variant < 0 || variant > 2) throw std::invalid_argument("bad variant");
+        if (alt < 1 || alt > 2 || (alt == 2 && variant != 2))
+            throw std::invalid_argument("alt must be 1 (use_ours) or 2 (use_4p4d, two-focal only)");
+        double sols[48];
+        mp::Model poses[8];
+        int np = 0;
+        mp::solve_md_direct(variant, x_homo, y_homo, depth_x, depth_y, sols, 8, poses, 8, &np, device, alt);
+        for (int i = 0; i < std::min(np, max_out); ++i) to_model(poses[i], &out[i]);
+        return -(np + 1000);
+    });
+    return r <= -1000 ? -(r + 1000) : -r;
+}
+
 int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
                     const double *cam0, const double *cam1, const mp_ransac_options *options,
                     const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,

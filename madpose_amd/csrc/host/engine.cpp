@@ -202,6 +202,9 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
     C.score_type = cfg.score_type;
     C.min_depth_constraint = cfg.min_depth_constraint ? 1 : 0;
     C.use_shift = cfg.use_shift ? 1 : 0;
+    // option-gated MD alternates (src/hybrid_pose_estimator.cpp:75-78, ..shared..cpp:62-65,
+    // ..two..cpp:87-94); use_ours wins over use_4p4d, 4p4d exists for two-focal only
+    C.md_alt = o.use_ours ? 1 : ((o.use_4p4d && in.variant == kTF) ? 2 : 0);
     C.min_depth[0] = in.min_depth[0];
     C.min_depth[1] = in.min_depth[1];
     HostPair &H = P.H;
@@ -716,8 +719,7 @@ void validate(const PairInput &in, const RansacOptions &o) {
     if (in.n > 0 && (!in.x0 || !in.x1 || !in.d0 || !in.d1)) throw std::invalid_argument("null input array");
     if (!(o.squared_inlier_thresholds[0] > 0) || !(o.squared_inlier_thresholds[1] > 0))
         throw std::invalid_argument("squared_inlier_thresholds must hold two positive values");
-    if (o.use_ours || o.use_4p4d)
-        throw std::invalid_argument("use_ours / use_4p4d solvers are not implemented in this build");
+
 }
 
 } // namespace
@@ -780,7 +782,7 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
 }
 
 int solve_md_direct(int variant, const double *x, const double *y, const double *dx, const double *dy, double *sols,
-                    int max_sols, Model *poses, int max_poses, int *nposes, int device) {
+                    int max_sols, Model *poses, int max_poses, int *nposes, int device, int alt) {
     CtxLease lease(device);
     DeviceCtx &X = *lease.c;
     const int k = variant == kCal ? 3 : 4;
@@ -797,7 +799,7 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
     MP_HIP(hipMalloc(&d_n, sizeof(int) * 2));
     MP_HIP(hipMalloc(&d_poses, sizeof(Model) * 8));
     MP_HIP(hipMemcpyAsync(d_in, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, X.stream));
-    MP_HIP(launch_md_direct(X.stream, variant, d_in, d_sols, d_n, d_poses, d_n + 1));
+    MP_HIP(launch_md_direct(X.stream, variant, alt, d_in, d_sols, d_n, d_poses, d_n + 1));
     double hs[48];
     int hn[2];
     Model hp[8];

@@ -61,8 +61,9 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
                   int nm, double *scores, double *errors, int device, double *norm_scale);
 
 // Standalone solvers on the device (mp_solve_* / mp_relpose_5pt).
+// alt: 0 default MD solver, 1 use_ours, 2 use_4p4d (two-focal)
 int solve_md_direct(int variant, const double *x, const double *y, const double *dx, const double *dy, double *sols,
-                    int max_sols, Model *poses, int max_poses, int *nposes, int device);
+                    int max_sols, Model *poses, int max_poses, int *nposes, int device, int alt = 0);
 // kind 0: relpose_5pt on unit bearings; 1: shared-focal 6pt; 2: two-focal 7pt +
 // Bougnoux + recoverPose (normalized 2-D points).  Models before the depth fit.
 int solve_point_direct(int kind, const double *x1, const double *x2, Model *poses, int max_poses, int device);

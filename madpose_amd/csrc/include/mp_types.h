@@ -41,7 +41,7 @@ struct PairConst {
     int score_type; // 0 hybrid, 1 epi-only, 2 md-only (EstimatorConfig::score_type)
     int min_depth_constraint;
     int use_shift;
-    int pad0;
+    int md_alt; // 0 default MD solvers, 1 use_ours, 2 use_4p4d (two-focal)
     double K0[9], K1[9], K0i[9], K1i[9]; // identity for SF/TF (focal lives in the model)
     double thr[3], w[3];                 // squared thresholds / weights after the option transform
     double loss_scale;                   // calibrated Sampson scale (src/hybrid_pose_estimator.h:35-36)

@@ -29,7 +29,7 @@ hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst
                                double *scores);
 
 // standalone solvers (mp_solve_* C API): one sample, one thread
-hipError_t launch_md_direct(hipStream_t s, int variant, const double *in /* x(3K) y(3K) dx(K) dy(K) */,
+hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *in /* x(3K) y(3K) dx(K) dy(K) */,
                             double *sols, int *nsols, Model *poses, int *nposes);
 hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes);
 

@@ -12,7 +12,7 @@
 //  sweep<V>       one model, all points: errors for GetInliers + gated score
 #include <cfloat>
 
-#include "../include/mp_pt67.h"
+#include "../include/mp_md_alt.h"
 #include "../include/mp_score.h"
 #include "kernels.h"
 
@@ -100,6 +100,11 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
             m.focal0 = m.focal1 = 1.0;
             md_pose_noshift_cal(x, y, dx, dy, m);
             out[n++] = m;
+        } else if (C.md_alt == 1) {
+            Model tmp[4];
+            const int ns = md_pose_cal_ours(x, y, dx, dy, tmp);
+            for (int k = 0; k < ns; ++k)
+                if (md_accept(C, tmp[k])) out[n++] = tmp[k];
         } else {
             double sols[4][6];
             const int ns = md_sols_cal(x, y, dx, dy, sols);
@@ -122,6 +127,16 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
             y[j][2] = 1.0;
             dx[j] = D.d0[i];
             dy[j] = D.d1[i];
+        }
+        if (C.md_alt != 0) {
+            Model tmp[4];
+            const int ns = (V == kSF) ? md_pose_sf_ours(x, y, dx, dy, tmp)
+                                      : (C.md_alt == 1 ? md_pose_tf_ours(x, y, dx, dy, tmp)
+                                                       : md_pose_tf_4p4d(x, y, dx, dy, tmp));
+            for (int k = 0; k < ns; ++k)
+                if (md_accept(C, tmp[k])) out[n++] = tmp[k];
+            write_models(C, out, n, b, maxm, models, recs, counts);
+            return;
         }
         double sols[8][6];
         int ns;
@@ -359,9 +374,37 @@ __global__ void __launch_bounds__(kBlock) score_models_kernel(PairData D, PairCo
     }
 }
 
-__global__ void md_direct_kernel(int variant, const double *in, double *sols_out, int *nsols, Model *poses,
+__global__ void md_direct_kernel(int variant, int alt, const double *in, double *sols_out, int *nsols, Model *poses,
                                  int *nposes) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (variant == kCal && alt != 0) {
+        double x[3][3], y[3][3], dx[3], dy[3];
+        for (int j = 0; j < 3; ++j) {
+            for (int c = 0; c < 3; ++c) {
+                x[j][c] = in[3 * j + c];
+                y[j][c] = in[9 + 3 * j + c];
+            }
+            dx[j] = in[18 + j];
+            dy[j] = in[21 + j];
+        }
+        *nposes = *nsols = md_pose_cal_ours(x, y, dx, dy, poses);
+        return;
+    }
+    if (variant != kCal && alt != 0) {
+        double x[4][3], y[4][3], dx[4], dy[4];
+        for (int j = 0; j < 4; ++j) {
+            for (int c = 0; c < 3; ++c) {
+                x[j][c] = in[3 * j + c];
+                y[j][c] = in[12 + 3 * j + c];
+            }
+            dx[j] = in[24 + j];
+            dy[j] = in[28 + j];
+        }
+        *nposes = *nsols = (variant == kSF) ? md_pose_sf_ours(x, y, dx, dy, poses)
+                                            : (alt == 1 ? md_pose_tf_ours(x, y, dx, dy, poses)
+                                                        : md_pose_tf_4p4d(x, y, dx, dy, poses));
+        return;
+    }
     if (variant == kCal) {
         double x[3][3], y[3][3], dx[3], dy[3];
         for (int j = 0; j < 3; ++j) {
@@ -536,9 +579,9 @@ hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst
     });
 }
 
-hipError_t launch_md_direct(hipStream_t s, int variant, const double *in, double *sols, int *nsols, Model *poses,
+hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *in, double *sols, int *nsols, Model *poses,
                             int *nposes) {
-    md_direct_kernel<<<1, 64, 0, s>>>(variant, in, sols, nsols, poses, nposes);
+    md_direct_kernel<<<1, 64, 0, s>>>(variant, alt, in, sols, nsols, poses, nposes);
     return hipGetLastError();
 }
 

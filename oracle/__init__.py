@@ -128,6 +128,14 @@ def md_pose(variant, x_homo_pm, y_homo_pm, dx, dy):
     return [model_to_dict(out[i]) for i in range(min(n, 16))]
 
 
+def md_pose_alt(variant, alt, x_homo_pm, y_homo_pm, dx, dy):
+    """use_ours (alt=1) / use_4p4d (alt=2, two-focal) MD solvers; same layout as md_pose."""
+    out = (OrModel * 16)()
+    n = lib().oracle_md_pose_alt(variant, alt, _dp(_c(x_homo_pm)), _dp(_c(y_homo_pm)), _dp(_c(dx)), _dp(_c(dy)),
+                                 out, 16)
+    return [model_to_dict(out[i]) for i in range(min(n, 16))]
+
+
 def relpose_5pt(b1, b2):
     out = (OrModel * 32)()
     n = lib().oracle_relpose_5pt(_dp(_c(b1)), _dp(_c(b2)), out, 32)

@@ -104,6 +104,20 @@ int oracle_md_scale_shift(int variant, const double *x, const double *y, const d
     return (int)sols.size();
 }
 
+// alt: 1 = use_ours, 2 = use_4p4d (two-focal only)
+int oracle_md_pose_alt(int variant, int alt, const double *x, const double *y, const double *dx, const double *dy,
+                       or_model *out, int max_out) {
+    std::vector<oracle::Model> sols;
+    if (alt == 1)
+        sols = variant == 0 ? oracle::md_pose_cal_ours(x, y, dx, dy)
+                            : (variant == 1 ? oracle::md_pose_sf_ours(x, y, dx, dy) : oracle::md_pose_tf_ours(x, y, dx, dy));
+    else if (alt == 2 && variant == 2)
+        sols = oracle::md_pose_tf_4p4d(x, y, dx, dy);
+    int n = std::min((int)sols.size(), max_out);
+    for (int i = 0; i < n; ++i) put_model(sols[i], &out[i]);
+    return (int)sols.size();
+}
+
 int oracle_md_pose(int variant, const double *x, const double *y, const double *dx, const double *dy, or_model *out,
                    int max_out) {
     auto sols = oracle::md_pose((oracle::Variant)variant, x, y, dx, dy);

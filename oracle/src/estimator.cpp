@@ -323,7 +323,17 @@ int minimal_solver(const Problem &P, const std::vector<std::vector<int>> &sample
             models->push_back(md_pose_noshift_cal(x, y, dx, dy));
             return (int)models->size();
         }
-        std::vector<Model> sols = md_pose(P.variant, x, y, dx, dy);
+        std::vector<Model> sols;
+        if (P.variant == CAL && P.use_ours)
+            sols = md_pose_cal_ours(x, y, dx, dy);
+        else if (P.variant == SF && P.use_ours)
+            sols = md_pose_sf_ours(x, y, dx, dy);
+        else if (P.variant == TF && P.use_ours)
+            sols = md_pose_tf_ours(x, y, dx, dy);
+        else if (P.variant == TF && P.use_4p4d)
+            sols = md_pose_tf_4p4d(x, y, dx, dy);
+        else
+            sols = md_pose(P.variant, x, y, dx, dy);
         for (Model m : sols) {
             // src/hybrid_pose_estimator.cpp:80-85
             if (!P.cfg.min_depth_constraint ||

@@ -1,0 +1,86 @@
+"""Option-gated alternative MD solvers (HybridLORansacOptions::use_ours / use_4p4d;
+src/solver.cpp:536-680, 741-984, 1045-1148, 1287-1406): device vs oracle, directly
+and through the estimators."""
+import numpy as np
+import pytest
+
+import madpose
+import oracle
+from madpose_amd import synthetic
+from tests.helpers import oracle_cfg, oracle_opts, rot_angle_deg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def require_gpu():
+    if madpose.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X")
+
+
+def _rand_rot(rng):
+    R = np.linalg.qr(rng.standard_normal((3, 3)))[0]
+    return R * np.linalg.det(R)
+
+
+CASES = [("cal", 0, 1, madpose.solve_scale_shift_pose_ours),
+         ("sf", 1, 1, madpose.solve_scale_shift_pose_shared_focal_ours),
+         ("tf", 2, 1, madpose.solve_scale_shift_pose_two_focal_ours),
+         ("4p4d", 2, 2, madpose.solve_scale_shift_pose_two_focal_4p4d)]
+
+
+@pytest.mark.parametrize("name,variant,alt,fn", CASES)
+def test_alt_solver_matches_oracle(name, variant, alt, fn):
+    rng = np.random.default_rng(5 + variant + alt)
+    total = 0
+    for trial in range(150):
+        R = _rand_rot(rng)
+        t = rng.standard_normal(3) * 0.5
+        X = np.c_[rng.uniform(-1, 1, (4, 2)), rng.uniform(2, 6, 4)]
+        Y = X @ R.T + t
+        f0, f1 = rng.uniform(0.5, 3, 2)
+        noise = 0.0 if trial % 2 == 0 else 1e-2
+        if variant == 0:
+            x, y = X / X[:, 2:], Y / np.abs(Y[:, 2:])
+        else:
+            fy = f0 if variant == 1 else f1
+            x = np.c_[f0 * X[:, :2] / X[:, 2:], np.ones(4)]
+            y = np.c_[fy * Y[:, :2] / Y[:, 2:], np.ones(4)]
+        dx = X[:, 2] + rng.normal(0, noise, 4)
+        dy = Y[:, 2]
+        k = 3 if variant == 0 else 4
+        dev = fn(x[:k].T, y[:k].T, dx[:k], dy[:k])
+        ref = oracle.md_pose_alt(variant, alt, x[:k], y[:k], dx[:k], dy[:k])
+        assert len(dev) == len(ref), (trial, len(dev), len(ref))
+        for m, r in zip(dev, ref):
+            assert np.allclose(m.R(), r["R"], rtol=1e-7, atol=1e-8)
+            assert np.allclose(m.t(), r["t"], rtol=1e-7, atol=1e-8)
+            assert abs(m.scale - r["scale"]) <= 1e-7 * (1 + abs(r["scale"]))
+        total += len(dev)
+    assert total > 50
+
+
+def _parity(variant, o, c, p):
+    cam0, cam1 = (p["K0"], p["K1"]) if variant == 0 else (p["pp0"], p["pp1"])
+    fn = [madpose.HybridEstimatePoseScaleOffset, madpose.HybridEstimatePoseScaleOffsetSharedFocal,
+          madpose.HybridEstimatePoseScaleOffsetTwoFocal][variant]
+    pose, st = fn(p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], cam0, cam1, o, c)
+    om, ost, oinl = oracle.estimate(variant, p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], cam0, cam1,
+                                    oracle_opts(o), oracle_cfg(c))
+    assert st.num_iterations_total == ost.num_iterations_total
+    assert st.num_iterations_per_solver == list(ost.num_iterations_per_solver)
+    assert st.number_lo_iterations == ost.number_lo_iterations
+    for t in range(3):
+        assert np.array_equal(np.array(st.inlier_indices[t]), oinl[t])
+    assert rot_angle_deg(pose.R(), om["R"]) < 1e-6
+    assert abs(st.best_model_score - ost.best_model_score) <= 1e-9 * abs(ost.best_model_score)
+    return pose, st
+
+
+@pytest.mark.parametrize("variant,flag", [(0, "use_ours"), (1, "use_ours"), (2, "use_ours"), (2, "use_4p4d")])
+def test_estimator_with_alternates_parity(variant, flag):
+    p = synthetic.make_pair(60 + variant, n=400)
+    kind = ["calibrated", "shared_focal", "two_focal"][variant]
+    o, c = synthetic.example_options(kind, iterations=300)
+    setattr(o, flag, True)
+    _parity(variant, o, c, p)

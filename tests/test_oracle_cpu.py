@@ -68,3 +68,30 @@ def test_oracle_estimator_recovers_pose():
     # true inliers dominate the returned set
     frac = np.mean(p["inlier_mask"][inl[2]])
     assert frac > 0.9
+
+
+def test_oracle_alt_solvers_recover_ground_truth():
+    """use_ours / use_4p4d restatements (oracle/src/md_alt.cpp) on noise-free instances."""
+    rng = np.random.default_rng(0)
+    hits = {"cal": 0, "sf": 0, "tf": 0}
+    n = 60
+    for _ in range(n):
+        while True:
+            R = np.linalg.qr(rng.standard_normal((3, 3)))[0]
+            R *= np.linalg.det(R)
+            t = rng.standard_normal(3) * 0.5
+            X = np.c_[rng.uniform(-1, 1, (4, 2)), rng.uniform(2, 6, 4)]
+            Y = X @ R.T + t
+            if np.all(Y[:, 2] > 0.5):
+                break
+        u, v, s = rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), rng.uniform(0.5, 2)
+        sols = oracle.md_pose_alt(0, 1, (X / X[:, 2:])[:3], (Y / Y[:, 2:])[:3], X[:3, 2] - u, Y[:3, 2] / s - v)
+        hits["cal"] += any(np.abs(m["R"] - R).max() < 1e-6 and abs(m["offset0"] - u) < 1e-6 for m in sols)
+        f0, f1 = rng.uniform(0.5, 3, 2)
+        xs = np.c_[f0 * X[:, :2] / X[:, 2:], np.ones(4)]
+        sols = oracle.md_pose_alt(1, 1, xs, np.c_[f0 * Y[:, :2] / Y[:, 2:], np.ones(4)], X[:, 2], Y[:, 2] / s)
+        hits["sf"] += any(np.abs(m["R"] - R).max() < 1e-6 and abs(m["focal0"] - f0) < 1e-6 for m in sols)
+        sols = oracle.md_pose_alt(2, 1, xs, np.c_[f1 * Y[:, :2] / Y[:, 2:], np.ones(4)], X[:, 2], Y[:, 2] / s)
+        hits["tf"] += any(abs(m["focal0"] - f0) < 1e-6 and abs(m["focal1"] - f1) < 1e-6 for m in sols)
+    # the calibrated solver drops roots that the reference's column bookkeeping loses
+    assert hits["cal"] >= 0.9 * n and hits["sf"] == n and hits["tf"] == n, hits
