@@ -26,6 +26,7 @@ extern "C" {
 #define MP_CALIBRATED 0   /* HybridEstimatePoseScaleOffset          */
 #define MP_SHARED_FOCAL 1 /* HybridEstimatePoseScaleOffsetSharedFocal */
 #define MP_TWO_FOCAL 2    /* HybridEstimatePoseScaleOffsetTwoFocal    */
+#define MP_SCALE_ONLY 3   /* HybridEstimatePoseAndScale (K0/K1 as cam0/cam1, min_depth ignored) */
 
 /* ExtendedHybridLORansacOptions (src/hybrid_ransac.h:17-25, src/bindings.cpp:78-95) */
 typedef struct mp_ransac_options {
@@ -91,6 +92,7 @@ typedef struct mp_stats {
  *   HybridEstimatePoseScaleOffset            (src/hybrid_pose_estimator.cpp:8-35, bindings.cpp:169-170)
  *   HybridEstimatePoseScaleOffsetSharedFocal (src/hybrid_pose_shared_focal_estimator.cpp:8-51, :171-172)
  *   HybridEstimatePoseScaleOffsetTwoFocal    (src/hybrid_pose_two_focal_estimator.cpp:34-75, :173-174)
+ *   HybridEstimatePoseAndScale               (src/hybrid_pose_estimator.cpp:37-63, 297-442, :167-168)
  * x0, x1: n x 2 row-major pixels; d0, d1: n depth priors; min_depth[2];
  * cam0/cam1: K (9, row-major) for MP_CALIBRATED, principal point (2) otherwise.
  * inlier_idx: optional caller buffer of 3*n int32; list t starts at t*n and has
@@ -99,6 +101,11 @@ int mp_estimate(int variant, int64_t n, const double *x0, const double *x1, cons
                 const double *min_depth, const double *cam0, const double *cam1, const mp_ransac_options *options,
                 const mp_estimator_config *config, mp_model *out_model, mp_stats *out_stats, int32_t *inlier_idx,
                 int device);
+
+/* estimate_scale_and_pose(X, Y, W) (src/solver.cpp:5-33, binding src/bindings.cpp:156):
+ * weighted Procrustes with scale, Y ~ scale R X + t; X, Y point-major n x 3. */
+int mp_estimate_scale_and_pose(const double *X, const double *Y, const double *W, int64_t n, mp_model *out,
+                               int device);
 
 /* Many independent pairs in one call (pairs concatenated; offsets[p]..offsets[p+1]).
  * min_depth: 2 per pair; cams: 9 or 2 doubles per pair; inlier buffers per pair at

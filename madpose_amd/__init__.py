@@ -22,6 +22,7 @@ from .api import (  # noqa: F401
     RansacStats,
     device_count,
     estimate_batch,
+    estimate_scale_and_pose,
     profile_enable,
     profile_read,
     profile_reset,

@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmadpose_mi355x.so")
 
 MP_OK, MP_EINVAL, MP_EDEVICE = 0, 1, 2
-CALIBRATED, SHARED_FOCAL, TWO_FOCAL = 0, 1, 2
+CALIBRATED, SHARED_FOCAL, TWO_FOCAL, SCALE_ONLY = 0, 1, 2, 3
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int32_p = ctypes.POINTER(ctypes.c_int32)
@@ -112,6 +112,8 @@ EXPORTS = {
                                          ctypes.POINTER(mp_ransac_options), ctypes.POINTER(mp_estimator_config),
                                          ctypes.POINTER(mp_model), ctypes.POINTER(mp_stats), c_int32_p, ctypes.c_int,
                                          ctypes.c_int]),
+    "mp_estimate_scale_and_pose": (ctypes.c_int, [c_double_p, c_double_p, c_double_p, ctypes.c_int64,
+                                                  ctypes.POINTER(mp_model), ctypes.c_int]),
     "mp_solve_scale_and_shift": (ctypes.c_int, [ctypes.c_int, c_double_p, c_double_p, c_double_p, c_double_p,
                                                 c_double_p, ctypes.c_int, ctypes.c_int]),
     "mp_solve_scale_shift_pose": (ctypes.c_int, [ctypes.c_int, c_double_p, c_double_p, c_double_p, c_double_p,

@@ -234,6 +234,8 @@ def _model_from_c(m, variant):
         return PoseScaleOffset(R, t, m.scale, m.offset0, m.offset1)
     if variant == L.SHARED_FOCAL:
         return PoseScaleOffsetSharedFocal(R, t, m.scale, m.offset0, m.offset1, m.focal0)
+    if variant == L.SCALE_ONLY:
+        return PoseAndScale(R, t, m.scale)
     return PoseScaleOffsetTwoFocal(R, t, m.scale, m.offset0, m.offset1, m.focal0, m.focal1)
 
 
@@ -310,7 +312,7 @@ def _estimate(variant, x0, x1, depth0, depth1, min_depth, cam0, cam1, options, e
     md = np.ascontiguousarray(np.asarray(min_depth, dtype=np.float64).reshape(-1))
     if md.shape[0] != 2:
         raise ValueError("min_depth must hold two values")
-    ncam = 9 if variant == L.CALIBRATED else 2
+    ncam = 9 if variant in (L.CALIBRATED, L.SCALE_ONLY) else 2
     c0 = np.ascontiguousarray(np.asarray(cam0, dtype=np.float64).reshape(-1))
     c1 = np.ascontiguousarray(np.asarray(cam1, dtype=np.float64).reshape(-1))
     if c0.shape[0] != ncam or c1.shape[0] != ncam:
@@ -346,9 +348,26 @@ def HybridEstimatePoseScaleOffsetTwoFocal(x0, x1, depth0, depth1, min_depth, pp0
     return _estimate(L.TWO_FOCAL, x0, x1, depth0, depth1, min_depth, pp0, pp1, options, est_config, device)
 
 
-def HybridEstimatePoseAndScale(x0, x1, depth0, depth1, K0, K1, options, est_config=None):
-    """src/hybrid_pose_estimator.cpp:37-63 -- scale-only estimator (not yet ported)."""
-    raise NotImplementedError("HybridEstimatePoseAndScale is not available in this build yet")
+def HybridEstimatePoseAndScale(x0, x1, depth0, depth1, K0, K1, options, est_config=None, device=None):
+    """src/hybrid_pose_estimator.cpp:37-63, 297-442 (bindings.cpp:167-168): scale-only
+    estimator (no depth offsets); returns (PoseAndScale, HybridRansacStatistics)."""
+    return _estimate(L.SCALE_ONLY, x0, x1, depth0, depth1, [0.0, 0.0], K0, K1, options, est_config, device)
+
+
+def estimate_scale_and_pose(X, Y, W):
+    """src/solver.cpp:5-33 (bindings.cpp:156): weighted Procrustes with scale on the
+    device; X, Y are 3 x N point matrices (columns), W the N weights."""
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.asarray(Y, dtype=np.float64)
+    if X.ndim != 2 or X.shape[0] != 3 or X.shape != Y.shape:
+        raise ValueError("X and Y must be 3 x N matrices of the same shape")
+    n = X.shape[1]
+    W = _vec(W, n, "W")
+    Xp = np.ascontiguousarray(X.T)
+    Yp = np.ascontiguousarray(Y.T)
+    out = L.mp_model()
+    L.check(L.lib().mp_estimate_scale_and_pose(_dp(Xp), _dp(Yp), _dp(W), n, ctypes.byref(out), _DEFAULT_DEVICE))
+    return _model_from_c(out, L.SCALE_ONLY)
 
 
 def estimate_batch(variant, pairs, options, est_config=None, device=None, num_streams=4):

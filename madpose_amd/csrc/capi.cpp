@@ -99,7 +99,7 @@ mp::PairInput make_input(int variant, int64_t n, const double *x0, const double 
         in.min_depth[0] = min_depth[0];
         in.min_depth[1] = min_depth[1];
     }
-    const int nc = variant == MP_CALIBRATED ? 9 : 2;
+    const int nc = (variant == MP_CALIBRATED || variant == MP_SCALE_ONLY) ? 9 : 2;
     if (!cam0 || !cam1) throw std::invalid_argument("camera parameters missing");
     std::memcpy(in.cam0, cam0, sizeof(double) * nc);
     std::memcpy(in.cam1, cam1, sizeof(double) * nc);
@@ -145,7 +145,7 @@ int mp_estimate_batch(int variant, int32_t num_pairs, const int64_t *offsets, co
     return guarded([&]() {
         if (num_pairs < 0 || !offsets || !options || !out_models || !out_stats)
             throw std::invalid_argument("bad batch arguments");
-        const int nc = variant == MP_CALIBRATED ? 9 : 2;
+        const int nc = (variant == MP_CALIBRATED || variant == MP_SCALE_ONLY) ? 9 : 2;
         const mp::RansacOptions opts = to_opts(options);
         const mp::EstimatorConfig cfg = to_cfg(config);
         std::atomic<int> next(0);
@@ -179,6 +179,17 @@ int mp_estimate_batch(int variant, int32_t num_pairs, const int64_t *offsets, co
         for (auto &t : threads) t.join();
         for (int p = 0; p < num_pairs; ++p)
             if (codes[p] != MP_OK) return fail(codes[p], "pair " + std::to_string(p) + ": " + errors[p]);
+        return MP_OK;
+    });
+}
+
+int mp_estimate_scale_and_pose(const double *X, const double *Y, const double *W, int64_t n, mp_model *out,
+                               int device) {
+    return guarded([&]() {
+        if (!X || !Y || !W || !out || n < 1) throw std::invalid_argument("bad arguments");
+        mp::Model m;
+        mp::scale_and_pose_direct(X, Y, W, n, &m, device);
+        to_model(m, out);
         return MP_OK;
     });
 }

@@ -197,18 +197,20 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
     const int n = (int)in.n;
     PairConst &C = P.C;
     std::memset(&C, 0, sizeof(C));
-    C.variant = in.variant;
+    // the scale-only estimator runs on the calibrated geometry (src/hybrid_pose_estimator.h:110-134)
+    C.scale_only = in.variant == kScaleOnly ? 1 : 0;
+    C.variant = C.scale_only ? kCal : in.variant;
     C.n = n;
     C.score_type = cfg.score_type;
     C.min_depth_constraint = cfg.min_depth_constraint ? 1 : 0;
     C.use_shift = cfg.use_shift ? 1 : 0;
     // option-gated MD alternates (src/hybrid_pose_estimator.cpp:75-78, ..shared..cpp:62-65,
     // ..two..cpp:87-94); use_ours wins over use_4p4d, 4p4d exists for two-focal only
-    C.md_alt = o.use_ours ? 1 : ((o.use_4p4d && in.variant == kTF) ? 2 : 0);
+    C.md_alt = C.scale_only ? 0 : (o.use_ours ? 1 : ((o.use_4p4d && in.variant == kTF) ? 2 : 0));
     C.min_depth[0] = in.min_depth[0];
     C.min_depth[1] = in.min_depth[1];
     HostPair &H = P.H;
-    H.variant = in.variant;
+    H.variant = C.variant;
     H.n = n;
     H.x0.resize(2 * n);
     H.x1.resize(2 * n);
@@ -217,7 +219,7 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
     H.min_depth[0] = in.min_depth[0];
     H.min_depth[1] = in.min_depth[1];
     double thr0 = o.squared_inlier_thresholds[0], thr1 = o.squared_inlier_thresholds[1];
-    if (in.variant == kCal) {
+    if (C.variant == kCal) {
         std::memcpy(C.K0, in.cam0, sizeof(C.K0));
         std::memcpy(C.K1, in.cam1, sizeof(C.K1));
         inv3(C.K0, C.K0i);
@@ -429,6 +431,10 @@ class Run {
         // LeastSquares) and by the shared-focal NonMinimalSolver only.
         S.use_shift = (variant_ == kCal || (variant_ == kSF && nonminimal)) ? cfg_.use_shift : true;
         S.min_depth_constraint = cfg_.min_depth_constraint;
+        if (P_.C.scale_only) { // HybridPoseOptimizerScaleOnly: offsets constant, unbounded
+            S.use_shift = false;
+            S.min_depth_constraint = false;
+        }
         S.w_sampson = variant_ == kCal ? std::sqrt(P_.H.sampson_squared_weight) /
                                              (1.0 / (P_.C.K0[0] + P_.C.K0[4]) + 1.0 / (P_.C.K1[0] + P_.C.K1[4]))
                                        : std::sqrt(P_.H.sampson_squared_weight);
@@ -714,7 +720,8 @@ void Run::run(Model *best, Stats *S) {
 }
 
 void validate(const PairInput &in, const RansacOptions &o) {
-    if (in.variant < 0 || in.variant > 2) throw std::invalid_argument("variant must be 0 (calibrated), 1 or 2");
+    if (in.variant < 0 || in.variant > 3)
+        throw std::invalid_argument("variant must be 0 (calibrated), 1 (shared focal), 2 (two focal) or 3 (scale only)");
     if (in.n < 0 || in.n > (int64_t)1 << 30) throw std::invalid_argument("bad number of correspondences");
     if (in.n > 0 && (!in.x0 || !in.x1 || !in.d0 || !in.d1)) throw std::invalid_argument("null input array");
     if (!(o.squared_inlier_thresholds[0] > 0) || !(o.squared_inlier_thresholds[1] > 0))
@@ -757,7 +764,7 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
     DeviceCtx &X = *lease.c;
     Problem P = make_problem(in, opts, cfg);
     if (norm_scale) *norm_scale = P.norm_scale;
-    X.ensure(in.n, 64, max_models(in.variant));
+    X.ensure(in.n, 64, max_models(in.variant == kScaleOnly ? kCal : in.variant));
     PairData D;
     upload_pair(X, P, &D);
     std::vector<ScoreRec> recs(std::max(nm, 1));
@@ -846,6 +853,25 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
     hipFree(d_poses);
     for (int i = 0; i < std::min(std::min(hn, kCap), max_poses); ++i) poses[i] = hp[i];
     return hn;
+}
+
+void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device) {
+    CtxLease lease(device);
+    DeviceCtx &C = *lease.c;
+    std::vector<double> in(7 * (size_t)n);
+    std::memcpy(in.data(), X, sizeof(double) * 3 * n);
+    std::memcpy(in.data() + 3 * n, Y, sizeof(double) * 3 * n);
+    std::memcpy(in.data() + 6 * n, W, sizeof(double) * n);
+    double *d_in;
+    Model *d_out;
+    MP_HIP(hipMalloc(&d_in, sizeof(double) * in.size()));
+    MP_HIP(hipMalloc(&d_out, sizeof(Model)));
+    MP_HIP(hipMemcpyAsync(d_in, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, C.stream));
+    MP_HIP(launch_scale_and_pose(C.stream, d_in, n, d_out));
+    MP_HIP(hipMemcpyAsync(out, d_out, sizeof(Model), hipMemcpyDeviceToHost, C.stream));
+    MP_HIP(hipStreamSynchronize(C.stream));
+    hipFree(d_in);
+    hipFree(d_out);
 }
 
 int device_count() {

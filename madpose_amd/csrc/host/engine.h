@@ -68,6 +68,9 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
 // Bougnoux + recoverPose (normalized 2-D points).  Models before the depth fit.
 int solve_point_direct(int kind, const double *x1, const double *x2, Model *poses, int max_poses, int device);
 
+// estimate_scale_and_pose (src/solver.cpp:5-33) on the device; X, Y point-major n x 3
+void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device);
+
 int device_count();
 
 // Per-kernel device timing of the estimator's batch launches, measured with HIP

@@ -418,6 +418,54 @@ MP_HD bool md_pose_from_sol(const double (&x)[K][3], const double (&y)[K][3], co
     return true;
 }
 
+// estimate_scale_and_pose (src/solver.cpp:5-33) for K points: Y ~ scale R X + t with
+// weights W on the centroids and the cross-covariance, R from Horn's quaternion
+// method (the Kabsch optimum, identical to the reference's SVD solution).
+template <int K>
+MP_HD void scale_and_pose(const double (&X)[K][3], const double (&Y)[K][3], const double *W, Model &m) {
+    double ws = 0.0, cx[3] = {0, 0, 0}, cy[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        ws += W[i];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            cx[c] += X[i][c] * W[i];
+            cy[c] += Y[i][c] * W[i];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        cx[c] /= ws;
+        cy[c] /= ws;
+    }
+    double Mx[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) Mx[a][b] += (X[i][a] - cx[a]) * W[i] * (Y[i][b] - cy[b]);
+    horn_rotation(Mx, m.R);
+    double num = 0.0, den = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double xc[3] = {X[i][0] - cx[0], X[i][1] - cx[1], X[i][2] - cx[2]};
+        double rx[3];
+        matvec3(m.R, xc, rx);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            num += (Y[i][c] - cy[c]) * rx[c];
+            den += rx[c] * rx[c];
+        }
+    }
+    m.scale = num / den;
+    double rc[3];
+    matvec3(m.R, cx, rc);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) m.t[c] = cy[c] - m.scale * rc[c];
+    m.offset0 = m.offset1 = 0.0;
+}
+
 // use_shift = false branch of the calibrated MD solver (src/hybrid_pose_estimator.cpp:87-120)
 MP_HD void md_pose_noshift_cal(const double (&x)[3][3], const double (&y)[3][3], const double *dx, const double *dy,
                                Model &m) {

@@ -111,6 +111,10 @@ MP_HD void eval_corr(const PairConst &C, const ScoreRec &r, const Corr &p, bool 
     const bool skip_epi = gate && C.score_type == 2; // MD_ONLY: Sampson gated
     e0 = skip_md ? DBL_MAX : reproj_err(r.M0, r.k0, p.x0u, p.x0v, p.d0 + r.o0, p.x1u, p.x1v);
     e1 = skip_md ? DBL_MAX : reproj_err(r.M1, r.k1, p.x1u, p.x1v, p.d1 * r.s + r.o1s, p.x0u, p.x0v);
+    if (C.scale_only) { // HybridPoseEstimatorScaleOnly also rejects small priors (:395, :408)
+        if (p.d0 < 1e-2) e0 = DBL_MAX;
+        if (p.d1 < 1e-2) e1 = DBL_MAX;
+    }
     if (skip_epi) {
         e2 = DBL_MAX;
         return;

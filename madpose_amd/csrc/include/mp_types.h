@@ -13,7 +13,7 @@
 
 namespace mp {
 
-enum Variant : int { kCal = 0, kSF = 1, kTF = 2 };
+enum Variant : int { kCal = 0, kSF = 1, kTF = 2, kScaleOnly = 3 }; // kScaleOnly: host-side only
 
 // Model layout == mp_model of include/madpose_mi355x.h (src/pose.h:7-56).
 // R row-major, x1 = R x0 + t.
@@ -42,6 +42,8 @@ struct PairConst {
     int min_depth_constraint;
     int use_shift;
     int md_alt; // 0 default MD solvers, 1 use_ours, 2 use_4p4d (two-focal)
+    int scale_only; // HybridEstimatePoseAndScale (calibrated geometry, no offsets)
+    int pad1;
     double K0[9], K1[9], K0i[9], K1i[9]; // identity for SF/TF (focal lives in the model)
     double thr[3], w[3];                 // squared thresholds / weights after the option transform
     double loss_scale;                   // calibrated Sampson scale (src/hybrid_pose_estimator.h:35-36)

@@ -95,7 +95,15 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
             dx[j] = D.d0[i];
             dy[j] = D.d1[i];
         }
-        if (!C.use_shift) {
+        if (C.scale_only) {
+            // HybridPoseEstimatorScaleOnly::MinimalSolver (src/hybrid_pose_estimator.cpp:319-327)
+            const double W[3] = {1.0, 1.0, 1.0};
+            Model m;
+            m.focal0 = m.focal1 = 1.0;
+            scale_and_pose<3>(x, y, W, m);
+            m.scale = 1.0 / m.scale;
+            out[n++] = m;
+        } else if (!C.use_shift) {
             Model m;
             m.focal0 = m.focal1 = 1.0;
             md_pose_noshift_cal(x, y, dx, dy, m);
@@ -222,7 +230,7 @@ __global__ void __launch_bounds__(64) pt_solve_kernel(PairData D, PairConst C, c
         const int np = relpose_5pt(b1, b2, poses, kMaxModelsCal);
         for (int k = 0; k < np; ++k) {
             Model m = poses[k];
-            if (point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, shift, mdc, C.min_depth, m))
+            if (point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, shift && !C.scale_only, mdc, C.min_depth, m))
                 put_model(C, m, b, n++, maxm, models, recs);
         }
     } else if (V == kSF) {
@@ -515,6 +523,47 @@ __global__ void point_direct_kernel(int kind, const double *in, Model *poses, in
     }
 }
 
+// estimate_scale_and_pose (src/solver.cpp:5-33) for an arbitrary number of points
+__global__ void scale_and_pose_kernel(const double *in, int64_t n, Model *out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const double *X = in, *Y = in + 3 * n, *W = in + 6 * n;
+    double ws = 0.0, cx[3] = {0, 0, 0}, cy[3] = {0, 0, 0};
+    for (int64_t i = 0; i < n; ++i) {
+        ws += W[i];
+        for (int c = 0; c < 3; ++c) {
+            cx[c] += X[3 * i + c] * W[i];
+            cy[c] += Y[3 * i + c] * W[i];
+        }
+    }
+    for (int c = 0; c < 3; ++c) {
+        cx[c] /= ws;
+        cy[c] /= ws;
+    }
+    double Mx[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int64_t i = 0; i < n; ++i)
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) Mx[a][b] += (X[3 * i + a] - cx[a]) * W[i] * (Y[3 * i + b] - cy[b]);
+    Model m;
+    horn_rotation(Mx, m.R);
+    double num = 0.0, den = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double xc[3] = {X[3 * i] - cx[0], X[3 * i + 1] - cx[1], X[3 * i + 2] - cx[2]};
+        double rx[3];
+        matvec3(m.R, xc, rx);
+        for (int c = 0; c < 3; ++c) {
+            num += (Y[3 * i + c] - cy[c]) * rx[c];
+            den += rx[c] * rx[c];
+        }
+    }
+    m.scale = num / den;
+    double rc[3];
+    matvec3(m.R, cx, rc);
+    for (int c = 0; c < 3; ++c) m.t[c] = cy[c] - m.scale * rc[c];
+    m.offset0 = m.offset1 = 0.0;
+    m.focal0 = m.focal1 = 1.0;
+    *out = m;
+}
+
 template <class F> hipError_t by_variant(int v, F f) {
     if (v == kCal) return f(std::integral_constant<int, kCal>());
     if (v == kSF) return f(std::integral_constant<int, kSF>());
@@ -582,6 +631,11 @@ hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst
 hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *in, double *sols, int *nsols, Model *poses,
                             int *nposes) {
     md_direct_kernel<<<1, 64, 0, s>>>(variant, alt, in, sols, nsols, poses, nposes);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out) {
+    scale_and_pose_kernel<<<1, 64, 0, s>>>(in, n, out);
     return hipGetLastError();
 }
 

@@ -136,6 +136,14 @@ def md_pose_alt(variant, alt, x_homo_pm, y_homo_pm, dx, dy):
     return [model_to_dict(out[i]) for i in range(min(n, 16))]
 
 
+def estimate_scale_and_pose(X, Y, W):
+    """src/solver.cpp:5-33; X, Y: k x 3 points, W: k weights."""
+    X, Y, W = _c(X), _c(Y), _c(W)
+    out = OrModel()
+    lib().oracle_scale_and_pose(_dp(X), _dp(Y), _dp(W), len(W), ctypes.byref(out))
+    return model_to_dict(out)
+
+
 def relpose_5pt(b1, b2):
     out = (OrModel * 32)()
     n = lib().oracle_relpose_5pt(_dp(_c(b1)), _dp(_c(b2)), out, 32)

@@ -133,6 +133,11 @@ int oracle_relpose_5pt(const double *x1, const double *x2, or_model *out, int ma
     return (int)sols.size();
 }
 
+int oracle_scale_and_pose(const double *X, const double *Y, const double *W, int k, or_model *out) {
+    put_model(oracle::estimate_scale_and_pose(X, Y, W, k), out);
+    return 0;
+}
+
 int oracle_relpose_7pt(const double *x1, const double *x2, double *F_out, int max_out) {
     auto sols = oracle::relpose_7pt(x1, x2);
     int n = std::min((int)sols.size(), max_out);

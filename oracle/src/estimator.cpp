@@ -41,6 +41,9 @@ Problem make_problem(Variant v, int n, const double *x0, const double *x1, const
                      const double min_depth[2], const double *cam0, const double *cam1, const EstConfig &cfg,
                      Options *opts) {
     Problem P;
+    // the scale-only estimator shares the calibrated geometry (src/hybrid_pose_estimator.h:110-134)
+    P.scale_only = (v == SCALE);
+    if (v == SCALE) v = CAL;
     P.variant = v;
     P.n = n;
     P.cfg = cfg;
@@ -143,7 +146,7 @@ double evaluate_point(const Problem &P, const Model &m, int t, int i, bool is_fo
         mv3(K1, q, pr);
         double z = pr[2];
         double u = pr[0] / z, v = pr[1] / z;
-        if (z < 1e-2) return kMax;
+        if (z < 1e-2 || (P.scale_only && P.d0[i] < 1e-2)) return kMax; // scale-only: :395
         return (u - xb[0]) * (u - xb[0]) + (v - xb[1]) * (v - xb[1]);
     } else if (t == 1) {
         double c[3], p[3], q[3], pr[3];
@@ -154,7 +157,7 @@ double evaluate_point(const Problem &P, const Model &m, int t, int i, bool is_fo
         mv3(K0, q, pr);
         double z = pr[2];
         double u = pr[0] / z, v = pr[1] / z;
-        if (z < 1e-2) return kMax;
+        if (z < 1e-2 || (P.scale_only && P.d1[i] < 1e-2)) return kMax; // scale-only: :408
         return (u - xa[0]) * (u - xa[0]) + (v - xa[1]) * (v - xa[1]);
     }
     // t == 2
@@ -253,7 +256,7 @@ bool point_model_tail(const Problem &P, const std::vector<int> &idx, const doubl
     Model m = *out;
     for (int a = 0; a < 9; ++a) m.R[a] = R[a];
     double tt[3] = {t[0], t[1], t[2]};
-    if (!P.cfg.use_shift) {
+    if (!P.cfg.use_shift || P.scale_only) { // scale-only tail: :340-354
         double num = 0, den = 0;
         for (int j = 0; j < k; ++j) {
             num += dd0[j] * X[3 * j + 2];
@@ -318,6 +321,15 @@ int minimal_solver(const Problem &P, const std::vector<std::vector<int>> &sample
             }
             dx[j] = P.d0[i];
             dy[j] = P.d1[i];
+        }
+        if (P.scale_only) {
+            // src/hybrid_pose_estimator.cpp:319-327: Procrustes of the (unlifted)
+            // calibrated points, scale moved onto the second camera
+            const double W[3] = {1.0, 1.0, 1.0};
+            Model m = estimate_scale_and_pose(x, y, W, 3);
+            m.scale = 1.0 / m.scale;
+            models->push_back(m);
+            return 1;
         }
         if (P.variant == CAL && !P.cfg.use_shift) {
             models->push_back(md_pose_noshift_cal(x, y, dx, dy));
@@ -850,8 +862,9 @@ bool lm_call(const Problem &P, const std::vector<std::vector<int>> &sample, Mode
     L.i2 = &sample[2];
     L.use_reproj = P.cfg.lo_type != EPI_ONLY;
     L.use_sampson = P.cfg.lo_type != MD_ONLY;
-    L.use_shift = use_shift;
-    L.min_depth_constraint = P.cfg.min_depth_constraint;
+    // HybridPoseOptimizerScaleOnly: offsets constant and unbounded (src/optimizer.h:202-209)
+    L.use_shift = use_shift && !P.scale_only;
+    L.min_depth_constraint = P.cfg.min_depth_constraint && !P.scale_only;
     if (P.variant == CAL)
         L.w_sampson = std::sqrt(P.sampson_squared_weight) / (1.0 / (P.K0[0] + P.K0[4]) + 1.0 / (P.K1[0] + P.K1[4]));
     else
@@ -872,6 +885,54 @@ bool non_minimal_solver(const Problem &P, const std::vector<std::vector<int>> &s
     // NonMinimalSolver passes est_config.use_shift (cal :203, sf :146); tf leaves the default (true)
     bool use_shift = (P.variant == TF) ? true : P.cfg.use_shift;
     return lm_call(P, sample, m, use_shift);
+}
+
+Model estimate_scale_and_pose(const double *X, const double *Y, const double *W, int k) {
+    double wsum = 0.0, cX[3] = {0, 0, 0}, cY[3] = {0, 0, 0};
+    for (int i = 0; i < k; ++i) {
+        wsum += W[i];
+        for (int c = 0; c < 3; ++c) {
+            cX[c] += X[3 * i + c] * W[i];
+            cY[c] += Y[3 * i + c] * W[i];
+        }
+    }
+    for (int c = 0; c < 3; ++c) {
+        cX[c] /= wsum;
+        cY[c] /= wsum;
+    }
+    Mat S(3, 3);
+    for (int i = 0; i < k; ++i)
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) S(a, b) += (Y[3 * i + a] - cY[a]) * W[i] * (X[3 * i + b] - cX[b]);
+    Mat U, V;
+    std::vector<double> sv;
+    jacobi_svd(S, &U, &sv, &V);
+    double Um[9], Vm[9];
+    for (int a = 0; a < 9; ++a) {
+        Um[a] = U(a / 3, a % 3);
+        Vm[a] = V(a / 3, a % 3);
+    }
+    if (det3(Um) * det3(Vm) < 0)
+        for (int r = 0; r < 3; ++r) Um[3 * r + 2] = -Um[3 * r + 2];
+    Model m;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) m.R[3 * r + c] = Um[3 * r] * Vm[3 * c] + Um[3 * r + 1] * Vm[3 * c + 1] + Um[3 * r + 2] * Vm[3 * c + 2];
+    double num = 0.0, den = 0.0;
+    for (int i = 0; i < k; ++i) {
+        double xc[3], rx[3];
+        for (int c = 0; c < 3; ++c) xc[c] = X[3 * i + c] - cX[c];
+        mv3(m.R, xc, rx);
+        for (int c = 0; c < 3; ++c) {
+            num += (Y[3 * i + c] - cY[c]) * rx[c];
+            den += rx[c] * rx[c];
+        }
+    }
+    m.scale = num / den;
+    double rc[3];
+    mv3(m.R, cX, rc);
+    for (int c = 0; c < 3; ++c) m.t[c] = cY[c] - m.scale * rc[c];
+    m.offset0 = m.offset1 = 0.0;
+    return m;
 }
 
 void least_squares(const Problem &P, const std::vector<std::vector<int>> &sample, int, Model *m) {

@@ -36,7 +36,7 @@ def test_python_surface_matches_reference_bindings():
                  "PoseScaleOffsetTwoFocal", "PoseAndScale", "HybridRansacStatistics", "RansacOptions",
                  "LORansacOptions", "RansacStats", "HybridEstimatePoseScaleOffset",
                  "HybridEstimatePoseScaleOffsetSharedFocal", "HybridEstimatePoseScaleOffsetTwoFocal",
-                 "HybridEstimatePoseAndScale", "solve_scale_and_shift", "solve_scale_and_shift_shared_focal",
+                 "HybridEstimatePoseAndScale", "estimate_scale_and_pose", "solve_scale_and_shift", "solve_scale_and_shift_shared_focal",
                  "solve_scale_and_shift_two_focal", "solve_scale_shift_pose", "solve_scale_shift_pose_shared_focal",
                  "solve_scale_shift_pose_two_focal"]:
         assert hasattr(madpose, name), name
