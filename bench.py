@@ -73,8 +73,22 @@ def cpu_baseline(wl, pair, budget_s=15.0):
                       f"{st.num_hypotheses} hypotheses, {st.number_lo_iterations} LO runs"}
 
 
+def pmc_traffic_model():
+    """Latest committed PMC fit (profiles/r*/pmc_score_batch.json): memory-side read
+    bytes of one score_batch launch = fixed + per_iteration x iterations."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_score_batch.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        m = json.load(f)
+    m["file"] = os.path.relpath(files[-1], ROOT)
+    return m
+
+
 COUNTERS = ["elapsed_s", "hypotheses", "iterations", "lo_runs", "lo_s", "score_ms", "solve_ms", "prof_hypotheses",
-            "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms"]
+            "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms", "prof_iterations"]
 
 
 def gather_counters(local, world):
@@ -104,6 +118,15 @@ def summarize(allv, wl, steps, warmup, world):
     score_ms = float(c["score_ms"].sum())
     achieved = float(c["prof_correspondences"].sum()) * BYTES_PER_CORR / (score_ms * 1e-3) / 1e9 if score_ms > 0 else 0.0
     launches = int(c["prof_batches"].sum())
+    traffic, traffic_note = None, None
+    tm = pmc_traffic_model()
+    if tm is not None and launches > 0:
+        it_per_launch = float(c["prof_iterations"].sum()) / launches
+        traffic = tm["fetch_bytes_fixed_per_launch"] + tm["fetch_bytes_per_iteration"] * it_per_launch
+        traffic_note = (f"bytes per launch from the FETCH_SIZE fit in {tm['file']} ({tm['correction']}) at "
+                        f"{it_per_launch:.0f} iterations per launch; algorithmic bytes per launch "
+                        f"{float(c['prof_correspondences'].sum()) * BYTES_PER_CORR / launches:.3g}: the pair's "
+                        f"arrays stay L2-resident across the workgroups of a launch")
     return {
         "metric": "RANSAC hypotheses/sec + image-pairs/sec on 1xMI355X",
         "value": float(c["hypotheses"].sum()) / t_max,
@@ -132,7 +155,8 @@ def summarize(allv, wl, steps, warmup, world):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_note": traffic_note,
             "launches": launches,
             "avg_launch_us": score_ms * 1e3 / max(launches, 1),
             "bytes_per_hypothesis": BYTES_PER_CORR * wl["n"],
@@ -202,7 +226,7 @@ def main():
 
     local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
              prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
-             prof["sweep_wall_ms"]]
+             prof["sweep_wall_ms"], prof["iterations"]]
     allv = gather_counters(local, world)
     if rank == 0:
         res = summarize(allv, wl, a.steps, a.warmup, world)
