@@ -67,6 +67,10 @@ struct DeviceCtx {
     double *d_scores = nullptr, *d_best = nullptr;
     ScoreRec *d_rec1 = nullptr;
     double *d_err = nullptr, *d_score1 = nullptr;
+    // staged point-solver workspace (kernels.h PtWorkspace)
+    double *d_pt_cand = nullptr;
+    int *d_pt_ncand = nullptr, *d_pt_valid = nullptr;
+    Model *d_pt_slots = nullptr;
     // pinned host mirrors
     int *h_samples = nullptr, *h_md_list = nullptr, *h_pt_list = nullptr, *h_counts = nullptr, *h_best_slot = nullptr;
     double *h_best = nullptr, *h_err = nullptr, *h_score1 = nullptr;
@@ -78,7 +82,8 @@ struct DeviceCtx {
         hipSetDevice(device);
         for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_md_list, (void *)d_pt_list, (void *)d_counts,
                         (void *)d_best_slot, (void *)d_models, (void *)d_recs, (void *)d_scores, (void *)d_best,
-                        (void *)d_rec1, (void *)d_err, (void *)d_score1})
+                        (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_ncand,
+                        (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
         for (void *p : {(void *)h_samples, (void *)h_md_list, (void *)h_pt_list, (void *)h_counts, (void *)h_best_slot,
                         (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1})
@@ -87,6 +92,9 @@ struct DeviceCtx {
         d_samples = d_md_list = d_pt_list = d_counts = d_best_slot = nullptr;
         d_models = nullptr;
         d_recs = d_rec1 = nullptr;
+        d_pt_cand = nullptr;
+        d_pt_ncand = d_pt_valid = nullptr;
+        d_pt_slots = nullptr;
         h_samples = h_md_list = h_pt_list = h_counts = h_best_slot = nullptr;
         h_best = h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
@@ -113,6 +121,10 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_scores, sizeof(double) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_rec1, sizeof(ScoreRec) * 64));
+        MP_HIP(hipMalloc(&d_pt_cand, sizeof(double) * (size_t)bb * kPtCandStride));
+        MP_HIP(hipMalloc(&d_pt_ncand, sizeof(int) * (size_t)bb));
+        MP_HIP(hipMalloc(&d_pt_valid, sizeof(int) * (size_t)bb * kPtSlotStride));
+        MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb * kPtSlotStride));
         MP_HIP(hipMalloc(&d_score1, sizeof(double) * 64));
         MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 8 * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_md_list, sizeof(int) * bb, hipHostMallocDefault));
@@ -609,7 +621,9 @@ void Run::run(Model *best, Stats *S) {
         MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
         if (prof) MP_HIP(hipEventRecord(X_.ev[0], s));
         MP_HIP(launch_md_solve(s, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs, X_.d_counts, maxm_));
-        MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, X_.d_models, X_.d_recs, X_.d_counts, maxm_));
+        const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid};
+        MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
+                               maxm_));
         if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
         MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_best,
                                   X_.d_best_slot));

@@ -386,10 +386,9 @@ MP_HD bool fivept_system(const double (&x1)[5][3], const double (&x2)[5][3], Fiv
     return true;
 }
 
-// Poses of one real root z of det B(z): (x, y) from the null vector of B(z), E, and
-// motion_from_essential with cheirality on the five points.  Appends at out[k..].
-MP_HD int fivept_poses_for_root(const FivePtSys &S, double z, const double (&x1)[5][3], const double (&x2)[5][3],
-                                Model *out, int k, int kmax) {
+// Essential matrix of one real root z of det B(z): (x, y) from the null vector of
+// B(z).  False when the null vector has no finite (x, y).
+MP_HD bool fivept_E_for_root(const FivePtSys &S, double z, double *Ee) {
     double Bm[3][3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -405,11 +404,19 @@ MP_HD int fivept_poses_for_root(const FivePtSys &S, double z, const double (&x1)
     double v[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) v[c] = (n01 >= n02 && n01 >= n12) ? v01[c] : (n02 >= n12 ? v02[c] : v12[c]);
-    if (v[2] == 0.0) return 0;
+    if (v[2] == 0.0) return false;
     const double x = v[0] / v[2], y = v[1] / v[2];
-    double Ee[9];
 #pragma unroll
     for (int e = 0; e < 9; ++e) Ee[e] = x * S.N[0][e] + y * S.N[1][e] + z * S.N[2][e] + S.N[3][e];
+    return true;
+}
+
+// Poses of one real root: E, then motion_from_essential with cheirality on the five
+// points.  Appends at out[k..].
+MP_HD int fivept_poses_for_root(const FivePtSys &S, double z, const double (&x1)[5][3], const double (&x2)[5][3],
+                                Model *out, int k, int kmax) {
+    double Ee[9];
+    if (!fivept_E_for_root(S, z, Ee)) return 0;
     return motion_from_essential<5>(Ee, x1, x2, out, k, kmax);
 }
 

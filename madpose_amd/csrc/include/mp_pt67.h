@@ -528,12 +528,9 @@ MP_HD bool null_vector10(double (&A)[10][10], double (&v)[10]) {
     return true;
 }
 
-// kStop < 4 truncates the solver after stage kStop (tools/solver_bench.hip timing).
-template <int kStop = 4>
-MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Model *out, int kmax) {
-    double Q[6][9], N[3][9];
-    epipolar_rows<6>(x1, x2, Q);
-    nullspace_kx9<6>(Q, N);
+// The ten equations of the 6-point system: M[a] holds the coefficients of w^a
+// (rows: det F, then the nine trace-constraint entries; columns: monomials of v).
+MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
     Lin2 F[9];
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
@@ -541,7 +538,6 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
         F[e].c[1] = N[1][e];
         F[e].c[2] = N[2][e];
     }
-    double M[3][10][10];
     for (int a = 0; a < 3; ++a)
         for (int r = 0; r < 10; ++r)
             for (int c = 0; c < 10; ++c) M[a][r][c] = 0.0;
@@ -608,7 +604,10 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
                 }
             }
     }
-    if (kStop == 0) return (int)(M[1][3][4] > 0);
+}
+
+// Positive real roots u = 1/w of det(u^2 M0 + u M1 + M2) / u^5 (ascending).
+MP_HD int sixpt_roots(const double (&M)[3][10][10], double (&roots)[15]) {
     // q(u): first pass on |u| = 1, then on the geometric mean of the root moduli
     double c[16];
     pencil_poly15(M, 1.0, c);
@@ -618,81 +617,118 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
         if (!(rho > 0.0) || !(rho < 1e300)) rho = 1.0;
     }
     if (rho != 1.0) pencil_poly15(M, rho, c);
-    if (kStop == 1) return (int)(c[7] > 0);
-    double roots[15];
-    const int nr = sturm_real_roots<15>(c, roots);
-    if (kStop == 2) return nr;
-    int nout = 0;
-    for (int k = 0; k < nr; ++k) {
-        if (!(roots[k] > 0.0)) continue;
-        double w = 1.0 / roots[k];
-        double A[10][10];
-        for (int r = 0; r < 10; ++r)
-            for (int cc = 0; cc < 10; ++cc) A[r][cc] = M[0][r][cc] + w * (M[1][r][cc] + w * M[2][r][cc]);
-        double v[10];
-        if (!null_vector10(A, v) || v[9] == 0.0) continue;
-        double x = v[7] / v[9], y = v[8] / v[9];
-        // Gauss-Newton polish of (x, y, w) on the ten equations
-        for (int it = 0; it < 5; ++it) {
-            double mv[10], dxv[10], dyv[10];
-            mono2(x, y, mv, dxv, dyv);
-            double JtJ[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, Jtr[3][1] = {{0}, {0}, {0}};
-            for (int r = 0; r < 10; ++r) {
-                double res = 0, jx = 0, jy = 0, jw = 0;
-                for (int cc = 0; cc < 10; ++cc) {
-                    const double m = M[0][r][cc] + w * (M[1][r][cc] + w * M[2][r][cc]);
-                    res += m * mv[cc];
-                    jx += m * dxv[cc];
-                    jy += m * dyv[cc];
-                    jw += (M[1][r][cc] + 2.0 * w * M[2][r][cc]) * mv[cc];
-                }
-                const double J[3] = {jx, jy, jw};
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    Jtr[a][0] += J[a] * res;
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) JtJ[a][b] += J[a] * J[b];
-                }
+    double all[15];
+    const int nr = sturm_real_roots<15>(c, all);
+    int n = 0;
+    for (int k = 0; k < nr; ++k)
+        if (all[k] > 0.0) roots[n++] = all[k];
+    return n;
+}
+
+// Poses of one root u: (x, y) from the null vector of M(w), Gauss-Newton polish of
+// (x, y, w), E = K F K, motion_from_essential on the f-calibrated bearings.
+MP_HD int sixpt_poses_for_root(const double (&M)[3][10][10], const double (&N)[3][9], double u,
+                               const double (&x1)[6][3], const double (&x2)[6][3], Model *out, int nout, int kmax) {
+    double w = 1.0 / u;
+    double A[10][10];
+    for (int r = 0; r < 10; ++r)
+        for (int cc = 0; cc < 10; ++cc) A[r][cc] = M[0][r][cc] + w * (M[1][r][cc] + w * M[2][r][cc]);
+    double v[10];
+    if (!null_vector10(A, v) || v[9] == 0.0) return 0;
+    double x = v[7] / v[9], y = v[8] / v[9];
+    // Gauss-Newton polish of (x, y, w) on the ten equations
+    for (int it = 0; it < 5; ++it) {
+        double mv[10], dxv[10], dyv[10];
+        mono2(x, y, mv, dxv, dyv);
+        double JtJ[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, Jtr[3][1] = {{0}, {0}, {0}};
+        for (int r = 0; r < 10; ++r) {
+            double res = 0, jx = 0, jy = 0, jw = 0;
+            for (int cc = 0; cc < 10; ++cc) {
+                const double m = M[0][r][cc] + w * (M[1][r][cc] + w * M[2][r][cc]);
+                res += m * mv[cc];
+                jx += m * dxv[cc];
+                jy += m * dyv[cc];
+                jw += (M[1][r][cc] + 2.0 * w * M[2][r][cc]) * mv[cc];
             }
-            if (!gauss_solve<3, 1>(JtJ, Jtr)) break;
-            x -= Jtr[0][0];
-            y -= Jtr[1][0];
-            w -= Jtr[2][0];
-        }
-        if (!(w > 0.0)) continue;
-        if (kStop == 3) {
-            nout += (x > y);
-            continue;
-        }
-        const double foc = 1.0 / sqrt(w);
-        double Fm[9], nn = 0.0;
+            const double J[3] = {jx, jy, jw};
 #pragma unroll
-        for (int e = 0; e < 9; ++e) {
-            Fm[e] = x * N[0][e] + y * N[1][e] + N[2][e];
-            nn += Fm[e] * Fm[e];
-        }
-        nn = 1.0 / sqrt(nn);
-        double E[9];
+            for (int a = 0; a < 3; ++a) {
+                Jtr[a][0] += J[a] * res;
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int cc = 0; cc < 3; ++cc) E[3 * r + cc] = Fm[3 * r + cc] * nn * (r < 2 ? foc : 1.0) * (cc < 2 ? foc : 1.0);
-        double c1[6][3], c2[6][3];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            double a[3] = {x1[i][0] / foc, x1[i][1] / foc, x1[i][2]}, b[3] = {x2[i][0] / foc, x2[i][1] / foc, x2[i][2]};
-            const double na = 1.0 / sqrt(dot3(a, a)), nb = 1.0 / sqrt(dot3(b, b));
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                c1[i][q] = a[q] * na;
-                c2[i][q] = b[q] * nb;
+                for (int b = 0; b < 3; ++b) JtJ[a][b] += J[a] * J[b];
             }
         }
-        const int added = motion_from_essential<6>(E, c1, c2, out, nout, kmax);
-        for (int q = 0; q < added; ++q) out[nout + q].focal0 = out[nout + q].focal1 = foc;
-        nout += added;
+        if (!gauss_solve<3, 1>(JtJ, Jtr)) break;
+        x -= Jtr[0][0];
+        y -= Jtr[1][0];
+        w -= Jtr[2][0];
     }
+    if (!(w > 0.0)) return 0;
+    const double foc = 1.0 / sqrt(w);
+    double Fm[9], nn = 0.0;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        Fm[e] = x * N[0][e] + y * N[1][e] + N[2][e];
+        nn += Fm[e] * Fm[e];
+    }
+    nn = 1.0 / sqrt(nn);
+    double E[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) E[3 * r + cc] = Fm[3 * r + cc] * nn * (r < 2 ? foc : 1.0) * (cc < 2 ? foc : 1.0);
+    // K^-1 x, re-normalised: check_cheirality assumes unit bearings
+    double c1[6][3], c2[6][3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const double a[3] = {x1[i][0] / foc, x1[i][1] / foc, x1[i][2]}, b[3] = {x2[i][0] / foc, x2[i][1] / foc, x2[i][2]};
+        const double na = 1.0 / sqrt(dot3(a, a)), nb = 1.0 / sqrt(dot3(b, b));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            c1[i][q] = a[q] * na;
+            c2[i][q] = b[q] * nb;
+        }
+    }
+    const int added = motion_from_essential<6>(E, c1, c2, out, nout, kmax);
+    for (int q = 0; q < added; ++q) out[nout + q].focal0 = out[nout + q].focal1 = foc;
+    return added;
+}
+
+// kStop < 4 truncates the solver after stage kStop (tools/solver_bench.hip timing).
+template <int kStop = 4>
+MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Model *out, int kmax) {
+    double Q[6][9], N[3][9];
+    epipolar_rows<6>(x1, x2, Q);
+    nullspace_kx9<6>(Q, N);
+    double M[3][10][10];
+    sixpt_matrices(N, M);
+    if (kStop == 0) return (int)(M[1][3][4] > 0);
+    double roots[15];
+    const int nr = sixpt_roots(M, roots);
+    if (kStop <= 2) return nr;
+    int nout = 0;
+    for (int k = 0; k < nr; ++k) nout += sixpt_poses_for_root(M, N, roots[k], x1, x2, out, nout, kmax);
     return nout;
+}
+
+// Two-focal candidate of one fundamental matrix: Bougnoux focals, E = K1^T F K0,
+// recoverPose on the normalized 2-D points (src/hybrid_pose_two_focal_estimator.cpp:118-146).
+template <int K>
+MP_HD void twofocal_pose_from_F(const double *F, const double (&p0)[K][2], const double (&p1)[K][2], Model &m) {
+    double f0, f1;
+    bougnoux_sq(F, &f0, &f1);
+    f0 = sqrt(fabs(f0));
+    f1 = sqrt(fabs(f1));
+    double E[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) E[3 * r + c] = (r < 2 ? f1 : 1.0) * F[3 * r + c] * (c < 2 ? f0 : 1.0);
+    recover_pose_cv<K>(E, p0, p1, 1e9, m.R, m.t);
+    m.scale = 1.0;
+    m.offset0 = m.offset1 = 0.0;
+    m.focal0 = f0;
+    m.focal1 = f1;
 }
 
 } // namespace mp

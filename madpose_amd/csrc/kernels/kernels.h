@@ -14,9 +14,19 @@ hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D
 // MD minimal solver over the listed iterations (one thread per iteration).
 hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm);
-// point minimal solver over the listed iterations.
+// Workspace of the staged point solvers (per point sample: candidate roots and model
+// slots).  cand: kPtCandStride doubles, slots / valid: kPtSlotStride entries.
+constexpr int kPtCandStride = 96, kPtSlotStride = 32;
+struct PtWorkspace {
+    double *cand;
+    int *ncand;
+    Model *slots;
+    int *valid;
+};
+// point minimal solver over the listed iterations (three launches, see kernels.hip).
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                           const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm);
+                           const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
+                           int maxm);
 // scoring sweep: one workgroup per iteration, every model of the iteration scored
 // over all correspondences; per-iteration argmin (first minimum wins).
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,

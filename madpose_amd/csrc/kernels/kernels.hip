@@ -193,83 +193,180 @@ __device__ inline void load_uncal_sample(const PairData &D, const int *s, double
     }
 }
 
+// ---------------------------------------------------------------------------
+// Point solvers in three stages, so that the per-root work (pose recovery, depth
+// tail) runs one root per lane instead of looping inside one lane per sample:
+//   pt_roots   lane per sample: polynomial system + real roots -> candidates
+//              (cal: E per root; sf: null-space basis + roots u; tf: F per root)
+//   pt_tail    lane per (root, sample), root-major so that waves of high root
+//              indices are empty and retire at once: poses + depth tail -> slots
+//   pt_compact lane per sample: valid slots in root order -> models + score records
+constexpr int kCandStride = kPtCandStride; // doubles of root-stage output per point sample
+constexpr int kSlotStride = kPtSlotStride; // candidate model slots per point sample
+
+template <int V> struct PtTraits;
+template <> struct PtTraits<kCal> {
+    static constexpr int kRoots = 10, kPosesPerRoot = 2, K = 5;
+};
+template <> struct PtTraits<kSF> {
+    static constexpr int kRoots = 15, kPosesPerRoot = 2, K = 6;
+};
+template <> struct PtTraits<kTF> {
+    static constexpr int kRoots = 3, kPosesPerRoot = 1, K = 7;
+};
+
+// calibrated bearings / 2-D points of a point sample (src/hybrid_pose_estimator.cpp:121-133)
+__device__ inline void load_cal_sample(const PairData &D, const PairConst &C, const int *s, double (&b1)[5][3],
+                                       double (&b2)[5][3], double (&p0)[5][2], double (&p1)[5][2], double (&dd0)[5],
+                                       double (&dd1)[5]) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const int i = s[j];
+        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+        double a[3], c[3];
+        matvec3(C.K0i, xa, a);
+        matvec3(C.K1i, xb, c);
+        const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            b1[j][q] = a[q] * na;
+            b2[j][q] = c[q] * nc;
+        }
+        p0[j][0] = a[0];
+        p0[j][1] = a[1];
+        p1[j][0] = c[0];
+        p1[j][1] = c[1];
+        dd0[j] = D.d0[i];
+        dd1[j] = D.d1[i];
+    }
+}
+
 template <int V>
-__global__ void __launch_bounds__(64) pt_solve_kernel(PairData D, PairConst C, const int *list, int nlist,
-                                                      const int *samples, Model *models, ScoreRec *recs, int *counts,
-                                                      int maxm) {
+__global__ void __launch_bounds__(64) pt_roots_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                      const int *samples, double *cand, int *ncand) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= nlist) return;
-    const int b = list[idx];
-    const int *s = samples + (size_t)b * kSampleStride;
+    const int *s = samples + (size_t)list[idx] * kSampleStride;
+    double *out = cand + (size_t)idx * kCandStride;
     int n = 0;
-    const bool shift = C.use_shift != 0, mdc = C.min_depth_constraint != 0;
     if (V == kCal) {
-        // src/hybrid_pose_estimator.cpp:121-185
         double b1[5][3], b2[5][3], p0[5][2], p1[5][2], dd0[5], dd1[5];
+        load_cal_sample(D, C, s, b1, b2, p0, p1, dd0, dd1);
+        FivePtSys S;
+        if (fivept_system(b1, b2, S)) {
+            double roots[10];
+            const int nr = sturm_real_roots<10>(S.d10, roots);
+            for (int r = 0; r < nr; ++r) {
+                double E[9];
+                if (!fivept_E_for_root(S, roots[r], E)) continue;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const int i = s[j];
-            const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
-            double a[3], c[3];
-            matvec3(C.K0i, xa, a);
-            matvec3(C.K1i, xb, c);
-            const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                b1[j][q] = a[q] * na;
-                b2[j][q] = c[q] * nc;
+                for (int e = 0; e < 9; ++e) out[9 * n + e] = E[e];
+                ++n;
             }
-            p0[j][0] = a[0];
-            p0[j][1] = a[1];
-            p1[j][0] = c[0];
-            p1[j][1] = c[1];
-            dd0[j] = D.d0[i];
-            dd1[j] = D.d1[i];
-        }
-        Model poses[kMaxModelsCal];
-        const int np = relpose_5pt(b1, b2, poses, kMaxModelsCal);
-        for (int k = 0; k < np; ++k) {
-            Model m = poses[k];
-            if (point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, shift && !C.scale_only, mdc, C.min_depth, m))
-                put_model(C, m, b, n++, maxm, models, recs);
         }
     } else if (V == kSF) {
-        // src/hybrid_pose_shared_focal_estimator.cpp:74-128
         double b0[6][3], b1[6][3], p0[6][2], p1[6][2], dd0[6], dd1[6];
         load_uncal_sample<6>(D, s, b0, b1, p0, p1, dd0, dd1);
-        Model poses[kMaxModelsSF];
-        const int np = relpose_6pt_sf(b0, b1, poses, kMaxModelsSF);
-        for (int k = 0; k < np; ++k) {
-            Model m = poses[k];
-            const double f = m.focal0;
-            if (point_model_tail<6>(p0, p1, dd0, dd1, f, f, shift, mdc, C.min_depth, m))
-                put_model(C, m, b, n++, maxm, models, recs);
-        }
+        double Q[6][9], N[3][9];
+        epipolar_rows<6>(b0, b1, Q);
+        nullspace_kx9<6>(Q, N);
+        double M[3][10][10];
+        sixpt_matrices(N, M);
+        double roots[15];
+        n = sixpt_roots(M, roots);
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int e = 0; e < 9; ++e) out[9 * a + e] = N[a][e];
+        for (int k = 0; k < n; ++k) out[27 + k] = roots[k];
     } else {
-        // src/hybrid_pose_two_focal_estimator.cpp:103-182
         double b0[7][3], b1[7][3], p0[7][2], p1[7][2], dd0[7], dd1[7];
         load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
         double F[3][9];
-        const int nf = relpose_7pt_F(b0, b1, F);
-        for (int k = 0; k < nf; ++k) {
-            double f0, f1;
-            bougnoux_sq(F[k], &f0, &f1);
-            f0 = sqrt(fabs(f0));
-            f1 = sqrt(fabs(f1));
-            double E[9];
+        n = relpose_7pt_F(b0, b1, F);
+        for (int k = 0; k < n; ++k)
 #pragma unroll
-            for (int r = 0; r < 3; ++r)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) E[3 * r + c] = (r < 2 ? f1 : 1.0) * F[k][3 * r + c] * (c < 2 ? f0 : 1.0);
-            Model m;
-            recover_pose_cv<7>(E, p0, p1, 1e9, m.R, m.t);
-            m.scale = 1.0;
-            m.offset0 = m.offset1 = 0.0;
-            m.focal0 = f0;
-            m.focal1 = f1;
-            if (point_model_tail<7>(p0, p1, dd0, dd1, f0, f1, shift, mdc, C.min_depth, m))
-                put_model(C, m, b, n++, maxm, models, recs);
+            for (int e = 0; e < 9; ++e) out[9 * k + e] = F[k][e];
+    }
+    ncand[idx] = n;
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) pt_tail_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                     const int *samples, const double *cand, const int *ncand,
+                                                     Model *slots, int *valid) {
+    using T = PtTraits<V>;
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = gid / nlist, idx = gid - k * nlist;
+    if (k >= T::kRoots || k >= ncand[idx]) return;
+    const int *s = samples + (size_t)list[idx] * kSampleStride;
+    const double *cd = cand + (size_t)idx * kCandStride;
+    Model *sl = slots + (size_t)idx * kSlotStride + T::kPosesPerRoot * k;
+    int *vl = valid + (size_t)idx * kSlotStride + T::kPosesPerRoot * k;
+    const bool shift = C.use_shift != 0 && !C.scale_only, mdc = C.min_depth_constraint != 0;
+    if (V == kCal) {
+        // src/hybrid_pose_estimator.cpp:134-182
+        double b1[5][3], b2[5][3], p0[5][2], p1[5][2], dd0[5], dd1[5];
+        load_cal_sample(D, C, s, b1, b2, p0, p1, dd0, dd1);
+        Model poses[2];
+        const int np = motion_from_essential<5>(cd + 9 * k, b1, b2, poses, 0, 2);
+        for (int j = 0; j < 2; ++j) {
+            bool ok = false;
+            if (j < np) {
+                Model m = poses[j];
+                ok = point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, shift, mdc, C.min_depth, m);
+                if (ok) sl[j] = m;
+            }
+            vl[j] = ok ? 1 : 0;
         }
+    } else if (V == kSF) {
+        // src/hybrid_pose_shared_focal_estimator.cpp:87-126
+        double b0[6][3], b1[6][3], p0[6][2], p1[6][2], dd0[6], dd1[6];
+        load_uncal_sample<6>(D, s, b0, b1, p0, p1, dd0, dd1);
+        double N[3][9];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int e = 0; e < 9; ++e) N[a][e] = cd[9 * a + e];
+        double M[3][10][10];
+        sixpt_matrices(N, M);
+        Model poses[2];
+        const int np = sixpt_poses_for_root(M, N, cd[27 + k], b0, b1, poses, 0, 2);
+        for (int j = 0; j < 2; ++j) {
+            bool ok = false;
+            if (j < np) {
+                Model m = poses[j];
+                const double f = m.focal0;
+                ok = point_model_tail<6>(p0, p1, dd0, dd1, f, f, shift, mdc, C.min_depth, m);
+                if (ok) sl[j] = m;
+            }
+            vl[j] = ok ? 1 : 0;
+        }
+    } else {
+        // src/hybrid_pose_two_focal_estimator.cpp:118-181
+        double b0[7][3], b1[7][3], p0[7][2], p1[7][2], dd0[7], dd1[7];
+        load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
+        Model m;
+        twofocal_pose_from_F<7>(cd + 9 * k, p0, p1, m);
+        const bool ok = point_model_tail<7>(p0, p1, dd0, dd1, m.focal0, m.focal1, shift, mdc, C.min_depth, m);
+        if (ok) sl[0] = m;
+        vl[0] = ok ? 1 : 0;
+    }
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *list, int nlist, const int *ncand,
+                                                        const Model *slots, const int *valid, Model *models,
+                                                        ScoreRec *recs, int *counts, int maxm) {
+    using T = PtTraits<V>;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= nlist) return;
+    const int b = list[idx];
+    const int total = T::kPosesPerRoot * min(ncand[idx], T::kRoots);
+    int n = 0;
+    for (int q = 0; q < total; ++q) {
+        if (!valid[(size_t)idx * kSlotStride + q] || n >= maxm) continue;
+        put_model(C, slots[(size_t)idx * kSlotStride + q], b, n++, maxm, models, recs);
     }
     counts[b] = n;
 }
@@ -589,11 +686,18 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
 }
 
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                           const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm) {
+                           const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
+                           int maxm) {
     if (nlist <= 0) return hipSuccess;
     const int grid = (nlist + 63) / 64;
     return by_variant(C.variant, [&](auto V) {
-        pt_solve_kernel<decltype(V)::value><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+        constexpr int v = decltype(V)::value;
+        pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
+        const long lanes = (long)nlist * PtTraits<v>::kRoots;
+        pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
+                                                                  W.slots, W.valid);
+        pt_compact_kernel<v><<<grid, 64, 0, s>>>(C, list, nlist, W.ncand, W.slots, W.valid, models, recs, counts,
+                                                 maxm);
         return hipGetLastError();
     });
 }
