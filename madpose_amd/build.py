@@ -32,7 +32,10 @@ HEADERS = [
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"), "-Wall",
-         "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
+         "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result",
+         # host side only: AVX2/FMA for the 4-wide LM residual loop (lm.cpp); the
+         # device side stays plain gfx950
+         "-Xarch_host", "-march=x86-64-v3"]
 
 
 def _newer(target, deps):
@@ -44,7 +47,7 @@ def _newer(target, deps):
 
 def _compile(src):
     obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
-    if _newer(obj, [src] + HEADERS):
+    if _newer(obj, [src, __file__] + HEADERS):
         cmd = [HIPCC, "-x", "hip"] + FLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

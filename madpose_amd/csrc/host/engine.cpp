@@ -71,6 +71,10 @@ struct DeviceCtx {
     double *d_pt_cand = nullptr;
     int *d_pt_ncand = nullptr, *d_pt_valid = nullptr;
     Model *d_pt_slots = nullptr;
+    // zero-copy LO sweep output (host-coherent pinned memory) and its completion flag
+    double *h_sweep = nullptr, *d_sweep = nullptr;
+    int *h_flag = nullptr, *d_flag = nullptr;
+    int seq = 0;
     // pinned host mirrors
     int *h_samples = nullptr, *h_md_list = nullptr, *h_pt_list = nullptr, *h_counts = nullptr, *h_best_slot = nullptr;
     double *h_best = nullptr, *h_err = nullptr, *h_score1 = nullptr;
@@ -86,7 +90,8 @@ struct DeviceCtx {
                         (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
         for (void *p : {(void *)h_samples, (void *)h_md_list, (void *)h_pt_list, (void *)h_counts, (void *)h_best_slot,
-                        (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1})
+                        (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1,
+                        (void *)h_sweep, (void *)h_flag})
             if (p) hipHostFree(p);
         d_pair = d_err = d_scores = d_best = d_score1 = nullptr;
         d_samples = d_md_list = d_pt_list = d_counts = d_best_slot = nullptr;
@@ -99,6 +104,8 @@ struct DeviceCtx {
         h_best = h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
         h_model1 = nullptr;
+        h_sweep = d_sweep = nullptr;
+        h_flag = d_flag = nullptr;
         cap_n = 0;
         cap_b = cap_m = 0;
     }
@@ -136,6 +143,11 @@ struct DeviceCtx {
         MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_model1, sizeof(Model) * 64, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_sweep, sizeof(double) * (3 * nn + 1), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostMalloc(&h_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostGetDevicePointer((void **)&d_sweep, h_sweep, 0));
+        MP_HIP(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
+        *h_flag = seq;
         cap_n = nn;
         cap_b = bb;
         cap_m = mm;
@@ -363,15 +375,22 @@ class Run {
             return err_.data();
         }
         auto t_sw = Clock::now();
-        prepare_score_rec(P_.C, m, X_.h_rec1[0]);
-        MP_HIP(hipMemcpyAsync(X_.d_rec1, X_.h_rec1, sizeof(ScoreRec), hipMemcpyHostToDevice, X_.stream));
-        MP_HIP(launch_sweep(X_.stream, D_, P_.C, X_.d_rec1, X_.d_err, X_.d_score1));
-        MP_HIP(hipMemcpyAsync(X_.h_err, X_.d_err, sizeof(double) * 3 * n_, hipMemcpyDeviceToHost, X_.stream));
-        MP_HIP(hipMemcpyAsync(X_.h_score1, X_.d_score1, sizeof(double), hipMemcpyDeviceToHost, X_.stream));
-        MP_HIP(hipStreamSynchronize(X_.stream));
-        err_.assign(X_.h_err, X_.h_err + 3 * n_);
+        ScoreRec rec;
+        prepare_score_rec(P_.C, m, rec);
+        const int seq = ++X_.seq;
+        MP_HIP(launch_sweep_host(X_.stream, D_, P_.C, rec, X_.d_sweep, X_.d_flag, seq));
+        // poll the completion flag; after 2 s fall back to a stream sync, which also
+        // surfaces any kernel error
+        for (uint64_t spin = 0; __atomic_load_n(X_.h_flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
+            if ((spin & 1023) == 1023 && secs(t_sw) > 2.0) {
+                MP_HIP(hipStreamSynchronize(X_.stream));
+                if (__atomic_load_n(X_.h_flag, __ATOMIC_ACQUIRE) != seq)
+                    throw std::runtime_error("LO sweep did not signal completion");
+            }
+        }
+        err_.assign(X_.h_sweep, X_.h_sweep + 3 * n_);
         cache_model_ = m;
-        cache_score_ = X_.h_score1[0];
+        cache_score_ = X_.h_sweep[3 * n_];
         cache_valid_ = true;
         S_->num_lo_sweeps++;
         if (g_prof_on.load(std::memory_order_relaxed)) {

@@ -34,6 +34,10 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
 // single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);
+// the same sweep writing errors + score (out[3n]) to host-mapped memory and raising
+// *flag = seq (system scope) when done; the host polls the flag
+hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
+                            int *flag, int seq);
 // scores of many explicit models (one workgroup per model) -- used by mp_score_models
 hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
                                double *scores);

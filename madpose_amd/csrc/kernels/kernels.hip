@@ -457,6 +457,38 @@ __global__ void __launch_bounds__(1024) sweep_kernel(PairData D, PairConst C, co
     }
 }
 
+// LO sweep straight into pinned host memory: errors (3 x n) and the gated score are
+// written to host-visible memory, then a completion flag is raised with system
+// scope, so the host polls one word instead of issuing a copy and a stream sync.
+template <int V>
+__global__ void __launch_bounds__(1024) sweep_host_kernel(PairData D, PairConst C, ScoreRec r, double *out,
+                                                          int *flag, int seq) {
+    double acc = 0.0;
+    const bool gate_md = C.score_type == 1, gate_epi = C.score_type == 2;
+    for (int i = threadIdx.x; i < C.n; i += blockDim.x) {
+        const Corr p = load_corr(D, i, V == kCal);
+        double e0, e1, e2;
+        eval_corr<V>(C, r, p, false, e0, e1, e2);
+        out[i] = e0;
+        out[C.n + i] = e1;
+        out[2 * C.n + i] = e2;
+        acc += gate_md ? C.thr[0] * C.w[0] + C.thr[1] * C.w[1] : msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]);
+        acc += gate_epi ? C.thr[2] * C.w[2] : msac(e2, C.thr[2], C.w[2]);
+    }
+    __shared__ double part[16];
+    const double v = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sc = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) sc += part[w];
+        out[3 * C.n] = sc;
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 template <int V>
 __global__ void __launch_bounds__(kBlock) score_models_kernel(PairData D, PairConst C, const ScoreRec *recs,
                                                               double *scores) {
@@ -713,6 +745,14 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
     else
         score_batch_kernel<kTF, kMaxModelsTF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, best, best_slot);
     return hipGetLastError();
+}
+
+hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
+                            int *flag, int seq) {
+    return by_variant(C.variant, [&](auto V) {
+        sweep_host_kernel<decltype(V)::value><<<1, 1024, 0, s>>>(D, C, rec, out, flag, seq);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
