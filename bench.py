@@ -88,7 +88,8 @@ def pmc_traffic_model():
 
 
 COUNTERS = ["elapsed_s", "hypotheses", "iterations", "lo_runs", "lo_s", "score_ms", "solve_ms", "prof_hypotheses",
-            "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms", "prof_iterations"]
+            "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms", "prof_iterations",
+            "sample_ms", "wait_ms", "run_ms"]
 
 
 def gather_counters(local, world):
@@ -148,6 +149,10 @@ def summarize(allv, wl, steps, warmup, world):
         "lo_share": float(c["lo_s"].sum() / c["elapsed_s"].sum()),
         "lo_breakdown": {"lm_calls": int(c["lm_calls"].sum()), "lm_ms": float(c["lm_ms"].sum()),
                          "sweeps": int(c["prof_sweeps"].sum()), "sweep_ms": float(c["sweep_ms"].sum())},
+        # where one pair's wall time goes (host clocks; GPU solve/score from HIP events)
+        "ms_per_pair": {k: float(c[src].sum()) / (world * steps) for k, src in
+                        [("run", "run_ms"), ("batch_wait", "wait_ms"), ("sampling", "sample_ms"), ("lm", "lm_ms"),
+                         ("lo_sweeps", "sweep_ms"), ("gpu_solve", "solve_ms"), ("gpu_score", "score_ms")]},
         "roofline": {
             "bound": "hbm",
             "kernel": "score_batch_kernel",
@@ -226,7 +231,8 @@ def main():
 
     local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
              prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
-             prof["sweep_wall_ms"], prof["iterations"]]
+             prof["sweep_wall_ms"], prof["iterations"], prof["sample_wall_ms"], prof["wait_wall_ms"],
+             prof["run_wall_ms"]]
     allv = gather_counters(local, world)
     if rank == 0:
         res = summarize(allv, wl, a.steps, a.warmup, world)

@@ -145,6 +145,14 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
 /* Point minimal solver (PoseLib relpose_5pt, src/hybrid_pose_estimator.cpp:134) on unit bearings
  * (5 points, point-major 3 doubles each).  Returns count or -code. */
 int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device);
+/* mp_debug_pt5_roots: the engine's batched root stage of the calibrated 5-point
+ * solver (the part of PoseLib relpose_5pt before pose recovery) over ns samples of
+ * five normalized image points (pts0, pts1: ns x 5 x 2, identity intrinsics).
+ * impl 0 = one lane per sample, 1 = one 16-lane group per sample (the default in
+ * the estimator).  cand: ns x 96 doubles, 9 per essential matrix (ascending roots);
+ * ncand: ns counts.  Test hook. */
+int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int32_t *ncand,
+                       int device);
 
 /* Point minimal solvers of the uncalibrated estimators on 2-D points in the
  * estimators' normalized pixel frame ((x - pp) / s, point-major, 2 doubles each),
@@ -180,6 +188,9 @@ typedef struct mp_kernel_profile {
     uint64_t lm_calls;        /* host LM solves inside LO                   */
     double lm_wall_ms;        /* host wall time spent in the LM             */
     double sweep_wall_ms;     /* host wall time of LO sweeps (incl. copies) */
+    double sample_wall_ms;    /* host minimal-sample generation + rewinds   */
+    double wait_wall_ms;      /* host wait for speculative batch results    */
+    double run_wall_ms;       /* whole estimator runs                       */
 } mp_kernel_profile;
 int mp_profile_enable(int on);
 int mp_profile_reset(void);

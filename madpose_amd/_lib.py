@@ -99,6 +99,9 @@ class mp_kernel_profile(ctypes.Structure):
         ("lm_calls", ctypes.c_uint64),
         ("lm_wall_ms", ctypes.c_double),
         ("sweep_wall_ms", ctypes.c_double),
+        ("sample_wall_ms", ctypes.c_double),
+        ("wait_wall_ms", ctypes.c_double),
+        ("run_wall_ms", ctypes.c_double),
     ]
 
 
@@ -125,6 +128,8 @@ EXPORTS = {
                                        ctypes.POINTER(mp_estimator_config), ctypes.POINTER(mp_model), ctypes.c_int32,
                                        c_double_p, c_double_p, ctypes.c_int]),
     "mp_relpose_5pt": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int, ctypes.c_int]),
+    "mp_debug_pt5_roots": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p,
+                                          ctypes.POINTER(ctypes.c_int32), ctypes.c_int]),
     "mp_relpose_6pt_shared_focal": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int,
                                                    ctypes.c_int]),
     "mp_relpose_7pt_two_focal": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int,

@@ -262,6 +262,15 @@ static int point_direct(int kind, const double *x1, const double *x2, mp_model *
     return r <= -1000 ? -(r + 1000) : -r;
 }
 
+int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int32_t *ncand,
+                       int device) {
+    if (!pts0 || !pts1 || !cand || !ncand) return fail(MP_EINVAL, "null pointer");
+    return guarded([&] {
+        mp::debug_pt5_roots(impl, ns, pts0, pts1, cand, ncand, device);
+        return MP_OK;
+    });
+}
+
 int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device) {
     return point_direct(0, x1, x2, out, max_out, device);
 }
@@ -338,6 +347,9 @@ int mp_profile_read(mp_kernel_profile *out) {
     out->lm_calls = p.lm_calls;
     out->lm_wall_ms = p.lm_wall_ms;
     out->sweep_wall_ms = p.sweep_wall_ms;
+    out->sample_wall_ms = p.sample_wall_ms;
+    out->wait_wall_ms = p.wait_wall_ms;
+    out->run_wall_ms = p.run_wall_ms;
     return MP_OK;
 }
 

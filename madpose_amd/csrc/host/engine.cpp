@@ -29,9 +29,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "../include/mp_score.h"
 #include "../kernels/kernels.h"
@@ -52,6 +55,114 @@ using Clock = std::chrono::steady_clock;
 double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::now() - a).count(); }
 
 const double kMax = DBL_MAX;
+
+// ---------------------------------------------------------------------------
+// Minimal-sample batches (host).  One batch holds its iterations' solver types and
+// samples (in a pinned host slot), plus snapshots of both random streams every
+// kSnap iterations so a rewind to iteration j replays fewer than kSnap iterations.
+constexpr uint32_t kSnap = 2048;
+struct Batch {
+    uint32_t B = 0;
+    int nmd = 0, npt = 0, slot = 0;
+    std::vector<uint8_t> types;
+    std::vector<IterationStream> snaps;
+};
+
+// Draws B iterations from rs into g (samples / md list / pt list of slot memory);
+// returns false if *abort was raised first (checked every 256 iterations).
+bool draw_batch(IterationStream &rs, Batch &g, uint32_t B, int slot, int *smp, int *md, int *pt,
+                const std::atomic<bool> *abort) {
+    g.B = B;
+    g.slot = slot;
+    g.nmd = g.npt = 0;
+    g.types.resize(B);
+    g.snaps.clear();
+    for (uint32_t j = 0; j < B; ++j) {
+        if (j % kSnap == 0) g.snaps.push_back(rs);
+        if (abort && (j & 255) == 0 && abort->load(std::memory_order_relaxed)) return false;
+        const int st = rs.next(smp + 8 * j);
+        g.types[j] = (uint8_t)st;
+        if (st == 0)
+            md[g.nmd++] = (int)j;
+        else
+            pt[g.npt++] = (int)j;
+    }
+    return true;
+}
+
+// Background sampler: draws the next speculative batch while the current one is on
+// the GPU and the host replays it / runs LO.  The batch is kept only if the current
+// one neither triggers LO nor terminates, so the worker can be told to give up.
+class Sampler {
+  public:
+    Sampler() : th_([this] { loop(); }) {}
+    ~Sampler() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+            abort_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // starts drawing B iterations from `from` into *g (the caller must not touch *g
+    // or the slot memory until finish()/cancel() returned)
+    void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp, int *md, int *pt) {
+        std::lock_guard<std::mutex> lk(mu_);
+        rs_ = from;
+        g_ = g;
+        B_ = B;
+        slot_ = slot;
+        smp_ = smp;
+        md_ = md;
+        pt_ = pt;
+        abort_ = false;
+        busy_ = true;
+        ok_ = false;
+        ++gen_;
+        cv_.notify_all();
+    }
+    // waits for the batch; on success *rs is the stream state after it
+    bool finish(IterationStream *rs) {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return !busy_; });
+        if (ok_) *rs = rs_;
+        return ok_;
+    }
+    void cancel() {
+        abort_ = true;
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return !busy_; });
+    }
+
+  private:
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+            if (quit_) return;
+            seen = gen_;
+            lk.unlock();
+            const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, md_, pt_, &abort_);
+            lk.lock();
+            ok_ = ok;
+            busy_ = false;
+            done_cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    IterationStream rs_;
+    Batch *g_ = nullptr;
+    uint32_t B_ = 0;
+    int slot_ = 0;
+    int *smp_ = nullptr, *md_ = nullptr, *pt_ = nullptr;
+    std::atomic<bool> abort_{false};
+    bool busy_ = false, ok_ = false, quit_ = false;
+    uint64_t gen_ = 0;
+    std::thread th_;
+};
 
 // ---------------------------------------------------------------------------
 // Device context: stream + cached buffers (one per device and concurrent caller)
@@ -75,19 +186,25 @@ struct DeviceCtx {
     double *h_sweep = nullptr, *d_sweep = nullptr;
     int *h_flag = nullptr, *d_flag = nullptr;
     int seq = 0;
+    double *d_sweep_part = nullptr; // per-workgroup partial scores of a sweep
+    unsigned *d_sweep_cnt = nullptr;
     // pinned host mirrors
     int *h_samples = nullptr, *h_md_list = nullptr, *h_pt_list = nullptr, *h_counts = nullptr, *h_best_slot = nullptr;
     double *h_best = nullptr, *h_err = nullptr, *h_score1 = nullptr;
     ScoreRec *h_rec1 = nullptr;
     Model *h_model1 = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr}; // solve start / score start / score end
+    // the MD solver runs on md_stream, concurrently with the point-solver stages
+    hipStream_t md_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    std::unique_ptr<Sampler> sampler;               // created on first use
 
     void free_all() {
         hipSetDevice(device);
         for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_md_list, (void *)d_pt_list, (void *)d_counts,
                         (void *)d_best_slot, (void *)d_models, (void *)d_recs, (void *)d_scores, (void *)d_best,
                         (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_ncand,
-                        (void *)d_pt_valid, (void *)d_pt_slots})
+                        (void *)d_pt_valid, (void *)d_pt_slots, (void *)d_sweep_part, (void *)d_sweep_cnt})
             if (p) hipFree(p);
         for (void *p : {(void *)h_samples, (void *)h_md_list, (void *)h_pt_list, (void *)h_counts, (void *)h_best_slot,
                         (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1,
@@ -106,6 +223,8 @@ struct DeviceCtx {
         h_model1 = nullptr;
         h_sweep = d_sweep = nullptr;
         h_flag = d_flag = nullptr;
+        d_sweep_part = nullptr;
+        d_sweep_cnt = nullptr;
         cap_n = 0;
         cap_b = cap_m = 0;
     }
@@ -133,9 +252,13 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_pt_valid, sizeof(int) * (size_t)bb * kPtSlotStride));
         MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb * kPtSlotStride));
         MP_HIP(hipMalloc(&d_score1, sizeof(double) * 64));
-        MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 8 * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_md_list, sizeof(int) * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_pt_list, sizeof(int) * bb, hipHostMallocDefault));
+        MP_HIP(hipMalloc(&d_sweep_part, sizeof(double) * sweep_blocks(nn)));
+        MP_HIP(hipMalloc(&d_sweep_cnt, sizeof(unsigned)));
+        MP_HIP(hipMemsetAsync(d_sweep_cnt, 0, sizeof(unsigned), stream));
+        // two slots each: the next batch is generated while the current one is in flight
+        MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 8 * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_md_list, sizeof(int) * 2 * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_pt_list, sizeof(int) * 2 * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_counts, sizeof(int) * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_best_slot, sizeof(int) * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_best, sizeof(double) * bb, hipHostMallocDefault));
@@ -182,7 +305,10 @@ struct CtxLease {
             c->device = device;
             MP_HIP(hipSetDevice(device));
             MP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            MP_HIP(hipStreamCreateWithFlags(&c->md_stream, hipStreamNonBlocking));
             for (auto &e : c->ev) MP_HIP(hipEventCreate(&e));
+            MP_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+            MP_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
         }
         MP_HIP(hipSetDevice(device));
     }
@@ -367,6 +493,7 @@ class Run {
     bool cache_valid_ = false;
     double cache_score_ = 0.0;
     std::vector<double> err_;
+    double sample_s_ = 0.0;
 
     // --- GPU sweeps ---
     const double *sweep(const Model &m, double *score) {
@@ -378,7 +505,7 @@ class Run {
         ScoreRec rec;
         prepare_score_rec(P_.C, m, rec);
         const int seq = ++X_.seq;
-        MP_HIP(launch_sweep_host(X_.stream, D_, P_.C, rec, X_.d_sweep, X_.d_flag, seq));
+        MP_HIP(launch_sweep_host(X_.stream, D_, P_.C, rec, X_.d_sweep, X_.d_flag, seq, X_.d_sweep_part, X_.d_sweep_cnt));
         // poll the completion flag; after 2 s fall back to a stream sync, which also
         // surfaces any kernel error
         for (uint64_t spin = 0; __atomic_load_n(X_.h_flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
@@ -570,6 +697,34 @@ class Run {
         S_->seconds_lo += secs(t0);
     }
 
+    // --- minimal-sample batches (host) ---
+    // Batches drawn on this thread (at the start, after LO or a cut batch) are sized so
+    // drawing them costs about one batch round trip on the GPU: cheap solvers get short
+    // synchronous batches (the worker draws the long ones), expensive ones long.
+    double draw_s_per_it_ = 40e-9, batch_s_ = 1e-3; // running estimates
+    uint32_t sync_batch(uint32_t want) const {
+        const double b = batch_s_ / std::max(draw_s_per_it_, 1e-9);
+        return std::min<uint32_t>(want, (uint32_t)std::max<double>(min_batch_, std::min<double>(b, 1e9)));
+    }
+    int *slot_ptr(int which, int slot) const {
+        const size_t so = (size_t)slot * max_batch_;
+        return which == 0 ? X_.h_samples + 8 * so : which == 1 ? X_.h_md_list + so : X_.h_pt_list + so;
+    }
+    void generate(Batch &g, uint32_t B, int slot) {
+        auto t0 = Clock::now();
+        draw_batch(rs_, g, B, slot, slot_ptr(0, slot), slot_ptr(1, slot), slot_ptr(2, slot), nullptr);
+        sample_s_ += secs(t0);
+    }
+    // both streams to the end of iteration j of batch g
+    void rewind(const Batch &g, uint32_t j) {
+        auto t0 = Clock::now();
+        const uint32_t k = j / kSnap;
+        rs_ = g.snaps[k];
+        int scratch[8];
+        for (uint32_t r = k * kSnap; r <= j; ++r) rs_.next(scratch);
+        sample_s_ += secs(t0);
+    }
+
     Model fetch_model(int b, int slot) {
         MP_HIP(hipMemcpyAsync(X_.h_model1, X_.d_models + (size_t)b * maxm_ + slot, sizeof(Model),
                               hipMemcpyDeviceToHost, X_.stream));
@@ -599,6 +754,7 @@ void Run::run(Model *best, Stats *S) {
         return;
     }
     X_.ensure(n_, max_batch_, maxm_);
+    if (!X_.sampler) X_.sampler.reset(new Sampler());
     upload_pair(X_, P_, &D_);
     rs_.n = n_;
     rs_.seed(o_.random_seed);
@@ -614,35 +770,60 @@ void Run::run(Model *best, Stats *S) {
     uint32_t it = 0;
     bool done = false;
     int bcur = min_batch_;
-    std::vector<uint8_t> types(max_batch_);
+    // batch size at position `at`: the solver kernels are latency-bound (cost ~flat
+    // up to tens of thousands of samples) and new bests -- the only thing that cuts
+    // a batch -- thin out like records of an iid sequence, so speculate on a window
+    // proportional to the position in the stream; batches stop at lo_start.
+    auto batch_size = [&](uint32_t at, uint32_t want) {
+        uint32_t B = std::min<uint32_t>(want, max_total - at);
+        if (at < lo_start) B = std::min<uint32_t>(B, lo_start - at);
+        return B;
+    };
+    Batch gen[2];
+    // the worker may be drawing into gen[] when an exception unwinds this frame
+    struct CancelOnExit {
+        Sampler *s;
+        ~CancelOnExit() { s->cancel(); }
+    } cancel_on_exit{X_.sampler.get()};
+    int cur = 0;
+    bool have_next = false; // gen[cur] already holds the batch starting at `it`
     while (it < max_total && !done) {
         if (it == lo_start && best_min_score < kMax) {
             ++S->number_lo_iterations;
             local_opt(S->best_solver_type, best, &S->best_model_score, &S->best_solver_type);
             termination(*best, max_per);
         }
-        uint32_t B = std::min<uint32_t>((uint32_t)bcur, max_total - it);
-        if (it < lo_start) B = std::min<uint32_t>(B, lo_start - it);
-        const IterationStream rs0 = rs_;
-        int nmd = 0, npt = 0;
-        for (uint32_t j = 0; j < B; ++j) {
-            const int st = rs_.next(X_.h_samples + 8 * j);
-            types[j] = (uint8_t)st;
-            if (st == 0)
-                X_.h_md_list[nmd++] = (int)j;
-            else
-                X_.h_pt_list[npt++] = (int)j;
+        // (drawn here only at the start and after LO / a cut batch: kept short so the
+        // GPU starts early and the worker draws the big ones)
+        if (!have_next) {
+            auto t0 = Clock::now();
+            generate(gen[cur], batch_size(it, sync_batch((uint32_t)bcur)), cur);
+            if (gen[cur].B >= 256) draw_s_per_it_ = 0.5 * draw_s_per_it_ + 0.5 * secs(t0) / gen[cur].B;
         }
+        auto t_batch = Clock::now();
+        const Batch &g = gen[cur];
+        const uint32_t B = g.B;
+        const int nmd = g.nmd, npt = g.npt;
         hipStream_t s = X_.stream;
         const bool prof = g_prof_on.load(std::memory_order_relaxed);
-        MP_HIP(hipMemcpyAsync(X_.d_samples, X_.h_samples, sizeof(int) * 8 * B, hipMemcpyHostToDevice, s));
-        MP_HIP(hipMemcpyAsync(X_.d_md_list, X_.h_md_list, sizeof(int) * std::max(nmd, 1), hipMemcpyHostToDevice, s));
-        MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
+        const size_t so = (size_t)g.slot * max_batch_;
+        MP_HIP(hipMemcpyAsync(X_.d_samples, X_.h_samples + 8 * so, sizeof(int) * 8 * B, hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(X_.d_md_list, X_.h_md_list + so, sizeof(int) * std::max(nmd, 1), hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list + so, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
         if (prof) MP_HIP(hipEventRecord(X_.ev[0], s));
-        MP_HIP(launch_md_solve(s, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs, X_.d_counts, maxm_));
+        // MD iterations on the side stream, point iterations on the main one (they
+        // write disjoint model slots); scoring waits for both
+        if (nmd > 0) {
+            MP_HIP(hipEventRecord(X_.ev_fork, s));
+            MP_HIP(hipStreamWaitEvent(X_.md_stream, X_.ev_fork, 0));
+            MP_HIP(launch_md_solve(X_.md_stream, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs,
+                                   X_.d_counts, maxm_));
+            MP_HIP(hipEventRecord(X_.ev_join, X_.md_stream));
+        }
         const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid};
         MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
                                maxm_));
+        if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
         if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
         MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_best,
                                   X_.d_best_slot));
@@ -650,9 +831,22 @@ void Run::run(Model *best, Stats *S) {
         MP_HIP(hipMemcpyAsync(X_.h_best, X_.d_best, sizeof(double) * B, hipMemcpyDeviceToHost, s));
         MP_HIP(hipMemcpyAsync(X_.h_best_slot, X_.d_best_slot, sizeof(int) * B, hipMemcpyDeviceToHost, s));
         MP_HIP(hipMemcpyAsync(X_.h_counts, X_.d_counts, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        // While the batch is in flight, the sampler thread draws the next one into the
+        // other slot.  It is kept if this batch neither triggers LO nor terminates (both
+        // rewind the streams); never across lo_start, where an LO runs before the next
+        // batch.
+        const uint32_t it_next = it + B;
+        const uint32_t Bn = (it_next < max_total && it_next != lo_start)
+                                ? batch_size(it_next, (uint32_t)std::min<uint64_t>(
+                                                          (uint64_t)max_batch_,
+                                                          std::max<uint64_t>((uint64_t)min_batch_, 4ull * it_next)))
+                                : 0;
+        if (Bn > 0) X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(0, cur ^ 1), slot_ptr(1, cur ^ 1),
+                                      slot_ptr(2, cur ^ 1));
         auto tw = Clock::now();
         MP_HIP(hipStreamSynchronize(s));
         S->seconds_gpu_wait += secs(tw);
+        batch_s_ = 0.5 * batch_s_ + 0.5 * secs(t_batch);
         S->num_batches++;
         if (prof) {
             float ms_solve = 0.f, ms_score = 0.f;
@@ -673,7 +867,7 @@ void Run::run(Model *best, Stats *S) {
         uint32_t j = 0;
         for (; j < B; ++j) {
             const uint32_t iter = it + j;
-            const int st = types[j];
+            const int st = g.types[j];
             S->num_iterations_per_solver[st] += 1;
             const int nm = X_.h_counts[j];
             S->num_hypotheses += (uint64_t)nm;
@@ -692,9 +886,7 @@ void Run::run(Model *best, Stats *S) {
                     if (new_best || run_lo) {
                         if (run_lo) {
                             // rewind both streams to the end of iteration `iter`
-                            rs_ = rs0;
-                            int scratch[8];
-                            for (uint32_t r = 0; r <= j; ++r) rs_.next(scratch);
+                            rewind(g, j);
                             ++S->number_lo_iterations;
                             double sc = best_min_score;
                             local_opt(S->best_solver_type, &best_min, &sc, &S->best_solver_type);
@@ -711,11 +903,7 @@ void Run::run(Model *best, Stats *S) {
                 // `break` in the reference skips the loop increment
                 S->num_iterations_total = iter;
                 done = true;
-                if (!lo_here) {
-                    rs_ = rs0;
-                    int scratch[8];
-                    for (uint32_t r = 0; r <= j; ++r) rs_.next(scratch);
-                }
+                if (!lo_here) rewind(g, j);
                 break;
             }
             if (invalidated) {
@@ -723,11 +911,20 @@ void Run::run(Model *best, Stats *S) {
                 break;
             }
         }
-        if (!done && !invalidated) it += B;
-        // batch-size schedule: the solver kernels are latency-bound (cost ~flat up to
-        // tens of thousands of samples) and new bests -- the only thing that cuts a
-        // batch -- thin out like records of an iid sequence, so speculate on a window
-        // proportional to the position in the stream.
+        if (!done && !invalidated) {
+            it += B;
+            have_next = false;
+            if (Bn > 0) { // rs_ moves to the end of the drawn batch
+                auto t0 = Clock::now();
+                have_next = X_.sampler->finish(&rs_);
+                sample_s_ += secs(t0);
+                if (have_next) cur ^= 1;
+            }
+            // (otherwise rs_ stands at the end of this batch)
+        } else {
+            if (Bn > 0) X_.sampler->cancel();
+            have_next = false;
+        }
         bcur = (int)std::min<uint64_t>((uint64_t)max_batch_, std::max<uint64_t>((uint64_t)min_batch_, 4ull * it));
     }
     if (!done) S->num_iterations_total = it;
@@ -750,6 +947,12 @@ void Run::run(Model *best, Stats *S) {
         S->seconds_lo += secs(t0);
     }
     S->seconds_total = secs(t_start);
+    if (g_prof_on.load(std::memory_order_relaxed)) {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof.sample_wall_ms += 1e3 * sample_s_;
+        g_prof.wait_wall_ms += 1e3 * S->seconds_gpu_wait;
+        g_prof.run_wall_ms += 1e3 * S->seconds_total;
+    }
 }
 
 void validate(const PairInput &in, const RansacOptions &o) {
@@ -886,6 +1089,53 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
     hipFree(d_poses);
     for (int i = 0; i < std::min(std::min(hn, kCap), max_poses); ++i) poses[i] = hp[i];
     return hn;
+}
+
+void debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int *ncand,
+                     int device) {
+    if (impl < 0 || impl > 1) throw std::invalid_argument("impl must be 0 (lane) or 1 (group)");
+    if (ns <= 0 || ns > (1 << 22)) throw std::invalid_argument("bad number of samples");
+    CtxLease lease(device);
+    DeviceCtx &X = *lease.c;
+    const int64_t np = 5 * ns;
+    // one correspondence per sample point, identity intrinsics, sample s = points 5s..5s+4
+    std::vector<double> host(8 * (size_t)np);
+    for (int64_t i = 0; i < np; ++i) {
+        host[i] = pts0[2 * i];
+        host[np + i] = pts0[2 * i + 1];
+        host[2 * np + i] = pts1[2 * i];
+        host[3 * np + i] = pts1[2 * i + 1];
+        host[4 * np + i] = host[5 * np + i] = 1.0;
+        host[6 * np + i] = 1.0 / std::sqrt(pts0[2 * i] * pts0[2 * i] + pts0[2 * i + 1] * pts0[2 * i + 1] + 1.0);
+        host[7 * np + i] = 1.0 / std::sqrt(pts1[2 * i] * pts1[2 * i] + pts1[2 * i + 1] * pts1[2 * i + 1] + 1.0);
+    }
+    std::vector<int> smp(8 * (size_t)ns, 0), list(ns);
+    for (int64_t s = 0; s < ns; ++s) {
+        list[s] = (int)s;
+        for (int j = 0; j < 5; ++j) smp[8 * s + j] = (int)(5 * s + j);
+    }
+    double *d_pair, *d_cand;
+    int *d_smp, *d_list, *d_n;
+    MP_HIP(hipMalloc(&d_pair, sizeof(double) * host.size()));
+    MP_HIP(hipMalloc(&d_cand, sizeof(double) * kPtCandStride * (size_t)ns));
+    MP_HIP(hipMalloc(&d_smp, sizeof(int) * smp.size()));
+    MP_HIP(hipMalloc(&d_list, sizeof(int) * list.size()));
+    MP_HIP(hipMalloc(&d_n, sizeof(int) * (size_t)ns));
+    MP_HIP(hipMemcpyAsync(d_pair, host.data(), sizeof(double) * host.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemcpyAsync(d_smp, smp.data(), sizeof(int) * smp.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemcpyAsync(d_list, list.data(), sizeof(int) * list.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemsetAsync(d_cand, 0, sizeof(double) * kPtCandStride * (size_t)ns, X.stream));
+    PairData D{d_pair, d_pair + np, d_pair + 2 * np, d_pair + 3 * np, d_pair + 4 * np, d_pair + 5 * np,
+               d_pair + 6 * np, d_pair + 7 * np};
+    PairConst C{};
+    C.variant = kCal;
+    C.n = (int)np;
+    for (int k = 0; k < 9; ++k) C.K0[k] = C.K1[k] = C.K0i[k] = C.K1i[k] = (k % 4 == 0) ? 1.0 : 0.0;
+    MP_HIP(launch_pt5_roots(X.stream, D, C, d_list, (int)ns, d_smp, d_cand, d_n, impl));
+    MP_HIP(hipMemcpyAsync(cand, d_cand, sizeof(double) * kPtCandStride * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(ncand, d_n, sizeof(int) * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipStreamSynchronize(X.stream));
+    for (void *p : {(void *)d_pair, (void *)d_cand, (void *)d_smp, (void *)d_list, (void *)d_n}) hipFree(p);
 }
 
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device) {

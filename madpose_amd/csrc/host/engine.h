@@ -67,6 +67,10 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
 // kind 0: relpose_5pt on unit bearings; 1: shared-focal 6pt; 2: two-focal 7pt +
 // Bougnoux + recoverPose (normalized 2-D points).  Models before the depth fit.
 int solve_point_direct(int kind, const double *x1, const double *x2, Model *poses, int max_poses, int device);
+// root stage of the calibrated 5-point solver over ns samples of 5 normalized image
+// points each (pts*: ns x 5 x 2); E's into cand (ns x 96), counts into ncand
+void debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int *ncand,
+                     int device);
 
 // estimate_scale_and_pose (src/solver.cpp:5-33) on the device; X, Y point-major n x 3
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device);
@@ -86,6 +90,9 @@ struct KernelProfile {
     uint64_t lm_calls = 0;         // host LM solves inside LO
     double lm_wall_ms = 0.0;       // host wall time in the LM
     double sweep_wall_ms = 0.0;    // host wall time of single-model sweeps (incl. copies + sync)
+    double sample_wall_ms = 0.0;   // host minimal-sample generation (incl. LO rewinds)
+    double wait_wall_ms = 0.0;     // host wait for batch results
+    double run_wall_ms = 0.0;      // whole estimator runs
 };
 void profile_enable(bool on);
 void profile_reset();

@@ -24,23 +24,33 @@ class Mt19937 {
     }
     uint32_t operator()() {
         if (idx_ >= 624) twist();
-        uint32_t y = mt_[idx_++];
-        y ^= y >> 11;
-        y ^= (y << 7) & 0x9d2c5680u;
-        y ^= (y << 15) & 0xefc60000u;
-        y ^= y >> 18;
-        return y;
+        return out_[idx_++];
     }
 
   private:
+    // the recurrence split at the two wrap points so the inner loops carry no modulo
+    // and vectorize; the 624 outputs of a block are tempered in one pass
+    static inline uint32_t step(uint32_t cur, uint32_t nxt, uint32_t far) {
+        const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+        return far ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
     void twist() {
-        for (int i = 0; i < 624; ++i) {
-            const uint32_t y = (mt_[i] & 0x80000000u) | (mt_[(i + 1) % 624] & 0x7fffffffu);
-            mt_[i] = mt_[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        int i = 0;
+        for (; i < 624 - 397; ++i) mt_[i] = step(mt_[i], mt_[i + 1], mt_[i + 397]);
+        for (; i < 623; ++i) mt_[i] = step(mt_[i], mt_[i + 1], mt_[i + 397 - 624]);
+        mt_[623] = step(mt_[623], mt_[0], mt_[396]);
+        for (i = 0; i < 624; ++i) {
+            uint32_t y = mt_[i];
+            y ^= y >> 11;
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= y >> 18;
+            out_[i] = y;
         }
         idx_ = 0;
     }
     uint32_t mt_[624];
+    uint32_t out_[624];
     int idx_;
 };
 
@@ -61,12 +71,28 @@ inline int uniform_int(Mt19937 &g, int a, int b) {
     return (int)((uint32_t)a + (uint32_t)(product >> 32));
 }
 
+// uniform_int(g, 0, range - 1) with the rejection threshold precomputed: identical
+// draws (low < threshold implies low < range, so the two-step test above reduces
+// to this one)
+struct UniformIndex {
+    uint32_t range = 1, threshold = 0;
+    void set(uint32_t r) {
+        range = r;
+        threshold = (uint32_t)(-r) % r;
+    }
+    inline int operator()(Mt19937 &g) const {
+        uint64_t product = (uint64_t)g() * (uint64_t)range;
+        while ((uint32_t)product < threshold) product = (uint64_t)g() * (uint64_t)range;
+        return (int)(uint32_t)(product >> 32);
+    }
+};
+
 // uniform real in [a, b)
 inline double uniform_real(Mt19937 &g, double a, double b) {
     const double r = 4294967296.0; // 2^32
     double sum = (double)g();
     sum += (double)g() * r;
-    double c = sum / (r * r);
+    double c = sum * 0x1p-64; // == sum / 2^64 exactly
     if (c >= 1.0) c = std::nextafter(1.0, 0.0);
     return (b - a) * c + a;
 }
@@ -83,10 +109,41 @@ struct IterationStream {
     double prior[2] = {1.0, 1.0};
     int ss[2][3] = {{3, 3, 0}, {0, 0, 5}};
     int n = 0;
+    UniformIndex pick;
 
     void seed(uint32_t s) {
         sel.seed_with(s);
         samp.seed_with(s);
+    }
+    // K distinct draws into out (redrawing duplicates)
+    template <int K> inline void distinct(int *out) {
+        for (int i = 0; i < K; ++i) {
+            int v;
+            bool dup;
+            do {
+                v = pick(samp);
+                dup = false;
+                for (int j = 0; j < i; ++j) dup |= out[j] == v;
+            } while (dup);
+            out[i] = v;
+        }
+    }
+    inline void distinct(int k, int *out) {
+        switch (k) {
+        case 3: distinct<3>(out); break;
+        case 5: distinct<5>(out); break;
+        default:
+            for (int i = 0; i < k; ++i) {
+                int v;
+                bool dup;
+                do {
+                    v = pick(samp);
+                    dup = false;
+                    for (int j = 0; j < i; ++j) dup |= out[j] == v;
+                } while (dup);
+                out[i] = v;
+            }
+        }
     }
     int next(int *idx) {
         const double u = uniform_real(sel, 0.0, prior[0] + prior[1]);
@@ -101,23 +158,13 @@ struct IterationStream {
             }
         }
         if (st < 0) st = prior[1] > 0 ? 1 : 0; // unreachable: u < prior sum
+        if (pick.range != (uint32_t)n) pick.set((uint32_t)n);
         int tmp[8];
         for (int t = 0; t < 3; ++t) {
             const int k = ss[st][t];
-            for (int i = 0; i < k; ++i) {
-                bool dup = true;
-                while (dup) {
-                    tmp[i] = uniform_int(samp, 0, n - 1);
-                    dup = false;
-                    for (int j = 0; j < i; ++j)
-                        if (tmp[j] == tmp[i]) {
-                            dup = true;
-                            break;
-                        }
-                }
-            }
-            if ((st == 0 && t == 0) || (st == 1 && t == 2))
-                for (int j = 0; j < k; ++j) idx[j] = tmp[j];
+            if (k == 0) continue;
+            const bool keep = (st == 0 && t == 0) || (st == 1 && t == 2);
+            distinct(k, keep ? idx : tmp);
         }
         return st;
     }

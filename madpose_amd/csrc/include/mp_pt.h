@@ -13,6 +13,8 @@
 // PoseLib is not vendored, so this solver is pinned against the oracle's
 // independent Stewenius action-matrix solver (tests/test_point_solvers.py).
 #pragma once
+#include <utility>
+
 #include "mp_md.h"
 
 namespace mp {
@@ -131,84 +133,88 @@ struct Cub {
     double c[20];
 }; // mono_col layout
 
+// The products below are expanded with compile-time indices (fold expressions over
+// an index sequence) rather than loops: with loop indices the output slot
+// quad_index / mono_col is only constant after unrolling, which comes too late for
+// the accumulators to leave private (scratch) memory.  Terms are accumulated in
+// the order of the loops they replace: i outer, j inner (lin_mul); a, b >= a, c
+// (quad_lin_acc).
+template <int K> MP_HD void lin_mul_term(const Lin &a, const Lin &b, Quad &o) {
+    constexpr int slot = quad_index(K / 4, K % 4);
+    o.c[slot] += a.c[K / 4] * b.c[K % 4];
+}
+template <int... K> MP_HD void lin_mul_all(const Lin &a, const Lin &b, Quad &o, std::integer_sequence<int, K...>) {
+    (lin_mul_term<K>(a, b, o), ...);
+}
 MP_HD void lin_mul(const Lin &a, const Lin &b, Quad &o) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) o.c[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o.c[quad_index(i, j)] += a.c[i] * b.c[j];
+    static_for<10>([&](auto i) { o.c[i] = 0.0; });
+    lin_mul_all(a, b, o, std::make_integer_sequence<int, 16>());
 }
 
+template <int A, int B, int Cc> MP_HD void quad_lin_term(const Quad &q, const Lin &l, double s, Cub &o) {
+    if constexpr (A <= B) {
+        constexpr int ex = lin_e(A, 0) + lin_e(B, 0) + lin_e(Cc, 0);
+        constexpr int ey = lin_e(A, 1) + lin_e(B, 1) + lin_e(Cc, 1);
+        constexpr int ez = lin_e(A, 2) + lin_e(B, 2) + lin_e(Cc, 2);
+        constexpr int slot = mono_col(ex, ey, ez), qs = quad_index(A, B);
+        o.c[slot] += s * q.c[qs] * l.c[Cc];
+    }
+}
+template <int... K>
+MP_HD void quad_lin_all(const Quad &q, const Lin &l, double s, Cub &o, std::integer_sequence<int, K...>) {
+    (quad_lin_term<K / 16, (K / 4) % 4, K % 4>(q, l, s, o), ...);
+}
 MP_HD void quad_lin_acc(const Quad &q, const Lin &l, double s, Cub &o) {
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = a; b < 4; ++b)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int ex = lin_e(a, 0) + lin_e(b, 0) + lin_e(c, 0);
-                const int ey = lin_e(a, 1) + lin_e(b, 1) + lin_e(c, 1);
-                const int ez = lin_e(a, 2) + lin_e(b, 2) + lin_e(c, 2);
-                o.c[mono_col(ex, ey, ez)] += s * q.c[quad_index(a, b)] * l.c[c];
-            }
+    quad_lin_all(q, l, s, o, std::make_integer_sequence<int, 64>());
 }
 
 // Householder null space of the 5x9 system (rows = points), returning 4 basis
 // vectors of length 9 (E row-major coefficients).
 MP_HD void nullspace_5x9(const double (&Q)[5][9], double (&N)[4][9]) {
+    // (compile-time indices throughout: see static_for in mp_types.h)
     double A[9][5]; // Q^T
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-#pragma unroll
-        for (int e = 0; e < 9; ++e) A[e][i] = Q[i][e];
+    static_for<5>([&](auto i) { static_for<9>([&](auto e) { A[e][i] = Q[i][e]; }); });
     double V[5][9], beta[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    static_for<5>([&](auto k) {
         double nrm = 0.0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i)
-            if (i >= k) nrm += A[i][k] * A[i][k];
+        static_for<9>([&](auto i) {
+            if constexpr (i >= k) nrm += A[i][k] * A[i][k];
+        });
         nrm = sqrt(nrm);
         const double alpha = (A[k][k] > 0) ? -nrm : nrm;
         double vn = 0.0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            V[k][i] = (i < k) ? 0.0 : A[i][k];
-            if (i == k) V[k][i] -= alpha;
-            vn += V[k][i] * V[k][i];
-        }
-        beta[k] = (vn > 0) ? 2.0 / vn : 0.0;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            if (j >= k) {
-                double d = 0.0;
-#pragma unroll
-                for (int i = 0; i < 9; ++i) d += V[k][i] * A[i][j];
-                d *= beta[k];
-#pragma unroll
-                for (int i = 0; i < 9; ++i) A[i][j] -= d * V[k][i];
+        static_for<9>([&](auto i) {
+            if constexpr (i < k) {
+                V[k][i] = 0.0;
+            } else {
+                V[k][i] = A[i][k];
+                if constexpr (i == k) V[k][i] -= alpha;
             }
-        }
-    }
+            vn += V[k][i] * V[k][i];
+        });
+        beta[k] = (vn > 0) ? 2.0 / vn : 0.0;
+        static_for<5>([&](auto j) {
+            if constexpr (j >= k) {
+                double d = 0.0;
+                static_for<9>([&](auto i) { d += V[k][i] * A[i][j]; });
+                d *= beta[k];
+                static_for<9>([&](auto i) { A[i][j] -= d * V[k][i]; });
+            }
+        });
+    });
     // columns 5..8 of Q = H0 H1 H2 H3 H4 applied to unit vectors
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    static_for<4>([&](auto b) {
         double v[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) v[i] = (i == 5 + b) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 4; k >= 0; --k) {
+        static_for<9>([&](auto i) { v[i] = (i == 5 + b) ? 1.0 : 0.0; });
+        static_for<5>([&](auto kk) {
+            constexpr int k = 4 - kk;
             double d = 0.0;
-#pragma unroll
-            for (int i = 0; i < 9; ++i) d += V[k][i] * v[i];
+            static_for<9>([&](auto i) { d += V[k][i] * v[i]; });
             d *= beta[k];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) v[i] -= d * V[k][i];
-        }
-#pragma unroll
-        for (int i = 0; i < 9; ++i) N[b][i] = v[i];
-    }
+            static_for<9>([&](auto i) { v[i] -= d * V[k][i]; });
+        });
+        static_for<9>([&](auto i) { N[b][i] = v[i]; });
+    });
 }
 
 // The 5-point system of one sample: null-space basis, the hidden-variable matrix

@@ -1,6 +1,8 @@
 // Shared types of the MI355X hybrid-RANSAC engine (device kernels + host controller).
 #pragma once
 #include <cstdint>
+#include <type_traits>
+#include <utility>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -59,6 +61,17 @@ struct PairData {
 constexpr int kMaxModelsCal = 10; // MD <= 4, 5pt <= 10
 constexpr int kMaxModelsSF = 16;  // MD <= 8, 6pt <= 15
 constexpr int kMaxModelsTF = 4;   // MD <= 4, 7pt <= 3
+// static_for<N>(f): f(std::integral_constant<int, 0>()) ... f(<N-1>) -- loop bodies whose
+// array indices are constants from the front end on, so small per-lane arrays stay in
+// registers (a #pragma unroll loop index only becomes constant after unrolling,
+// which can be too late for the arrays it indexes to leave scratch).
+template <class F, int... I> MP_HD void static_for_seq(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>()), ...);
+}
+template <int N, class F> MP_HD void static_for(F &&f) {
+    static_for_seq(static_cast<F &&>(f), std::make_integer_sequence<int, N>());
+}
+
 MP_HD int max_models(int v) { return v == kCal ? kMaxModelsCal : (v == kSF ? kMaxModelsSF : kMaxModelsTF); }
 
 } // namespace mp

@@ -1,0 +1,502 @@
+// 5-point relative pose roots with one 16-lane group per sample (4 samples per
+// 64-lane workgroup) -- the root stage of the calibrated point solver
+// (PoseLib relpose_5pt as called at src/hybrid_pose_estimator.cpp:134).
+//
+// The one-lane-per-sample formulation (mp_pt.h fivept_system + sturm_real_roots)
+// needs the 10x20 elimination template (200 doubles) and the 11-polynomial Sturm
+// chain (121 doubles) live in one lane: far past the 512 registers of a lane, so
+// the compiler keeps them in scratch and the kernel is bound by scratch latency.
+// Here the same arithmetic is spread over the lanes of a group:
+//   * template rows: lane r builds row r of the template (row 0 = det E, rows
+//     1 + 3a + b = (2 E E^T E - tr(E E^T) E)_ab), 20 doubles per lane;
+//   * Gauss-Jordan with partial pivoting: the pivot lane is found by a group
+//     argmax (ties -> lowest lane), its row is broadcast through LDS and every
+//     other lane eliminates its own row (rows are tracked, not swapped);
+//   * det B(z) (degree 10) from the six reduced rows, redundantly in every lane;
+//   * Sturm chain coefficient-parallel (lane j owns coefficient j of every chain
+//     polynomial; the chain is kept in LDS), the sign-change counts at the 33 grid
+//     points of sturm_real_roots split over the lanes, the grid cells isolated
+//     lane-parallel, one lane per isolated root for the Newton refinement and the
+//     essential matrix of the root.
+// The operations per value are those of the one-lane code (same pivots, same
+// chain, same grid and bisection), so the roots agree with it bit for bit except on
+// pivot ties (lowest lane here, first row there): the row updates, chain divisions
+// and Horner evaluations are the same expressions.
+#pragma once
+#include "../include/mp_pt.h"
+#include "kernels.h"
+
+namespace mp {
+namespace {
+
+constexpr int kG5 = 16;           // lanes per sample
+constexpr int kS5 = 64 / kG5;     // samples per workgroup
+constexpr int kSturmN = 10;       // degree of det B(z)
+constexpr int kGridCells = 32;    // grid of sturm_real_roots
+
+// Phase timing for tools/pt5_bench.hip (compiled out otherwise): cycles per phase
+// summed over groups.
+#ifdef MP_GROUP5_PROFILE
+__device__ unsigned long long g5_prof[8];
+#define G5_MARK(i)                                                                                                     \
+    do {                                                                                                               \
+        const unsigned long long t_ = wall_clock64();                                                                 \
+        if (r == 0) atomicAdd(&g5_prof[i], t_ - t_prev);                                                               \
+        t_prev = t_;                                                                                                   \
+    } while (0)
+#define G5_START unsigned long long t_prev = wall_clock64()
+#else
+#define G5_MARK(i) ((void)0)
+#define G5_START ((void)0)
+#endif
+
+__device__ inline double gmax(double v) {
+#pragma unroll
+    for (int m = kG5 / 2; m > 0; m >>= 1) v = fmax(v, __shfl_xor(v, m, kG5));
+    return v;
+}
+__device__ inline double gbcast(double v, int src) { return __shfl(v, src, kG5); }
+__device__ inline int gbcast(int v, int src) { return __shfl(v, src, kG5); }
+// exclusive prefix sum over the group; *total = sum over the group
+__device__ inline int gscan(int v, int lane, int *total) {
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < kG5; d <<= 1) {
+        const int y = __shfl_up(x, d, kG5);
+        if (lane >= d) x += y;
+    }
+    *total = __shfl(x, kG5 - 1, kG5);
+    return x - v;
+}
+// Row r of the 10x20 template (Nister's monomial order); rows r >= 10 are zero.
+// N: null-space basis (in LDS: the lane-dependent operands are read by index),
+// E_e = N[0][e] x + N[1][e] y + N[2][e] z + N[3][e].
+__device__ inline void fivept_template_row(const double (*N)[9], int r, double (&row)[20]) {
+    auto lin = [&](auto e) {
+        Lin l;
+        static_for<4>([&](auto q) { l.c[q] = N[q][e]; });
+        return l;
+    };
+    Cub acc;
+    static_for<20>([&](auto c) { acc.c[c] = 0.0; });
+    if (r == 0) {
+        // det(E) = E0 (E4 E8 - E5 E7) - E1 (E3 E8 - E5 E6) + E2 (E3 E7 - E4 E6)
+        auto term = [&](auto i0, auto i1, auto i2, auto i3, auto i4, double sgn) {
+            Quad qa, qb;
+            lin_mul(lin(i1), lin(i2), qa);
+            lin_mul(lin(i3), lin(i4), qb);
+            static_for<10>([&](auto i) { qa.c[i] -= qb.c[i]; });
+            quad_lin_acc(qa, lin(i0), sgn, acc);
+        };
+        term(std::integral_constant<int, 0>(), std::integral_constant<int, 4>(), std::integral_constant<int, 8>(),
+             std::integral_constant<int, 5>(), std::integral_constant<int, 7>(), 1.0);
+        term(std::integral_constant<int, 1>(), std::integral_constant<int, 3>(), std::integral_constant<int, 8>(),
+             std::integral_constant<int, 5>(), std::integral_constant<int, 6>(), -1.0);
+        term(std::integral_constant<int, 2>(), std::integral_constant<int, 3>(), std::integral_constant<int, 7>(),
+             std::integral_constant<int, 4>(), std::integral_constant<int, 6>(), 1.0);
+    } else if (r < 10) {
+        // (2 E E^T E - tr(E E^T) E)_ab = sum_k 2 (E E^T)_ak E_kb - tr E_ab; only row a
+        // of E E^T is formed (the same products, in the same order, as the full one)
+        const int a = (r - 1) / 3, b = (r - 1) - 3 * ((r - 1) / 3);
+        Lin Ea[3], Ek[3], Eab;
+        static_for<4>([&](auto i) {
+            static_for<3>([&](auto m) {
+                Ea[m].c[i] = N[i][3 * a + m];
+                Ek[m].c[i] = N[i][3 * m + b];
+            });
+            Eab.c[i] = N[i][3 * a + b];
+        });
+        Quad tr;
+        {
+            Quad Dg[3];
+            static_for<3>([&](auto d) {
+                static_for<10>([&](auto i) { Dg[d].c[i] = 0.0; });
+                static_for<3>([&](auto m) {
+                    Quad t;
+                    const Lin l = lin(std::integral_constant<int, 3 * d + m>());
+                    lin_mul(l, l, t);
+                    static_for<10>([&](auto i) { Dg[d].c[i] += t.c[i]; });
+                });
+            });
+            static_for<10>([&](auto i) { tr.c[i] = Dg[0].c[i] + Dg[1].c[i] + Dg[2].c[i]; });
+        }
+        static_for<3>([&](auto k) {
+            Quad Q;
+            static_for<10>([&](auto i) { Q.c[i] = 0.0; });
+            static_for<3>([&](auto m) {
+                // operands in the order of (E E^T)_{min(a,k) max(a,k)}: with FMA
+                // contraction lin_mul is not symmetric in its arguments
+                const Lin Lk = lin(std::integral_constant<int, 3 * k + m>());
+                Lin u, v;
+                static_for<4>([&](auto i) {
+                    u.c[i] = k < a ? Lk.c[i] : Ea[m].c[i];
+                    v.c[i] = k < a ? Ea[m].c[i] : Lk.c[i];
+                });
+                Quad t;
+                lin_mul(u, v, t);
+                static_for<10>([&](auto i) { Q.c[i] += t.c[i]; });
+            });
+            quad_lin_acc(Q, Ek[k], 2.0, acc);
+        });
+        quad_lin_acc(tr, Eab, -1.0, acc);
+    }
+    static_for<20>([&](auto c) { row[c] = acc.c[c]; });
+}
+
+// Sturm sign changes at x from the chain in LDS (poly k: ascending, degree N-k)
+__device__ inline int sturm_count_lds(const double (*ch)[kSturmN + 1], int len, double x) {
+    int changes = 0;
+    double prev = 0.0;
+#pragma unroll
+    for (int k = 0; k <= kSturmN; ++k) {
+        if (k < len) {
+            double v = 0.0;
+#pragma unroll
+            for (int j = kSturmN - k; j >= 0; --j) v = v * x + ch[k][j];
+            if (v != 0.0) {
+                if (prev != 0.0 && ((v < 0) != (prev < 0))) ++changes;
+                prev = v;
+            }
+        }
+    }
+    return changes;
+}
+
+// The roots of one cell (x_lo, x_hi] holding clo - chi roots, as in sturm_isolate
+__device__ inline void cell_intervals(const double (*ch)[kSturmN + 1], int len, double lo, double hi, int clo,
+                                      int chi, RootIntervals<kSturmN> &I) {
+    if (clo - chi == 1) {
+        I.push(lo, hi);
+        return;
+    }
+    for (int guard = 0; guard < kSturmN && clo > chi; ++guard) {
+        double a = lo, b = hi;
+        int ca = clo, cb = chi;
+        for (int depth = 0; depth < 100; ++depth) {
+            if (ca - cb == 1 || b - a <= 1e-14 * fmax(1.0, fmax(fabs(a), fabs(b)))) break;
+            const double m = 0.5 * (a + b);
+            const int cm = sturm_count_lds(ch, len, m);
+            if (ca - cm >= 1) {
+                b = m;
+                cb = cm;
+            } else {
+                a = m;
+                ca = cm;
+            }
+        }
+        I.push(a, b);
+        lo = b;
+        clo = cb;
+    }
+}
+
+// B(z) of Nister's hidden-variable step from the reduced template rows 4..9
+// (columns 10..19): rows (e - z f), (g - z h), (i - z j), as in fivept_system
+__device__ inline void hidden_B(const double (*red)[10], double (&Bx)[3][4], double (&By)[3][4], double (&B1)[3][5]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const double *ar = red[2 * q], *br = red[2 * q + 1];
+        auto a = [&](int col) { return ar[col - 10]; };
+        auto b = [&](int col) { return br[col - 10]; };
+        Bx[q][0] = a(12);
+        Bx[q][1] = a(11) - b(12);
+        Bx[q][2] = a(10) - b(11);
+        Bx[q][3] = -b(10);
+        By[q][0] = a(15);
+        By[q][1] = a(14) - b(15);
+        By[q][2] = a(13) - b(14);
+        By[q][3] = -b(13);
+        B1[q][0] = a(19);
+        B1[q][1] = a(18) - b(19);
+        B1[q][2] = a(17) - b(18);
+        B1[q][3] = a(16) - b(17);
+        B1[q][4] = -b(16);
+    }
+}
+
+struct Group5Shared {
+    double piv[kS5][20];                          // broadcast pivot row
+    double red[kS5][6][10];                       // reduced rows 4..9, columns 10..19
+    double chain[kS5][kSturmN + 1][kSturmN + 1];  // Sturm chain
+    int cnt[kS5][kGridCells + 1];                 // sign-change counts at the grid points
+    double lo[kS5][kSturmN], hi[kS5][kSturmN];    // isolating intervals (scaled variable)
+    double N[kS5][4][9];                          // null-space basis
+};
+
+// cand: 9 doubles per root (E, ascending roots), ncand: number of E written
+__global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                             const int *samples, double *cand, int *ncand,
+                                                             int cand_stride) {
+    __shared__ Group5Shared sh;
+    const int g = threadIdx.x / kG5, r = threadIdx.x % kG5;
+    const int idx = blockIdx.x * kS5 + g;
+    const bool active = idx < nlist;
+    const int *s = samples + (size_t)list[active ? idx : nlist - 1] * kSampleStride;
+    G5_START;
+
+    // ---- null space of the epipolar constraints (every lane) ----
+    double b1[5][3], b2[5][3];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const int i = s[j];
+        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+        double a[3], c[3];
+        matvec3(C.K0i, xa, a);
+        matvec3(C.K1i, xb, c);
+        const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            b1[j][q] = a[q] * na;
+            b2[j][q] = c[q] * nc;
+        }
+    }
+    double row[20];
+    {
+        double N[4][9];
+        double Q[5][9];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) Q[i][3 * rr + cc] = b2[i][rr] * b1[i][cc];
+        nullspace_5x9(Q, N);
+        static_for<36>([&](auto q) {
+            if (q % kG5 == r) sh.N[g][q / 9][q % 9] = N[q / 9][q % 9];
+        });
+    }
+    __syncthreads();
+    G5_MARK(0);
+    // ---- template row of this lane ----
+    fivept_template_row(sh.N[g], r, row);
+    G5_MARK(1);
+    // ---- Gauss-Jordan over the group ----
+    bool used = r >= 10, ok = true;
+    int logical = -1;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        double bv = used ? -1.0 : fabs(row[k]);
+        int bi = r;
+#pragma unroll
+        for (int m = kG5 / 2; m > 0; m >>= 1) {
+            const double ov = __shfl_xor(bv, m, kG5);
+            const int oi = __shfl_xor(bi, m, kG5);
+            if (ov > bv || (ov == bv && oi < bi)) {
+                bv = ov;
+                bi = oi;
+            }
+        }
+        ok = ok && (bv > 0.0);
+        const bool piv_lane = r == bi;
+        if (piv_lane) {
+#pragma unroll
+            for (int c = 0; c < 20; ++c) sh.piv[g][c] = row[c];
+        }
+        __syncthreads();
+        const double inv = 1.0 / sh.piv[g][k];
+        if (piv_lane) {
+#pragma unroll
+            for (int c = 0; c < 20; ++c) row[c] *= inv;
+            used = true;
+            logical = k;
+        } else {
+            const double f = row[k];
+#pragma unroll
+            for (int c = 0; c < 20; ++c) row[c] -= f * (sh.piv[g][c] * inv);
+        }
+        __syncthreads();
+    }
+    if (logical >= 4) {
+#pragma unroll
+        for (int c = 0; c < 10; ++c) sh.red[g][logical - 4][c] = row[10 + c];
+    }
+    __syncthreads();
+
+    G5_MARK(2);
+    // ---- det B(z) (every lane) ----
+    double d10[11];
+    {
+        double Bx[3][4], By[3][4], B1[3][5];
+        hidden_B(sh.red[g], Bx, By, B1);
+        double t7a[8], t7b[8], t6a[7], t6b[7], t10[11];
+#pragma unroll
+        for (int i = 0; i < 11; ++i) d10[i] = 0.0;
+        pmul<3, 4>(By[1], B1[2], t7a);
+        pmul<3, 4>(By[2], B1[1], t7b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t7a[i] -= t7b[i];
+        pmul<3, 7>(Bx[0], t7a, t10);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) d10[i] += t10[i];
+        pmul<3, 4>(Bx[1], B1[2], t7a);
+        pmul<3, 4>(Bx[2], B1[1], t7b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t7a[i] -= t7b[i];
+        pmul<3, 7>(By[0], t7a, t10);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) d10[i] -= t10[i];
+        pmul<3, 3>(Bx[1], By[2], t6a);
+        pmul<3, 3>(By[1], Bx[2], t6b);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) t6a[i] -= t6b[i];
+        pmul<4, 6>(B1[0], t6a, t10);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) d10[i] += t10[i];
+    }
+
+    G5_MARK(3);
+    // ---- sturm_real_roots<10> over the group ----
+    constexpr int NN = kSturmN;
+    double mx = 0.0;
+#pragma unroll
+    for (int j = 0; j <= NN; ++j) mx = fmax(mx, fabs(d10[j]));
+    ok = ok && (mx > 0.0) && (fabs(d10[NN]) > 1e-300);
+    double c[NN + 1];
+    const double lead = 1.0 / d10[NN];
+#pragma unroll
+    for (int j = 0; j <= NN; ++j) c[j] = d10[j] * lead; // monic
+    // sigma = max_j |c_j|^(1/(N-j)): lane j takes coefficient j
+    double sigma;
+    {
+        double cj = 0.0;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) cj = (r == j) ? c[j] : cj;
+        const double pj = (r < NN && cj != 0.0) ? pow(fabs(cj), 1.0 / (NN - r)) : 0.0;
+        sigma = gmax(pj);
+        if (!(sigma > 0.0) || !(sigma < 1e300)) sigma = 1.0;
+    }
+    // this lane's coefficient of the scaled monic polynomial (lane j: cs[j])
+    double cs_j;
+    {
+        const double inv = 1.0 / sigma;
+        double p = 1.0, v = (r == NN) ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = NN - 1; j >= 0; --j) {
+            p *= inv;
+            v = (r == j) ? c[j] * p : v;
+        }
+        cs_j = v;
+    }
+    // chain, coefficient-parallel: lane j holds coefficient j of s[k-1] (a) and s[k] (b)
+    int len;
+    {
+        const double m0 = gmax(fabs(cs_j));
+        const double sc0 = m0 > 0 ? 1.0 / m0 : 1.0;
+        double a = cs_j * sc0; // s[0]
+        const double up = __shfl(a, (r + 1) & (kG5 - 1), kG5);
+        double b = (r < NN) ? (r + 1) * up : 0.0; // derivative
+        const double m1 = gmax(fabs(b));
+        if (r < NN) b /= m1;
+        if (r <= NN) {
+            sh.chain[g][0][r] = a;
+            sh.chain[g][1][r] = b;
+        }
+        len = 2;
+        bool alive = true;
+#pragma unroll
+        for (int k = 1; k < NN; ++k) {
+            const int d = NN - k;
+            const double bd = gbcast(b, d);
+            const double bmax = gmax((r <= d) ? fabs(b) : 0.0);
+            if (!(fabs(bd) > 1e-14 * bmax)) alive = false;
+            const double ad1 = gbcast(a, d + 1), ad = gbcast(a, d), bdm1 = gbcast(b, d - 1);
+            const double q1 = ad1 / bd;
+            const double q0 = (ad - q1 * bdm1) / bd;
+            // (the shuffle runs on every lane: a shuffle inside the conditional would
+            // read lane 0 while lane 0 is masked off)
+            const double b_left = __shfl(b, (r + kG5 - 1) & (kG5 - 1), kG5);
+            const double bm1 = r > 0 ? b_left : 0.0;
+            const double nxt = (r < d) ? -(a - q1 * bm1 - q0 * b) : 0.0;
+            const double rmax = gmax(fabs(nxt));
+            const double amax = gmax((r <= d + 1) ? fabs(a) : 0.0);
+            if (alive && !(rmax > 1e-15 * amax)) alive = false;
+            if (alive) {
+                const double s_next = (r < d) ? nxt / rmax : 0.0;
+                if (r <= NN) sh.chain[g][k + 1][r] = s_next;
+                len = k + 2;
+                a = b;
+                b = s_next;
+            }
+        }
+    }
+    __syncthreads();
+    const double(*ch)[NN + 1] = sh.chain[g];
+    G5_MARK(4);
+
+    // ---- counts at the grid points x_i = -B + i h (i = 0..32), lanes i and i + 16 ----
+    const double Bnd = 3.0, h = 2.0 * Bnd / kGridCells;
+    {
+        const double xa = -Bnd + r * h, xb = -Bnd + (r + kG5) * h;
+        sh.cnt[g][r] = sturm_count_lds(ch, len, xa);
+        sh.cnt[g][r + kG5] = sturm_count_lds(ch, len, xb);
+        if (r == 0) sh.cnt[g][kGridCells] = sturm_count_lds(ch, len, Bnd);
+    }
+    __syncthreads();
+
+    G5_MARK(5);
+    // ---- cells r and r + 16 isolated by this lane; intervals gathered in cell order ----
+    int nint = 0;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        const int cell = r + pass * kG5;
+        const double x_lo = -Bnd + cell * h, x_hi = (cell + 1 == kGridCells) ? Bnd : -Bnd + (cell + 1) * h;
+        const int v_lo = sh.cnt[g][cell], v_hi = sh.cnt[g][cell + 1];
+        RootIntervals<NN> I;
+        if (ok && v_lo > v_hi) cell_intervals(ch, len, x_lo, x_hi, v_lo, v_hi, I);
+        int total;
+        const int off = gscan(I.n, r, &total);
+#pragma unroll
+        for (int q = 0; q < NN; ++q)
+            if (q < I.n && nint + off + q < NN) {
+                sh.lo[g][nint + off + q] = I.lo[q];
+                sh.hi[g][nint + off + q] = I.hi[q];
+            }
+        nint = min(nint + total, NN);
+    }
+    __syncthreads();
+
+    G5_MARK(6);
+    // ---- one lane per root: refinement and the essential matrix ----
+    bool have = false;
+    double Ee[9];
+    if (ok && r < nint) {
+        const double z = refine_root<NN>(c, sigma * sh.lo[g][r], sigma * sh.hi[g][r]);
+        double Bx[3][4], By[3][4], B1[3][5];
+        hidden_B(sh.red[g], Bx, By, B1);
+        double Bm[3][3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            Bm[q][0] = peval<3>(Bx[q], z);
+            Bm[q][1] = peval<3>(By[q], z);
+            Bm[q][2] = peval<4>(B1[q], z);
+        }
+        double v01[3], v02[3], v12[3];
+        cross3(Bm[0], Bm[1], v01);
+        cross3(Bm[0], Bm[2], v02);
+        cross3(Bm[1], Bm[2], v12);
+        const double n01 = dot3(v01, v01), n02 = dot3(v02, v02), n12 = dot3(v12, v12);
+        double v[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[q] = (n01 >= n02 && n01 >= n12) ? v01[q] : (n02 >= n12 ? v02[q] : v12[q]);
+        if (v[2] != 0.0) {
+            const double x = v[0] / v[2], y = v[1] / v[2];
+#pragma unroll
+            for (int e = 0; e < 9; ++e) Ee[e] = x * sh.N[g][0][e] + y * sh.N[g][1][e] + z * sh.N[g][2][e] + sh.N[g][3][e];
+            have = true;
+        }
+    }
+    G5_MARK(7);
+    int nE;
+    const int pos = gscan(have ? 1 : 0, r, &nE);
+    if (active) {
+        double *out = cand + (size_t)idx * cand_stride;
+        if (have) {
+#pragma unroll
+            for (int e = 0; e < 9; ++e) out[9 * pos + e] = Ee[e];
+        }
+        if (r == 0) ncand[idx] = ok ? nE : 0;
+    }
+}
+
+} // namespace
+} // namespace mp

@@ -36,8 +36,14 @@ hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, co
                         double *score);
 // the same sweep writing errors + score (out[3n]) to host-mapped memory and raising
 // *flag = seq (system scope) when done; the host polls the flag
+// calibrated 5-point root stage alone (impl 0: lane per sample, 1: 16-lane groups);
+// cand: kPtCandStride doubles per sample (9 per essential matrix), ncand: count
+hipError_t launch_pt5_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                            const int *samples, double *cand, int *ncand, int impl);
+// part: sweep_blocks(n) doubles, cnt: one zero-initialised counter (device memory)
+int sweep_blocks(int64_t n);
 hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
-                            int *flag, int seq);
+                            int *flag, int seq, double *part, unsigned *cnt);
 // scores of many explicit models (one workgroup per model) -- used by mp_score_models
 hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
                                double *scores);

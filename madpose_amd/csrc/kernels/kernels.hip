@@ -11,9 +11,11 @@
 //                 the workgroup also performs GetBestEstimatedModelId's argmin.
 //  sweep<V>       one model, all points: errors for GetInliers + gated score
 #include <cfloat>
+#include <cstdlib>
 
 #include "../include/mp_md_alt.h"
 #include "../include/mp_score.h"
+#include "group_5pt.h"
 #include "kernels.h"
 
 namespace mp {
@@ -460,12 +462,18 @@ __global__ void __launch_bounds__(1024) sweep_kernel(PairData D, PairConst C, co
 // LO sweep straight into pinned host memory: errors (3 x n) and the gated score are
 // written to host-visible memory, then a completion flag is raised with system
 // scope, so the host polls one word instead of issuing a copy and a stream sync.
+// One correspondence per lane over ceil(n / kSweepBlock) workgroups (the sweep is
+// latency-bound: one evaluation deep instead of n / 1024); each workgroup leaves its
+// partial score in part[], and the last one to arrive (system-scope acq_rel counter)
+// sums them in workgroup order -- deterministic -- publishes the score and raises the
+// flag.
+constexpr int kSweepBlock = 256;
 template <int V>
-__global__ void __launch_bounds__(1024) sweep_host_kernel(PairData D, PairConst C, ScoreRec r, double *out,
-                                                          int *flag, int seq) {
+__global__ void __launch_bounds__(kSweepBlock) sweep_host_kernel(PairData D, PairConst C, ScoreRec r, double *out,
+                                                                 int *flag, int seq, double *part, unsigned *cnt) {
     double acc = 0.0;
     const bool gate_md = C.score_type == 1, gate_epi = C.score_type == 2;
-    for (int i = threadIdx.x; i < C.n; i += blockDim.x) {
+    for (int i = blockIdx.x * kSweepBlock + threadIdx.x; i < C.n; i += gridDim.x * kSweepBlock) {
         const Corr p = load_corr(D, i, V == kCal);
         double e0, e1, e2;
         eval_corr<V>(C, r, p, false, e0, e1, e2);
@@ -475,17 +483,28 @@ __global__ void __launch_bounds__(1024) sweep_host_kernel(PairData D, PairConst 
         acc += gate_md ? C.thr[0] * C.w[0] + C.thr[1] * C.w[1] : msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]);
         acc += gate_epi ? C.thr[2] * C.w[2] : msac(e2, C.thr[2], C.w[2]);
     }
-    __shared__ double part[16];
+    __shared__ double wpart[kSweepBlock / 64];
+    __shared__ bool last;
     const double v = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
-    __threadfence_system();
+    if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = v;
+    __threadfence_system(); // this workgroup's error rows reach host memory
     __syncthreads();
     if (threadIdx.x == 0) {
         double sc = 0.0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) sc += part[w];
-        out[3 * C.n] = sc;
-        __threadfence_system();
-        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int w = 0; w < kSweepBlock / 64; ++w) sc += wpart[w];
+        part[blockIdx.x] = sc;
+        const unsigned arrived =
+            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = arrived == gridDim.x - 1;
+        if (last) {
+            double tot = 0.0;
+            for (unsigned b = 0; b < gridDim.x; ++b)
+                tot += __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            out[3 * C.n] = tot;
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // ready for the next launch
+            __threadfence_system();
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -724,7 +743,14 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
     const int grid = (nlist + 63) / 64;
     return by_variant(C.variant, [&](auto V) {
         constexpr int v = decltype(V)::value;
-        pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
+        // calibrated: one 16-lane group per sample (group_5pt.h); MADPOSE_PT5_LANE=1
+        // selects the one-lane-per-sample kernel (A/B measurements)
+        static const bool lane5 = std::getenv("MADPOSE_PT5_LANE") != nullptr;
+        if (v == kCal && !lane5)
+            pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
+                                                                          kCandStride);
+        else
+            pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
         const long lanes = (long)nlist * PtTraits<v>::kRoots;
         pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                   W.slots, W.valid);
@@ -747,10 +773,24 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
     return hipGetLastError();
 }
 
+hipError_t launch_pt5_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                            const int *samples, double *cand, int *ncand, int impl) {
+    if (nlist <= 0) return hipSuccess;
+    if (impl == 1)
+        pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand,
+                                                                      kCandStride);
+    else
+        pt_roots_kernel<kCal><<<(nlist + 63) / 64, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
+    return hipGetLastError();
+}
+
+int sweep_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kSweepBlock - 1) / kSweepBlock); }
+
 hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
-                            int *flag, int seq) {
+                            int *flag, int seq, double *part, unsigned *cnt) {
     return by_variant(C.variant, [&](auto V) {
-        sweep_host_kernel<decltype(V)::value><<<1, 1024, 0, s>>>(D, C, rec, out, flag, seq);
+        sweep_host_kernel<decltype(V)::value><<<sweep_blocks(C.n), kSweepBlock, 0, s>>>(D, C, rec, out, flag, seq, part,
+                                                                                        cnt);
         return hipGetLastError();
     });
 }

@@ -265,3 +265,66 @@ def test_too_few_points_returns_default_model():
                                                      [0, 0], np.eye(3), np.eye(3), o, c)
     assert st.num_iterations_total == 0 and st.best_num_inliers == 0
     assert np.all(pose.pose == 0) and pose.scale == 1.0
+
+
+def _pt5_roots(impl, p0, p1):
+    import ctypes
+    ns = p0.shape[0]
+    cand = np.zeros((ns, 96))
+    ncand = np.zeros(ns, dtype=np.int32)
+    dp = lambda a: np.ascontiguousarray(a, dtype=np.float64).ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    L.check(L.lib().mp_debug_pt5_roots(impl, ns, dp(p0), dp(p1), cand.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                       ncand.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), 0))
+    return cand, ncand
+
+
+def _five_point_samples(rng, ns, noise_free):
+    p0 = np.zeros((ns, 5, 2))
+    p1 = np.zeros((ns, 5, 2))
+    Es = []
+    for s in range(ns):
+        R = _rand_rot(rng)
+        t = rng.normal(size=3)
+        t /= np.linalg.norm(t)
+        X = np.c_[rng.uniform(-1, 1, (5, 2)), rng.uniform(2, 6, 5)]
+        Y = X @ R.T + t
+        p0[s] = X[:, :2] / X[:, 2:]
+        p1[s] = Y[:, :2] / Y[:, 2:]
+        if not noise_free:
+            p1[s] += rng.normal(scale=0.05, size=(5, 2))
+        tx = np.array([[0, -t[2], t[1]], [t[2], 0, -t[0]], [-t[1], t[0], 0]])
+        E = tx @ R
+        Es.append(E / np.linalg.norm(E))
+    return p0, p1, Es
+
+
+def test_group_5pt_kernel_matches_lane_kernel():
+    """The 16-lane-group 5-point root kernel (the estimator's default) against the
+    one-lane-per-sample kernel on the same samples: the same number of essential
+    matrices per sample and the same matrices (they perform the same operations per
+    value up to FMA contraction, so only ill-conditioned samples may drift), and on
+    noise-free samples both find the ground-truth essential matrix."""
+    rng = np.random.default_rng(5)
+    p0, p1, Es = _five_point_samples(rng, 2000, noise_free=True)
+    for impl in (0, 1):
+        cand, ncand = _pt5_roots(impl, p0, p1)
+        found = 0
+        for s in range(len(Es)):
+            best = 1.0
+            for k in range(ncand[s]):
+                E = cand[s, 9 * k: 9 * k + 9].reshape(3, 3)
+                E = E / np.linalg.norm(E)
+                best = min(best, np.abs(E - Es[s]).max(), np.abs(E + Es[s]).max())
+            found += best < 1e-6
+        assert found >= 0.995 * len(Es), (impl, found)
+    # noisy samples: compare the two kernels directly
+    p0, p1, _ = _five_point_samples(rng, 4000, noise_free=False)
+    c0, n0 = _pt5_roots(0, p0, p1)
+    c1, n1 = _pt5_roots(1, p0, p1)
+    same = n0 == n1
+    assert same.mean() >= 0.995, same.mean()
+    close = 0
+    for s in np.flatnonzero(same):
+        a, b = c0[s, : 9 * n0[s]], c1[s, : 9 * n0[s]]
+        close += np.abs(a - b).max(initial=0.0) <= 1e-6
+    assert close >= 0.98 * same.sum(), (close, same.sum())
