@@ -30,6 +30,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <condition_variable>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -165,6 +167,127 @@ class Sampler {
 };
 
 // ---------------------------------------------------------------------------
+// Zero-copy LO sweep resources of one issuing thread: errors (3 x n) and the score
+// land in host-coherent pinned memory, completion is a flag raised by the kernel.
+struct SweepSlot {
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int64_t cap = 0;
+    double *h_out = nullptr, *d_out = nullptr;
+    int *h_flag = nullptr, *d_flag = nullptr;
+    int seq = 0;
+    double *d_part = nullptr; // per-workgroup partial scores
+    unsigned *d_cnt = nullptr;
+
+    void release() {
+        if (d_part) hipFree(d_part);
+        if (d_cnt) hipFree(d_cnt);
+        if (h_out) hipHostFree(h_out);
+        if (h_flag) hipHostFree(h_flag);
+        d_part = nullptr;
+        d_cnt = nullptr;
+        h_out = d_out = nullptr;
+        h_flag = d_flag = nullptr;
+        cap = 0;
+    }
+    // stream: the owner's stream (slot 0) or nullptr for a stream of its own
+    void ensure(int64_t nn, hipStream_t borrowed) {
+        if (!stream) {
+            if (borrowed) {
+                stream = borrowed;
+            } else {
+                MP_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+                own_stream = true;
+            }
+        }
+        if (nn <= cap) return;
+        release();
+        MP_HIP(hipMalloc(&d_part, sizeof(double) * sweep_blocks(nn)));
+        MP_HIP(hipMalloc(&d_cnt, sizeof(unsigned)));
+        MP_HIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned), stream));
+        MP_HIP(hipHostMalloc(&h_out, sizeof(double) * (3 * nn + 1), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostMalloc(&h_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostGetDevicePointer((void **)&d_out, h_out, 0));
+        MP_HIP(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
+        *h_flag = seq;
+        MP_HIP(hipStreamSynchronize(stream));
+        cap = nn;
+    }
+};
+
+// Worker threads for the parallel LO steps: run(n, f) calls f(job, lane) for jobs
+// 0..n-1, lane 0 being the calling thread and lanes 1..size-1 the workers.
+class LoWorkers {
+  public:
+    explicit LoWorkers(int lanes) {
+        for (int i = 1; i < lanes; ++i) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~LoWorkers() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int lanes() const { return (int)th_.size() + 1; }
+    void run(int n, const std::function<void(int, int)> &f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            f_ = &f;
+            n_ = n;
+            next_.store(0);
+            active_ = (int)th_.size();
+            err_ = nullptr;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return active_ == 0; });
+        f_ = nullptr;
+        if (err_) std::rethrow_exception(err_);
+    }
+
+  private:
+    void work(int lane) {
+        for (int k; (k = next_.fetch_add(1)) < n_;) {
+            try {
+                (*f_)(k, lane);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(err_mu_);
+                if (!err_) err_ = std::current_exception();
+            }
+        }
+    }
+    void loop(int lane) {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+            }
+            work(lane);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--active_ == 0) done_cv_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, err_mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int, int)> *f_ = nullptr;
+    int n_ = 0, active_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+    std::exception_ptr err_;
+};
+
+constexpr int kLoLanes = 4; // concurrent LO steps (and sweep slots)
+
+// ---------------------------------------------------------------------------
 // Device context: stream + cached buffers (one per device and concurrent caller)
 struct DeviceCtx {
     int device = 0;
@@ -182,12 +305,10 @@ struct DeviceCtx {
     double *d_pt_cand = nullptr;
     int *d_pt_ncand = nullptr, *d_pt_valid = nullptr;
     Model *d_pt_slots = nullptr;
-    // zero-copy LO sweep output (host-coherent pinned memory) and its completion flag
-    double *h_sweep = nullptr, *d_sweep = nullptr;
-    int *h_flag = nullptr, *d_flag = nullptr;
-    int seq = 0;
-    double *d_sweep_part = nullptr; // per-workgroup partial scores of a sweep
-    unsigned *d_sweep_cnt = nullptr;
+    // LO sweep issuers: slot 0 on `stream` (the estimator thread), slots 1.. with
+    // streams of their own (parallel LO steps)
+    SweepSlot sweep_slot[kLoLanes];
+    std::unique_ptr<LoWorkers> lo_workers; // created on first parallel LO
     // pinned host mirrors
     int *h_samples = nullptr, *h_md_list = nullptr, *h_pt_list = nullptr, *h_counts = nullptr, *h_best_slot = nullptr;
     double *h_best = nullptr, *h_err = nullptr, *h_score1 = nullptr;
@@ -204,11 +325,10 @@ struct DeviceCtx {
         for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_md_list, (void *)d_pt_list, (void *)d_counts,
                         (void *)d_best_slot, (void *)d_models, (void *)d_recs, (void *)d_scores, (void *)d_best,
                         (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_ncand,
-                        (void *)d_pt_valid, (void *)d_pt_slots, (void *)d_sweep_part, (void *)d_sweep_cnt})
+                        (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
         for (void *p : {(void *)h_samples, (void *)h_md_list, (void *)h_pt_list, (void *)h_counts, (void *)h_best_slot,
-                        (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1,
-                        (void *)h_sweep, (void *)h_flag})
+                        (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1})
             if (p) hipHostFree(p);
         d_pair = d_err = d_scores = d_best = d_score1 = nullptr;
         d_samples = d_md_list = d_pt_list = d_counts = d_best_slot = nullptr;
@@ -221,10 +341,7 @@ struct DeviceCtx {
         h_best = h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
         h_model1 = nullptr;
-        h_sweep = d_sweep = nullptr;
-        h_flag = d_flag = nullptr;
-        d_sweep_part = nullptr;
-        d_sweep_cnt = nullptr;
+        for (auto &sl : sweep_slot) sl.release();
         cap_n = 0;
         cap_b = cap_m = 0;
     }
@@ -252,9 +369,6 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_pt_valid, sizeof(int) * (size_t)bb * kPtSlotStride));
         MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb * kPtSlotStride));
         MP_HIP(hipMalloc(&d_score1, sizeof(double) * 64));
-        MP_HIP(hipMalloc(&d_sweep_part, sizeof(double) * sweep_blocks(nn)));
-        MP_HIP(hipMalloc(&d_sweep_cnt, sizeof(unsigned)));
-        MP_HIP(hipMemsetAsync(d_sweep_cnt, 0, sizeof(unsigned), stream));
         // two slots each: the next batch is generated while the current one is in flight
         MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 8 * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_md_list, sizeof(int) * 2 * bb, hipHostMallocDefault));
@@ -266,11 +380,7 @@ struct DeviceCtx {
         MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_model1, sizeof(Model) * 64, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_sweep, sizeof(double) * (3 * nn + 1), hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostMalloc(&h_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostGetDevicePointer((void **)&d_sweep, h_sweep, 0));
-        MP_HIP(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
-        *h_flag = seq;
+        sweep_slot[0].ensure(nn, stream);
         cap_n = nn;
         cap_b = bb;
         cap_m = mm;
@@ -488,55 +598,72 @@ class Run {
     PairData D_;
     Stats *S_ = nullptr;
     IterationStream rs_; // sampler + selection/LO streams
-    // single-model sweep cache
-    Model cache_model_;
-    bool cache_valid_ = false;
-    double cache_score_ = 0.0;
-    std::vector<double> err_;
     double sample_s_ = 0.0;
 
     // --- GPU sweeps ---
-    const double *sweep(const Model &m, double *score) {
-        if (cache_valid_ && std::memcmp(&m, &cache_model_, sizeof(Model)) == 0) {
-            *score = cache_score_;
-            return err_.data();
+    // One issuer of single-model sweeps (the estimator thread, or an LO worker during
+    // parallel LO steps) with the cache of its last result; `sel` is the
+    // selection/LO random stream the issuer draws from.
+    struct Lane {
+        SweepSlot *slot = nullptr;
+        Mt19937 *sel = nullptr;
+        Model model;
+        bool valid = false;
+        double score = 0.0;
+        std::vector<double> err;
+        uint64_t count = 0;
+        double t[3] = {0, 0, 0}; // launch / wait / copy seconds (MADPOSE_SWEEP_TIMING)
+    };
+    Lane lanes_[kLoLanes]; // lanes_[0]: the estimator thread
+    bool lo_parallel_ = true;
+
+    const double *sweep(Lane &L, const Model &m, double *score) {
+        if (L.valid && std::memcmp(&m, &L.model, sizeof(Model)) == 0) {
+            *score = L.score;
+            return L.err.data();
         }
         auto t_sw = Clock::now();
         ScoreRec rec;
         prepare_score_rec(P_.C, m, rec);
-        const int seq = ++X_.seq;
-        MP_HIP(launch_sweep_host(X_.stream, D_, P_.C, rec, X_.d_sweep, X_.d_flag, seq, X_.d_sweep_part, X_.d_sweep_cnt));
+        SweepSlot &sl = *L.slot;
+        const int seq = ++sl.seq;
+        MP_HIP(launch_sweep_host(sl.stream, D_, P_.C, rec, sl.d_out, sl.d_flag, seq, sl.d_part, sl.d_cnt));
+        const double t_launched = secs(t_sw);
         // poll the completion flag; after 2 s fall back to a stream sync, which also
         // surfaces any kernel error
-        for (uint64_t spin = 0; __atomic_load_n(X_.h_flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
+        for (uint64_t spin = 0; __atomic_load_n(sl.h_flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
             if ((spin & 1023) == 1023 && secs(t_sw) > 2.0) {
-                MP_HIP(hipStreamSynchronize(X_.stream));
-                if (__atomic_load_n(X_.h_flag, __ATOMIC_ACQUIRE) != seq)
+                MP_HIP(hipStreamSynchronize(sl.stream));
+                if (__atomic_load_n(sl.h_flag, __ATOMIC_ACQUIRE) != seq)
                     throw std::runtime_error("LO sweep did not signal completion");
             }
         }
-        err_.assign(X_.h_sweep, X_.h_sweep + 3 * n_);
-        cache_model_ = m;
-        cache_score_ = X_.h_sweep[3 * n_];
-        cache_valid_ = true;
-        S_->num_lo_sweeps++;
+        const double t_done = secs(t_sw);
+        L.err.assign(sl.h_out, sl.h_out + 3 * n_);
+        L.t[0] += t_launched;
+        L.t[1] += t_done - t_launched;
+        L.t[2] += secs(t_sw) - t_done;
+        L.model = m;
+        L.score = sl.h_out[3 * n_];
+        L.valid = true;
+        L.count++;
         if (g_prof_on.load(std::memory_order_relaxed)) {
             const double dt = secs(t_sw);
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.sweeps += 1;
             g_prof.sweep_wall_ms += 1e3 * dt;
         }
-        *score = cache_score_;
-        return err_.data();
+        *score = L.score;
+        return L.err.data();
     }
-    double score(const Model &m) {
+    double score(Lane &L, const Model &m) {
         double s;
-        sweep(m, &s);
+        sweep(L, m, &s);
         return s;
     }
-    int inliers(const Model &m, const double *thr, std::vector<int> out[3]) {
+    int inliers(Lane &L, const Model &m, const double *thr, std::vector<int> out[3]) {
         double s;
-        const double *e = sweep(m, &s);
+        const double *e = sweep(L, m, &s);
         int c = 0;
         for (int t = 0; t < 3; ++t) {
             out[t].clear();
@@ -571,7 +698,7 @@ class Run {
 
     // UpdateRANSACTerminationCriteria (src/hybrid_ransac.h:351-378)
     void termination(const Model &m, uint32_t *max_per) {
-        S_->best_num_inliers = inliers(m, thr_, S_->inlier_indices);
+        S_->best_num_inliers = inliers(lanes_[0], m, thr_, S_->inlier_indices);
         for (int t = 0; t < 3; ++t)
             S_->inlier_ratios[t] = n_ > 0 ? (double)S_->inlier_indices[t].size() / (double)n_ : 0.0;
         for (int s = 0; s < 2; ++s) max_per[s] = num_required(s);
@@ -621,16 +748,22 @@ class Run {
             out[t].push_back(idx);
         }
     }
-    void shuffle_resize(int k, std::vector<int> *v) {
+    static void shuffle_resize(Mt19937 &sel, int k, std::vector<int> *v) {
         const int n = (int)v->size();
         if (n <= k) return;
-        for (int i = 0; i < k; ++i) std::swap((*v)[i], (*v)[uniform_int(rs_.sel, i, n - 1)]);
+        for (int i = 0; i < k; ++i) std::swap((*v)[i], (*v)[uniform_int(sel, i, n - 1)]);
         v->resize(k);
     }
+    // draws of one lsq_fit when every data type has enough inliers (the usual case)
+    int lsq_fit_draws(int st) const {
+        int k = 0;
+        for (int t = 0; t < 3; ++t) k += ss_[st][t] * o_.min_sample_multiplicator;
+        return k * o_.min_sample_multiplicator;
+    }
 
-    void lsq_fit(const double *thr, int st, Model *m, bool use_all) {
+    void lsq_fit(Lane &L, const double *thr, int st, Model *m, bool use_all) {
         std::vector<int> inl[3];
-        inliers(*m, thr, inl);
+        inliers(L, *m, thr, inl);
         int k[3];
         for (int t = 0; t < 3; ++t) {
             if ((int)inl[t].size() < ss_[st][t]) return;
@@ -644,55 +777,125 @@ class Run {
         std::vector<int> all;
         for (int t = 0; t < 3; ++t)
             for (int idx : inl[t]) all.push_back(idx + t * n_);
-        shuffle_resize(total, &all);
+        shuffle_resize(*L.sel, total, &all);
         std::vector<int> smp[3];
         split(all, n_, smp);
         least_squares(smp, m, false);
     }
 
+    // The non-minimal sample of an LO step is unusable (NonMinimalSolver returns 0,
+    // or Solve() sees no residuals): the step is skipped without drawing.
+    bool step_skipped(const std::vector<int> &sample_all) const {
+        std::vector<int> smp[3];
+        split(sample_all, n_, smp);
+        const int kmd = variant_ == kCal ? 3 : 4;
+        if (((int)smp[0].size() < kmd && (int)smp[1].size() < kmd) || (int)smp[2].size() < min_sample_size_)
+            return true;
+        const size_t nres = (cfg_.lo_type != 1 ? smp[0].size() + smp[1].size() : 0) +
+                            (cfg_.lo_type != 2 ? smp[2].size() : 0);
+        return nres == 0;
+    }
+    struct StepOut {
+        std::vector<std::pair<double, Model>> updates; // the step's update_best calls, in order
+        Mt19937 sel;                                   // LO stream after the step
+    };
+    // One LO step (the loop body of src/hybrid_ransac.h:435-470) from m_init on the
+    // non-minimal sample `sample_all`, drawing from *L.sel.
+    void lo_step(Lane &L, int st, const std::vector<int> &sample_all, const Model &m_init, const double *thr,
+                 const double *upd, StepOut &out) {
+        out.updates.clear();
+        if (step_skipped(sample_all)) return;
+        Model m = m_init;
+        std::vector<int> smp[3];
+        split(sample_all, n_, smp);
+        least_squares(smp, &m, true);
+        out.updates.emplace_back(score(L, m), m);
+        lsq_fit(L, thr_, st, &m, false);
+        double cur[3] = {thr[0], thr[1], thr[2]};
+        for (int i = 0; i < o_.num_lsq_iterations; ++i) {
+            lsq_fit(L, cur, st, &m, false);
+            out.updates.emplace_back(score(L, m), m);
+            for (int t = 0; t < 3; ++t) cur[t] -= upd[t];
+        }
+    }
+
+    // LocalOptimization (src/hybrid_ransac.h:383-470).  The steps depend on each
+    // other only through the LO random stream, and each step draws a predictable
+    // number of values (lsq_fit_draws per lsq_fit) unless an lsq_fit finds too few
+    // inliers or a draw is rejected.  So the steps run concurrently on kLoLanes
+    // threads from the stream positions they would start at; afterwards every
+    // step's end position is checked against the next step's start, steps after a
+    // mismatch are recomputed in order, and the steps' update_best calls are applied
+    // in step order -- the result is the serial one in every case.
     void local_opt(int st, Model *best_min, double *best_min_score, int *best_st) {
         auto t0 = Clock::now();
+        Lane &L0 = lanes_[0];
         double thr[3], upd[3];
         for (int t = 0; t < 3; ++t) {
             upd[t] = (o_.threshold_multiplier - 1.0) * thr_[t] / (int)(o_.num_lsq_iterations - 1);
             thr[t] = thr_[t] * o_.threshold_multiplier;
         }
         Model m_init = *best_min;
-        lsq_fit(thr, st, &m_init, true);
-        double sc = score(m_init);
+        lsq_fit(L0, thr, st, &m_init, true);
+        double sc = score(L0, m_init);
         update_best(sc, m_init, st, best_min_score, best_min, best_st);
         std::vector<int> base[3];
-        inliers(m_init, thr_, base);
+        inliers(L0, m_init, thr_, base);
         std::vector<int> base_all;
         for (int t = 0; t < 3; ++t)
             for (int idx : base[t]) base_all.push_back(idx + t * n_);
         const int k_nonmin = std::max(non_min_sample_size_,
                                       std::min(min_sample_size_ * o_.non_min_sample_multiplier, (int)base_all.size() / 2));
-        for (int r = 0; r < o_.num_lo_steps; ++r) {
-            std::vector<int> sample_all = base_all; // copied before the shuffle (:439-440)
-            shuffle_resize(k_nonmin, &base_all);
-            Model m = m_init;
-            std::vector<int> smp[3];
-            split(sample_all, n_, smp);
-            {
-                const int kmd = variant_ == kCal ? 3 : 4;
-                if (((int)smp[0].size() < kmd && (int)smp[1].size() < kmd) || (int)smp[2].size() < min_sample_size_)
-                    continue; // NonMinimalSolver returns 0
-                const size_t nres = (cfg_.lo_type != 1 ? smp[0].size() + smp[1].size() : 0) +
-                                    (cfg_.lo_type != 2 ? smp[2].size() : 0);
-                if (nres == 0) continue; // Solve() == false
-                least_squares(smp, &m, true);
+        const int R = o_.num_lo_steps;
+        if (R > 0) {
+            // step 0 solves on base_all as it is and then shuffles it down to
+            // k_nonmin; later steps shuffle nothing (it is that size already) and all
+            // solve on the shuffled sample (:439-440)
+            const std::vector<int> sample0 = base_all;
+            shuffle_resize(rs_.sel, k_nonmin, &base_all);
+            const std::vector<int> &sample1 = base_all;
+            std::vector<StepOut> outs(R);
+            int first_serial = 0; // steps [first_serial, R) still to run in order
+            Mt19937 sel = rs_.sel;
+            if (lo_parallel_ && R > 1) {
+                std::vector<uint64_t> start(R);
+                uint64_t pos = sel.draws();
+                const uint64_t per_step = (uint64_t)(1 + o_.num_lsq_iterations) * (uint64_t)lsq_fit_draws(st);
+                for (int r = 0; r < R; ++r) {
+                    start[r] = pos;
+                    if (!step_skipped(r == 0 ? sample0 : sample1)) pos += per_step;
+                }
+                const Mt19937 base_sel = sel;
+                X_.lo_workers->run(R, [&](int r, int lane) {
+                    if (lane != 0) MP_HIP(hipSetDevice(X_.device));
+                    Mt19937 my = base_sel;
+                    my.discard(start[r] - base_sel.draws());
+                    Lane &L = lanes_[lane];
+                    L.sel = &my;
+                    lo_step(L, st, r == 0 ? sample0 : sample1, m_init, thr, upd, outs[r]);
+                    L.sel = lane == 0 ? &rs_.sel : nullptr;
+                    outs[r].sel = my;
+                });
+                // steps 0..r are right while each one ended where the next one started
+                first_serial = R;
+                for (int r = 0; r + 1 < R; ++r)
+                    if (outs[r].sel.draws() != start[r + 1]) {
+                        first_serial = r + 1;
+                        break;
+                    }
+                sel = outs[first_serial - 1].sel;
+                if (trace_ && first_serial < R)
+                    std::fprintf(stderr, "[engine] LO step %d started off its predicted draw; recomputing\n",
+                                 first_serial);
             }
-            sc = score(m);
-            update_best(sc, m, st, best_min_score, best_min, best_st);
-            lsq_fit(thr_, st, &m, false);
-            double cur[3] = {thr[0], thr[1], thr[2]};
-            for (int i = 0; i < o_.num_lsq_iterations; ++i) {
-                lsq_fit(cur, st, &m, false);
-                sc = score(m);
-                update_best(sc, m, st, best_min_score, best_min, best_st);
-                for (int t = 0; t < 3; ++t) cur[t] -= upd[t];
+            for (int r = first_serial; r < R; ++r) {
+                L0.sel = &sel;
+                lo_step(L0, st, r == 0 ? sample0 : sample1, m_init, thr, upd, outs[r]);
+                L0.sel = &rs_.sel;
             }
+            rs_.sel = sel;
+            for (int r = 0; r < R; ++r)
+                for (const auto &u : outs[r].updates) update_best(u.first, u.second, st, best_min_score, best_min, best_st);
         }
         S_->seconds_lo += secs(t0);
     }
@@ -755,6 +958,19 @@ void Run::run(Model *best, Stats *S) {
     }
     X_.ensure(n_, max_batch_, maxm_);
     if (!X_.sampler) X_.sampler.reset(new Sampler());
+    lanes_[0].slot = &X_.sweep_slot[0];
+    lanes_[0].sel = &rs_.sel;
+    {
+        const char *e = std::getenv("MADPOSE_LO_PARALLEL");
+        lo_parallel_ = !(e && e[0] == '0') && o_.num_lo_steps > 1;
+    }
+    if (lo_parallel_) {
+        if (!X_.lo_workers) X_.lo_workers.reset(new LoWorkers(kLoLanes));
+        for (int l = 1; l < kLoLanes; ++l) {
+            X_.sweep_slot[l].ensure(X_.cap_n, nullptr);
+            lanes_[l].slot = &X_.sweep_slot[l];
+        }
+    }
     upload_pair(X_, P_, &D_);
     rs_.n = n_;
     rs_.seed(o_.random_seed);
@@ -938,7 +1154,7 @@ void Run::run(Model *best, Stats *S) {
         auto t0 = Clock::now();
         Model refined = *best;
         least_squares(S->inlier_indices, &refined, false);
-        const double sc = score(refined);
+        const double sc = score(lanes_[0], refined);
         if (sc < S->best_model_score) {
             S->best_model_score = sc;
             *best = refined;
@@ -947,6 +1163,15 @@ void Run::run(Model *best, Stats *S) {
         S->seconds_lo += secs(t0);
     }
     S->seconds_total = secs(t_start);
+    double tsum[3] = {0, 0, 0};
+    for (const Lane &L : lanes_) {
+        S->num_lo_sweeps += L.count;
+        for (int k = 0; k < 3; ++k) tsum[k] += L.t[k];
+    }
+    if (std::getenv("MADPOSE_SWEEP_TIMING") && S->num_lo_sweeps > 0)
+        std::fprintf(stderr, "[engine] %llu sweeps: launch %.2f us, wait %.2f us, copy %.2f us (avg)\n",
+                     (unsigned long long)S->num_lo_sweeps, 1e6 * tsum[0] / S->num_lo_sweeps,
+                     1e6 * tsum[1] / S->num_lo_sweeps, 1e6 * tsum[2] / S->num_lo_sweeps);
     if (g_prof_on.load(std::memory_order_relaxed)) {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof.sample_wall_ms += 1e3 * sample_s_;

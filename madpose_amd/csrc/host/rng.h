@@ -21,10 +21,27 @@ class Mt19937 {
         mt_[0] = seed;
         for (int i = 1; i < 624; ++i) mt_[i] = 1812433253u * (mt_[i - 1] ^ (mt_[i - 1] >> 30)) + (uint32_t)i;
         idx_ = 624;
+        draws_ = 0;
     }
     uint32_t operator()() {
         if (idx_ >= 624) twist();
+        ++draws_;
         return out_[idx_++];
+    }
+    // outputs consumed since seeding: two copies of one stream are at the same
+    // position iff their counts agree
+    uint64_t draws() const { return draws_; }
+    void discard(uint64_t k) {
+        for (uint64_t i = 0; i < k; ++i) (*this)();
+    }
+    // the next k outputs without consuming them, or nullptr if they cross a block
+    const uint32_t *window(int k) {
+        if (idx_ >= 624) twist();
+        return idx_ + k <= 624 ? out_ + idx_ : nullptr;
+    }
+    void skip(int k) {
+        idx_ += k;
+        draws_ += (uint64_t)k;
     }
 
   private:
@@ -52,6 +69,7 @@ class Mt19937 {
     uint32_t mt_[624];
     uint32_t out_[624];
     int idx_;
+    uint64_t draws_ = 0;
 };
 
 // uniform integer in [a, b]
@@ -131,7 +149,10 @@ struct IterationStream {
     inline void distinct(int k, int *out) {
         switch (k) {
         case 3: distinct<3>(out); break;
+        case 4: distinct<4>(out); break;
         case 5: distinct<5>(out); break;
+        case 6: distinct<6>(out); break;
+        case 7: distinct<7>(out); break;
         default:
             for (int i = 0; i < k; ++i) {
                 int v;
@@ -144,6 +165,47 @@ struct IterationStream {
                 out[i] = v;
             }
         }
+    }
+    // Fast path of one iteration's sample: the next A + B (MD: two groups) or A
+    // (point: one group) buffered outputs, taken when none of them would be
+    // redrawn -- no Lemire rejection, no duplicate within a group -- which is what
+    // the draw-by-draw code does in that case.  False: nothing consumed.
+    template <int A, int B> inline bool fast_groups(int *idx) {
+        const uint32_t *w = samp.window(A + B);
+        if (!w) return false;
+        int v[A + B];
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < A + B; ++k) {
+            const uint64_t prod = (uint64_t)w[k] * (uint64_t)pick.range;
+            bad |= (uint32_t)prod < pick.threshold;
+            v[k] = (int)(uint32_t)(prod >> 32);
+        }
+#pragma unroll
+        for (int i = 1; i < A; ++i)
+#pragma unroll
+            for (int j = 0; j < i; ++j) bad |= v[i] == v[j];
+#pragma unroll
+        for (int i = A + 1; i < A + B; ++i)
+#pragma unroll
+            for (int j = A; j < i; ++j) bad |= v[i] == v[j];
+        if (bad) return false;
+#pragma unroll
+        for (int k = 0; k < A; ++k) idx[k] = v[k];
+        samp.skip(A + B);
+        return true;
+    }
+    inline bool fast_sample(int st, int *idx) {
+        const int *g = ss[st];
+        if (st == 0 && g[2] == 0) {
+            if (g[0] == 3 && g[1] == 3) return fast_groups<3, 3>(idx);
+            if (g[0] == 4 && g[1] == 4) return fast_groups<4, 4>(idx);
+        } else if (st == 1 && g[0] == 0 && g[1] == 0) {
+            if (g[2] == 5) return fast_groups<5, 0>(idx);
+            if (g[2] == 6) return fast_groups<6, 0>(idx);
+            if (g[2] == 7) return fast_groups<7, 0>(idx);
+        }
+        return false;
     }
     int next(int *idx) {
         const double u = uniform_real(sel, 0.0, prior[0] + prior[1]);
@@ -159,6 +221,7 @@ struct IterationStream {
         }
         if (st < 0) st = prior[1] > 0 ? 1 : 0; // unreachable: u < prior sum
         if (pick.range != (uint32_t)n) pick.set((uint32_t)n);
+        if (fast_sample(st, idx)) return st;
         int tmp[8];
         for (int t = 0; t < 3; ++t) {
             const int k = ss[st][t];

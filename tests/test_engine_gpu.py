@@ -328,3 +328,28 @@ def test_group_5pt_kernel_matches_lane_kernel():
         a, b = c0[s, : 9 * n0[s]], c1[s, : 9 * n0[s]]
         close += np.abs(a - b).max(initial=0.0) <= 1e-6
     assert close >= 0.98 * same.sum(), (close, same.sum())
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_parallel_lo_steps_match_serial(monkeypatch, variant):
+    """LO steps run concurrently from predicted random-stream positions and are
+    validated afterwards; the whole run must equal the serial LO exactly."""
+    kind = ["calibrated", "shared_focal", "two_focal"][variant]
+    p = synthetic.make_pair(30 + variant, n=800)
+    o, c = synthetic.example_options(kind, iterations=1500, min_iterations=1500)
+    o.max_num_iterations_per_solver = 1500
+    cam0, cam1 = (p["K0"], p["K1"]) if variant == 0 else (p["pp0"], p["pp1"])
+    fn = [madpose.HybridEstimatePoseScaleOffset, madpose.HybridEstimatePoseScaleOffsetSharedFocal,
+          madpose.HybridEstimatePoseScaleOffsetTwoFocal][variant]
+    outs = []
+    for par in ["0", "1"]:
+        monkeypatch.setenv("MADPOSE_LO_PARALLEL", par)
+        outs.append(fn(p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], cam0, cam1, o, c))
+    (p0, s0), (p1, s1) = outs
+    assert s0.number_lo_iterations > 0
+    assert np.array_equal(p0.pose, p1.pose)
+    assert s0.inlier_indices == s1.inlier_indices
+    assert s0.num_iterations_total == s1.num_iterations_total
+    assert s0.number_lo_iterations == s1.number_lo_iterations
+    assert s0.num_hypotheses == s1.num_hypotheses
+    assert s0.best_model_score == s1.best_model_score
