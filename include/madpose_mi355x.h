@@ -153,6 +153,13 @@ int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_ou
  * ncand: ns counts.  Test hook. */
 int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int32_t *ncand,
                        int device);
+/* mp_debug_pt_roots: the same for variant 0 (calibrated 5-point, as above) or 1
+ * (shared-focal 6-point: the root stage of PoseLib relpose_6pt_shared_focal as
+ * called at src/hybrid_pose_shared_focal_estimator.cpp:87; pts0/pts1: ns x 6 x 2
+ * normalized points; cand per sample: the 3x9 epipolar null-space basis N, then the
+ * positive roots u = f^2 of the degree-15 focal polynomial, ascending).  Test hook. */
+int mp_debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
+                      int32_t *ncand, int device);
 
 /* Point minimal solvers of the uncalibrated estimators on 2-D points in the
  * estimators' normalized pixel frame ((x - pp) / s, point-major, 2 doubles each),

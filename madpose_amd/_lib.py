@@ -130,6 +130,8 @@ EXPORTS = {
     "mp_relpose_5pt": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int, ctypes.c_int]),
     "mp_debug_pt5_roots": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p,
                                           ctypes.POINTER(ctypes.c_int32), ctypes.c_int]),
+    "mp_debug_pt_roots": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p,
+                                         c_double_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]),
     "mp_relpose_6pt_shared_focal": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int,
                                                    ctypes.c_int]),
     "mp_relpose_7pt_two_focal": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int,

@@ -262,13 +262,18 @@ static int point_direct(int kind, const double *x1, const double *x2, mp_model *
     return r <= -1000 ? -(r + 1000) : -r;
 }
 
-int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int32_t *ncand,
-                       int device) {
+int mp_debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
+                      int32_t *ncand, int device) {
     if (!pts0 || !pts1 || !cand || !ncand) return fail(MP_EINVAL, "null pointer");
     return guarded([&] {
-        mp::debug_pt5_roots(impl, ns, pts0, pts1, cand, ncand, device);
+        mp::debug_pt_roots(variant, impl, ns, pts0, pts1, cand, ncand, device);
         return MP_OK;
     });
+}
+
+int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int32_t *ncand,
+                       int device) {
+    return mp_debug_pt_roots(0, impl, ns, pts0, pts1, cand, ncand, device);
 }
 
 int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device) {

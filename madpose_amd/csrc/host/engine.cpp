@@ -1316,14 +1316,16 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
     return hn;
 }
 
-void debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int *ncand,
-                     int device) {
+void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
+                    int *ncand, int device) {
     if (impl < 0 || impl > 1) throw std::invalid_argument("impl must be 0 (lane) or 1 (group)");
+    if (variant != kCal && variant != kSF) throw std::invalid_argument("variant must be 0 (5pt) or 1 (6pt)");
     if (ns <= 0 || ns > (1 << 22)) throw std::invalid_argument("bad number of samples");
     CtxLease lease(device);
     DeviceCtx &X = *lease.c;
-    const int64_t np = 5 * ns;
-    // one correspondence per sample point, identity intrinsics, sample s = points 5s..5s+4
+    const int K = variant == kCal ? 5 : 6;
+    const int64_t np = K * ns;
+    // one correspondence per sample point, identity intrinsics, sample s = points Ks..Ks+K-1
     std::vector<double> host(8 * (size_t)np);
     for (int64_t i = 0; i < np; ++i) {
         host[i] = pts0[2 * i];
@@ -1337,7 +1339,7 @@ void debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts
     std::vector<int> smp(8 * (size_t)ns, 0), list(ns);
     for (int64_t s = 0; s < ns; ++s) {
         list[s] = (int)s;
-        for (int j = 0; j < 5; ++j) smp[8 * s + j] = (int)(5 * s + j);
+        for (int j = 0; j < K; ++j) smp[8 * s + j] = (int)(K * s + j);
     }
     double *d_pair, *d_cand;
     int *d_smp, *d_list, *d_n;
@@ -1353,10 +1355,10 @@ void debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts
     PairData D{d_pair, d_pair + np, d_pair + 2 * np, d_pair + 3 * np, d_pair + 4 * np, d_pair + 5 * np,
                d_pair + 6 * np, d_pair + 7 * np};
     PairConst C{};
-    C.variant = kCal;
+    C.variant = variant;
     C.n = (int)np;
     for (int k = 0; k < 9; ++k) C.K0[k] = C.K1[k] = C.K0i[k] = C.K1i[k] = (k % 4 == 0) ? 1.0 : 0.0;
-    MP_HIP(launch_pt5_roots(X.stream, D, C, d_list, (int)ns, d_smp, d_cand, d_n, impl));
+    MP_HIP(launch_pt_roots(X.stream, D, C, d_list, (int)ns, d_smp, d_cand, d_n, impl));
     MP_HIP(hipMemcpyAsync(cand, d_cand, sizeof(double) * kPtCandStride * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipMemcpyAsync(ncand, d_n, sizeof(int) * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));

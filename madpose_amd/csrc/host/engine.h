@@ -67,10 +67,11 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
 // kind 0: relpose_5pt on unit bearings; 1: shared-focal 6pt; 2: two-focal 7pt +
 // Bougnoux + recoverPose (normalized 2-D points).  Models before the depth fit.
 int solve_point_direct(int kind, const double *x1, const double *x2, Model *poses, int max_poses, int device);
-// root stage of the calibrated 5-point solver over ns samples of 5 normalized image
-// points each (pts*: ns x 5 x 2); E's into cand (ns x 96), counts into ncand
-void debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int *ncand,
-                     int device);
+// root stage of the calibrated 5-point (variant 0) or shared-focal 6-point (variant 1)
+// solver over ns samples of K = 5 / 6 normalized image points each (pts*: ns x K x 2);
+// candidates into cand (ns x 96), counts into ncand
+void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
+                    int *ncand, int device);
 
 // estimate_scale_and_pose (src/solver.cpp:5-33) on the device; X, Y point-major n x 3
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device);

@@ -528,9 +528,11 @@ MP_HD bool null_vector10(double (&A)[10][10], double (&v)[10]) {
     return true;
 }
 
-// The ten equations of the 6-point system: M[a] holds the coefficients of w^a
-// (rows: det F, then the nine trace-constraint entries; columns: monomials of v).
-MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
+// The ten equations of the 6-point system, one row at a time: emit(row, t0, t1, t2)
+// receives the coefficients of w^0, w^1, w^2 of equation `row` (row 0: det F, which
+// has no w terms: t1 = t2 = nullptr; rows 1 + 3r + c: the trace constraint entry
+// (r, c)); columns are the monomials of v.  Rows are emitted in ascending order.
+template <class Emit> MP_HD void sixpt_rows(const double (&N)[3][9], Emit &&emit) {
     Lin2 F[9];
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
@@ -538,9 +540,6 @@ MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
         F[e].c[1] = N[1][e];
         F[e].c[2] = N[2][e];
     }
-    for (int a = 0; a < 3; ++a)
-        for (int r = 0; r < 10; ++r)
-            for (int c = 0; c < 10; ++c) M[a][r][c] = 0.0;
     {
         // det F
         Cub2 det;
@@ -562,7 +561,7 @@ MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) qa.c[i] -= qb.c[i];
         quad2_lin_acc(qa, F[2], 1.0, det);
-        for (int k = 0; k < 10; ++k) M[0][0][k] = det.c[k];
+        emit(0, det.c, (const double *)nullptr, (const double *)nullptr);
     }
     {
         // G = F D F^T = Ga + w Gb (symmetric; 6 entries each)
@@ -583,7 +582,9 @@ MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
             tr1.c[i] = Gb[0][0].c[i] + Gb[1][1].c[i] + Ga[2][2].c[i];
         }
         const Quad2 &tr2 = Gb[2][2];
+#pragma unroll
         for (int r = 0; r < 3; ++r)
+#pragma unroll
             for (int c = 0; c < 3; ++c) {
                 Cub2 T0, T1, T2;
                 for (int k = 0; k < 10; ++k) T0.c[k] = T1.c[k] = T2.c[k] = 0.0;
@@ -596,14 +597,20 @@ MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
                 quad2_lin_acc(tr1, F[3 * r + c], -1.0, T1);
                 quad2_lin_acc(Gb[r][2], F[6 + c], 2.0, T2);
                 quad2_lin_acc(tr2, F[3 * r + c], -1.0, T2);
-                const int row = 1 + 3 * r + c;
-                for (int k = 0; k < 10; ++k) {
-                    M[0][row][k] = T0.c[k];
-                    M[1][row][k] = T1.c[k];
-                    M[2][row][k] = T2.c[k];
-                }
+                emit(1 + 3 * r + c, T0.c, T1.c, T2.c);
             }
     }
+}
+
+// The whole system: M[a] holds the coefficients of w^a.
+MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
+    sixpt_rows(N, [&](int row, const double *t0, const double *t1, const double *t2) {
+        for (int k = 0; k < 10; ++k) {
+            M[0][row][k] = t0[k];
+            M[1][row][k] = t1 ? t1[k] : 0.0;
+            M[2][row][k] = t2 ? t2[k] : 0.0;
+        }
+    });
 }
 
 // Positive real roots u = 1/w of det(u^2 M0 + u M1 + M2) / u^5 (ascending).

@@ -24,15 +24,14 @@
 // and Horner evaluations are the same expressions.
 #pragma once
 #include "../include/mp_pt.h"
-#include "kernels.h"
+#include "group_sturm.h"
 
 namespace mp {
 namespace {
 
-constexpr int kG5 = 16;           // lanes per sample
-constexpr int kS5 = 64 / kG5;     // samples per workgroup
+constexpr int kG5 = kGrp;         // lanes per sample
+constexpr int kS5 = kGrpPerWg;    // samples per workgroup
 constexpr int kSturmN = 10;       // degree of det B(z)
-constexpr int kGridCells = 32;    // grid of sturm_real_roots
 
 // Phase timing for tools/pt5_bench.hip (compiled out otherwise): cycles per phase
 // summed over groups.
@@ -50,24 +49,6 @@ __device__ unsigned long long g5_prof[8];
 #define G5_START ((void)0)
 #endif
 
-__device__ inline double gmax(double v) {
-#pragma unroll
-    for (int m = kG5 / 2; m > 0; m >>= 1) v = fmax(v, __shfl_xor(v, m, kG5));
-    return v;
-}
-__device__ inline double gbcast(double v, int src) { return __shfl(v, src, kG5); }
-__device__ inline int gbcast(int v, int src) { return __shfl(v, src, kG5); }
-// exclusive prefix sum over the group; *total = sum over the group
-__device__ inline int gscan(int v, int lane, int *total) {
-    int x = v;
-#pragma unroll
-    for (int d = 1; d < kG5; d <<= 1) {
-        const int y = __shfl_up(x, d, kG5);
-        if (lane >= d) x += y;
-    }
-    *total = __shfl(x, kG5 - 1, kG5);
-    return x - v;
-}
 // Row r of the 10x20 template (Nister's monomial order); rows r >= 10 are zero.
 // N: null-space basis (in LDS: the lane-dependent operands are read by index),
 // E_e = N[0][e] x + N[1][e] y + N[2][e] z + N[3][e].
@@ -143,53 +124,6 @@ __device__ inline void fivept_template_row(const double (*N)[9], int r, double (
     static_for<20>([&](auto c) { row[c] = acc.c[c]; });
 }
 
-// Sturm sign changes at x from the chain in LDS (poly k: ascending, degree N-k)
-__device__ inline int sturm_count_lds(const double (*ch)[kSturmN + 1], int len, double x) {
-    int changes = 0;
-    double prev = 0.0;
-#pragma unroll
-    for (int k = 0; k <= kSturmN; ++k) {
-        if (k < len) {
-            double v = 0.0;
-#pragma unroll
-            for (int j = kSturmN - k; j >= 0; --j) v = v * x + ch[k][j];
-            if (v != 0.0) {
-                if (prev != 0.0 && ((v < 0) != (prev < 0))) ++changes;
-                prev = v;
-            }
-        }
-    }
-    return changes;
-}
-
-// The roots of one cell (x_lo, x_hi] holding clo - chi roots, as in sturm_isolate
-__device__ inline void cell_intervals(const double (*ch)[kSturmN + 1], int len, double lo, double hi, int clo,
-                                      int chi, RootIntervals<kSturmN> &I) {
-    if (clo - chi == 1) {
-        I.push(lo, hi);
-        return;
-    }
-    for (int guard = 0; guard < kSturmN && clo > chi; ++guard) {
-        double a = lo, b = hi;
-        int ca = clo, cb = chi;
-        for (int depth = 0; depth < 100; ++depth) {
-            if (ca - cb == 1 || b - a <= 1e-14 * fmax(1.0, fmax(fabs(a), fabs(b)))) break;
-            const double m = 0.5 * (a + b);
-            const int cm = sturm_count_lds(ch, len, m);
-            if (ca - cm >= 1) {
-                b = m;
-                cb = cm;
-            } else {
-                a = m;
-                ca = cm;
-            }
-        }
-        I.push(a, b);
-        lo = b;
-        clo = cb;
-    }
-}
-
 // B(z) of Nister's hidden-variable step from the reduced template rows 4..9
 // (columns 10..19): rows (e - z f), (g - z h), (i - z j), as in fivept_system
 __device__ inline void hidden_B(const double (*red)[10], double (&Bx)[3][4], double (&By)[3][4], double (&B1)[3][5]) {
@@ -217,9 +151,7 @@ __device__ inline void hidden_B(const double (*red)[10], double (&Bx)[3][4], dou
 struct Group5Shared {
     double piv[kS5][20];                          // broadcast pivot row
     double red[kS5][6][10];                       // reduced rows 4..9, columns 10..19
-    double chain[kS5][kSturmN + 1][kSturmN + 1];  // Sturm chain
-    int cnt[kS5][kGridCells + 1];                 // sign-change counts at the grid points
-    double lo[kS5][kSturmN], hi[kS5][kSturmN];    // isolating intervals (scaled variable)
+    GroupSturm<kSturmN> st[kS5];                  // root search of det B(z)
     double N[kS5][4][9];                          // null-space basis
 };
 
@@ -345,122 +277,14 @@ __global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairCon
     }
 
     G5_MARK(3);
-    // ---- sturm_real_roots<10> over the group ----
-    constexpr int NN = kSturmN;
-    double mx = 0.0;
-#pragma unroll
-    for (int j = 0; j <= NN; ++j) mx = fmax(mx, fabs(d10[j]));
-    ok = ok && (mx > 0.0) && (fabs(d10[NN]) > 1e-300);
-    double c[NN + 1];
-    const double lead = 1.0 / d10[NN];
-#pragma unroll
-    for (int j = 0; j <= NN; ++j) c[j] = d10[j] * lead; // monic
-    // sigma = max_j |c_j|^(1/(N-j)): lane j takes coefficient j
-    double sigma;
-    {
-        double cj = 0.0;
-#pragma unroll
-        for (int j = 0; j < NN; ++j) cj = (r == j) ? c[j] : cj;
-        const double pj = (r < NN && cj != 0.0) ? pow(fabs(cj), 1.0 / (NN - r)) : 0.0;
-        sigma = gmax(pj);
-        if (!(sigma > 0.0) || !(sigma < 1e300)) sigma = 1.0;
-    }
-    // this lane's coefficient of the scaled monic polynomial (lane j: cs[j])
-    double cs_j;
-    {
-        const double inv = 1.0 / sigma;
-        double p = 1.0, v = (r == NN) ? 1.0 : 0.0;
-#pragma unroll
-        for (int j = NN - 1; j >= 0; --j) {
-            p *= inv;
-            v = (r == j) ? c[j] * p : v;
-        }
-        cs_j = v;
-    }
-    // chain, coefficient-parallel: lane j holds coefficient j of s[k-1] (a) and s[k] (b)
-    int len;
-    {
-        const double m0 = gmax(fabs(cs_j));
-        const double sc0 = m0 > 0 ? 1.0 / m0 : 1.0;
-        double a = cs_j * sc0; // s[0]
-        const double up = __shfl(a, (r + 1) & (kG5 - 1), kG5);
-        double b = (r < NN) ? (r + 1) * up : 0.0; // derivative
-        const double m1 = gmax(fabs(b));
-        if (r < NN) b /= m1;
-        if (r <= NN) {
-            sh.chain[g][0][r] = a;
-            sh.chain[g][1][r] = b;
-        }
-        len = 2;
-        bool alive = true;
-#pragma unroll
-        for (int k = 1; k < NN; ++k) {
-            const int d = NN - k;
-            const double bd = gbcast(b, d);
-            const double bmax = gmax((r <= d) ? fabs(b) : 0.0);
-            if (!(fabs(bd) > 1e-14 * bmax)) alive = false;
-            const double ad1 = gbcast(a, d + 1), ad = gbcast(a, d), bdm1 = gbcast(b, d - 1);
-            const double q1 = ad1 / bd;
-            const double q0 = (ad - q1 * bdm1) / bd;
-            // (the shuffle runs on every lane: a shuffle inside the conditional would
-            // read lane 0 while lane 0 is masked off)
-            const double b_left = __shfl(b, (r + kG5 - 1) & (kG5 - 1), kG5);
-            const double bm1 = r > 0 ? b_left : 0.0;
-            const double nxt = (r < d) ? -(a - q1 * bm1 - q0 * b) : 0.0;
-            const double rmax = gmax(fabs(nxt));
-            const double amax = gmax((r <= d + 1) ? fabs(a) : 0.0);
-            if (alive && !(rmax > 1e-15 * amax)) alive = false;
-            if (alive) {
-                const double s_next = (r < d) ? nxt / rmax : 0.0;
-                if (r <= NN) sh.chain[g][k + 1][r] = s_next;
-                len = k + 2;
-                a = b;
-                b = s_next;
-            }
-        }
-    }
-    __syncthreads();
-    const double(*ch)[NN + 1] = sh.chain[g];
+    // ---- sturm_real_roots<10> over the group, one lane per root ----
+    double z = 0.0;
+    const int nint = group_sturm_roots<kSturmN>(d10, r, sh.st[g], ok, &z);
     G5_MARK(4);
-
-    // ---- counts at the grid points x_i = -B + i h (i = 0..32), lanes i and i + 16 ----
-    const double Bnd = 3.0, h = 2.0 * Bnd / kGridCells;
-    {
-        const double xa = -Bnd + r * h, xb = -Bnd + (r + kG5) * h;
-        sh.cnt[g][r] = sturm_count_lds(ch, len, xa);
-        sh.cnt[g][r + kG5] = sturm_count_lds(ch, len, xb);
-        if (r == 0) sh.cnt[g][kGridCells] = sturm_count_lds(ch, len, Bnd);
-    }
-    __syncthreads();
-
-    G5_MARK(5);
-    // ---- cells r and r + 16 isolated by this lane; intervals gathered in cell order ----
-    int nint = 0;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-        const int cell = r + pass * kG5;
-        const double x_lo = -Bnd + cell * h, x_hi = (cell + 1 == kGridCells) ? Bnd : -Bnd + (cell + 1) * h;
-        const int v_lo = sh.cnt[g][cell], v_hi = sh.cnt[g][cell + 1];
-        RootIntervals<NN> I;
-        if (ok && v_lo > v_hi) cell_intervals(ch, len, x_lo, x_hi, v_lo, v_hi, I);
-        int total;
-        const int off = gscan(I.n, r, &total);
-#pragma unroll
-        for (int q = 0; q < NN; ++q)
-            if (q < I.n && nint + off + q < NN) {
-                sh.lo[g][nint + off + q] = I.lo[q];
-                sh.hi[g][nint + off + q] = I.hi[q];
-            }
-        nint = min(nint + total, NN);
-    }
-    __syncthreads();
-
-    G5_MARK(6);
-    // ---- one lane per root: refinement and the essential matrix ----
+    // ---- the essential matrix of this lane's root ----
     bool have = false;
     double Ee[9];
-    if (ok && r < nint) {
-        const double z = refine_root<NN>(c, sigma * sh.lo[g][r], sigma * sh.hi[g][r]);
+    if (r < nint) {
         double Bx[3][4], By[3][4], B1[3][5];
         hidden_B(sh.red[g], Bx, By, B1);
         double Bm[3][3];
@@ -494,7 +318,7 @@ __global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairCon
 #pragma unroll
             for (int e = 0; e < 9; ++e) out[9 * pos + e] = Ee[e];
         }
-        if (r == 0) ncand[idx] = ok ? nE : 0;
+        if (r == 0) ncand[idx] = nE;
     }
 }
 

@@ -36,10 +36,11 @@ hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, co
                         double *score);
 // the same sweep writing errors + score (out[3n]) to host-mapped memory and raising
 // *flag = seq (system scope) when done; the host polls the flag
-// calibrated 5-point root stage alone (impl 0: lane per sample, 1: 16-lane groups);
-// cand: kPtCandStride doubles per sample (9 per essential matrix), ncand: count
-hipError_t launch_pt5_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                            const int *samples, double *cand, int *ncand, int impl);
+// point-solver root stage alone, C.variant kCal (5pt) or kSF (6pt); impl 0: lane
+// per sample, 1: 16-lane groups.  cand: kPtCandStride doubles per sample (cal: 9 per
+// essential matrix; sf: null-space basis N (27), then the positive roots u)
+hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                           const int *samples, double *cand, int *ncand, int impl);
 // part: sweep_blocks(n) doubles, cnt: one zero-initialised counter (device memory)
 int sweep_blocks(int64_t n);
 hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,

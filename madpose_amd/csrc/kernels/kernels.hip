@@ -16,6 +16,7 @@
 #include "../include/mp_md_alt.h"
 #include "../include/mp_score.h"
 #include "group_5pt.h"
+#include "group_6pt.h"
 #include "kernels.h"
 
 namespace mp {
@@ -743,12 +744,17 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
     const int grid = (nlist + 63) / 64;
     return by_variant(C.variant, [&](auto V) {
         constexpr int v = decltype(V)::value;
-        // calibrated: one 16-lane group per sample (group_5pt.h); MADPOSE_PT5_LANE=1
-        // selects the one-lane-per-sample kernel (A/B measurements)
+        // calibrated / shared focal: one 16-lane group per sample (group_5pt.h,
+        // group_6pt.h); MADPOSE_PT5_LANE=1 / MADPOSE_PT6_LANE=1 select the
+        // one-lane-per-sample kernels (A/B measurements)
         static const bool lane5 = std::getenv("MADPOSE_PT5_LANE") != nullptr;
+        static const bool lane6 = std::getenv("MADPOSE_PT6_LANE") != nullptr;
         if (v == kCal && !lane5)
             pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                           kCandStride);
+        else if (v == kSF && !lane6)
+            pt_roots6_group_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, C, list, nlist, samples,
+                                                                                      W.cand, W.ncand, kCandStride);
         else
             pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
         const long lanes = (long)nlist * PtTraits<v>::kRoots;
@@ -773,14 +779,23 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
     return hipGetLastError();
 }
 
-hipError_t launch_pt5_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                            const int *samples, double *cand, int *ncand, int impl) {
+hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                           const int *samples, double *cand, int *ncand, int impl) {
     if (nlist <= 0) return hipSuccess;
-    if (impl == 1)
-        pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand,
-                                                                      kCandStride);
-    else
-        pt_roots_kernel<kCal><<<(nlist + 63) / 64, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
+    const int ggrid = (nlist + kGrpPerWg - 1) / kGrpPerWg, lgrid = (nlist + 63) / 64;
+    if (C.variant == kCal) {
+        if (impl == 1)
+            pt_roots5_group_kernel<<<ggrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
+        else
+            pt_roots_kernel<kCal><<<lgrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
+    } else if (C.variant == kSF) {
+        if (impl == 1)
+            pt_roots6_group_kernel<<<ggrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
+        else
+            pt_roots_kernel<kSF><<<lgrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
+    } else {
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
