@@ -602,6 +602,74 @@ template <class Emit> MP_HD void sixpt_rows(const double (&N)[3][9], Emit &&emit
     }
 }
 
+// One row of the same system, for a caller that owns a single row (the group root
+// kernel): F(e) returns entry e of F = x N0 + y N1 + N2 as a Lin2.  Only the entries
+// of G that the row uses are formed, each with the operand order of sixpt_rows, and
+// every accumulator receives its terms in the order of sixpt_rows.
+template <class FGet>
+MP_HD void sixpt_row(FGet &&F, int row, double (&t0)[10], double (&t1)[10], double (&t2)[10]) {
+    Cub2 T0, T1, T2;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) T0.c[k] = T1.c[k] = T2.c[k] = 0.0;
+    if (row == 0) {
+        Quad2 qa, qb;
+        auto term = [&](int i0, int i1, int i2, int i3, int i4, double sgn) {
+            lin2_mul(F(i1), F(i2), qa);
+            lin2_mul(F(i3), F(i4), qb);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) qa.c[i] -= qb.c[i];
+            quad2_lin_acc(qa, F(i0), sgn, T0);
+        };
+        term(0, 4, 8, 5, 7, 1.0);
+        term(1, 3, 8, 5, 6, -1.0);
+        term(2, 3, 7, 4, 6, 1.0);
+    } else {
+        const int a = (row - 1) / 3, c = (row - 1) - 3 * ((row - 1) / 3);
+        // G_xy = Ga_xy + w Gb_xy, formed as G_{min max}
+        auto Gpair = [&](int x, int y, Quad2 &ga, Quad2 &gb) {
+            const int lo = x < y ? x : y, hi = x < y ? y : x;
+            Quad2 u0, u1;
+            lin2_mul(F(3 * lo), F(3 * hi), u0);
+            lin2_mul(F(3 * lo + 1), F(3 * hi + 1), u1);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ga.c[i] = u0.c[i] + u1.c[i];
+            lin2_mul(F(3 * lo + 2), F(3 * hi + 2), gb);
+        };
+        Quad2 tr0, tr1, tr2;
+        {
+            Quad2 ga0, gb0, ga1, gb1, ga2;
+            Gpair(0, 0, ga0, gb0);
+            Gpair(1, 1, ga1, gb1);
+            Gpair(2, 2, ga2, tr2);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                tr0.c[i] = ga0.c[i] + ga1.c[i];
+                tr1.c[i] = gb0.c[i] + gb1.c[i] + ga2.c[i];
+            }
+        }
+        const Lin2 Fac = F(3 * a + c);
+        Quad2 ga, gb;
+        Gpair(a, 0, ga, gb);
+        quad2_lin_acc(ga, F(c), 2.0, T0);
+        quad2_lin_acc(gb, F(c), 2.0, T1);
+        Gpair(a, 1, ga, gb);
+        quad2_lin_acc(ga, F(3 + c), 2.0, T0);
+        quad2_lin_acc(gb, F(3 + c), 2.0, T1);
+        quad2_lin_acc(tr0, Fac, -1.0, T0);
+        Gpair(a, 2, ga, gb);
+        quad2_lin_acc(ga, F(6 + c), 2.0, T1);
+        quad2_lin_acc(gb, F(6 + c), 2.0, T2);
+        quad2_lin_acc(tr1, Fac, -1.0, T1);
+        quad2_lin_acc(tr2, Fac, -1.0, T2);
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        t0[k] = T0.c[k];
+        t1[k] = T1.c[k];
+        t2[k] = T2.c[k];
+    }
+}
+
 // The whole system: M[a] holds the coefficients of w^a.
 MP_HD void sixpt_matrices(const double (&N)[3][9], double (&M)[3][10][10]) {
     sixpt_rows(N, [&](int row, const double *t0, const double *t1, const double *t2) {

@@ -207,17 +207,9 @@ __global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairCon
     int logical = -1;
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
-        double bv = used ? -1.0 : fabs(row[k]);
-        int bi = r;
-#pragma unroll
-        for (int m = kG5 / 2; m > 0; m >>= 1) {
-            const double ov = __shfl_xor(bv, m, kG5);
-            const int oi = __shfl_xor(bi, m, kG5);
-            if (ov > bv || (ov == bv && oi < bi)) {
-                bv = ov;
-                bi = oi;
-            }
-        }
+        double bv;
+        int bi;
+        gargmax(used ? -1.0 : fabs(row[k]), r, &bv, &bi);
         ok = ok && (bv > 0.0);
         const bool piv_lane = r == bi;
         if (piv_lane) {
@@ -279,12 +271,12 @@ __global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairCon
     G5_MARK(3);
     // ---- sturm_real_roots<10> over the group, one lane per root ----
     double z = 0.0;
-    const int nint = group_sturm_roots<kSturmN>(d10, r, sh.st[g], ok, &z);
+    const bool has_root = group_sturm_roots<kSturmN>(d10, r, sh.st[g], ok, &z);
     G5_MARK(4);
     // ---- the essential matrix of this lane's root ----
     bool have = false;
     double Ee[9];
-    if (r < nint) {
+    if (has_root) {
         double Bx[3][4], By[3][4], B1[3][5];
         hidden_B(sh.red[g], Bx, By, B1);
         double Bm[3][3];
@@ -311,7 +303,7 @@ __global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairCon
     }
     G5_MARK(7);
     int nE;
-    const int pos = gscan(have ? 1 : 0, r, &nE);
+    const int pos = gscan(have ? 1 : 0, &nE);
     if (active) {
         double *out = cand + (size_t)idx * cand_stride;
         if (have) {

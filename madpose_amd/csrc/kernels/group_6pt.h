@@ -8,7 +8,7 @@
 // complex 10x10 LU of each of the 18 determinant evaluations in one lane: about
 // 500 live doubles, so the compiler spills to scratch and one launch takes
 // milliseconds.  Here:
-//   * lane r < 10 builds and keeps row r of the pencil (sixpt_rows, 30 doubles);
+//   * lane r < 10 builds and keeps row r of the pencil (sixpt_row, 30 doubles);
 //   * each determinant is an LU over the group: lane r eliminates its own complex
 //     row, the pivot is a group argmax (|re| + |im|, ties to the lowest current row
 //     position, which is the lane code's first-maximum rule), the pivot row is
@@ -27,7 +27,24 @@ namespace {
 
 constexpr int kSixDeg = 15; // degree of q(u)
 
+// Phase timing for tools/pt6_bench.hip (compiled out otherwise): clock ticks per
+// phase summed over workgroups (lane 0).
+#ifdef MP_GROUP6_PROFILE
+__device__ unsigned long long g6_prof[8];
+#define G6_MARK(i)                                                                                                     \
+    do {                                                                                                               \
+        const unsigned long long t_ = wall_clock64();                                                                 \
+        if (threadIdx.x == 0) atomicAdd(&g6_prof[i], t_ - t_prev);                                                     \
+        t_prev = t_;                                                                                                   \
+    } while (0)
+#define G6_START unsigned long long t_prev = wall_clock64()
+#else
+#define G6_MARK(i) ((void)0)
+#define G6_START ((void)0)
+#endif
+
 struct Group6Shared {
+    double N[kGrpPerWg][3][9];          // null-space basis of the epipolar constraints
     double piv[kGrpPerWg][20];          // broadcast pivot row (complex, columns k..9)
     double qv[kGrpPerWg][9][2];         // q at the DFT nodes 0..8
     double q[kGrpPerWg][kSixDeg + 1];   // DFT coefficients gathered from the lanes
@@ -48,20 +65,13 @@ __device__ inline Cx group_det_pencil10(const double (&m0)[10], const double (&m
     bool zero = false;
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
-        double bv = (row_lane && pos >= k) ? fabs(A[k].r) + fabs(A[k].i) : -1.0;
-        int bp = row_lane ? pos : 64, bl = r;
-#pragma unroll
-        for (int m = kGrp / 2; m > 0; m >>= 1) {
-            const double ov = __shfl_xor(bv, m, kGrp);
-            const int op = __shfl_xor(bp, m, kGrp), ol = __shfl_xor(bl, m, kGrp);
-            if (ov > bv || (ov == bv && op < bp)) {
-                bv = ov;
-                bp = op;
-                bl = ol;
-            }
-        }
+        const bool cand = row_lane && pos >= k;
+        double bv;
+        int bp;
+        gargmax(cand ? fabs(A[k].r) + fabs(A[k].i) : -1.0, pos, &bv, &bp);
         if (bv == 0.0) zero = true;
-        if (r == bl) {
+        const bool piv_lane = cand && pos == bp;
+        if (piv_lane) {
 #pragma unroll
             for (int c = k; c < 10; ++c) {
                 piv[2 * c] = A[c].r;
@@ -75,7 +85,7 @@ __device__ inline Cx group_det_pencil10(const double (&m0)[10], const double (&m
             det.i = -det.i;
             if (pos == k) pos = bp;
         }
-        if (r == bl) pos = k;
+        if (piv_lane) pos = k;
         det = cmul(det, pk);
         const Cx inv = cdiv({1.0, 0.0}, pk);
         if (row_lane && pos > k) {
@@ -89,7 +99,11 @@ __device__ inline Cx group_det_pencil10(const double (&m0)[10], const double (&m
 }
 
 // cand: N (27 doubles) then the positive roots u (ascending); ncand: their number
-__global__ void __launch_bounds__(64) pt_roots6_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+// waves per SIMD the register allocation targets (tools/pt6_bench.hip A/B)
+#ifndef MP_G6_WAVES
+#define MP_G6_WAVES 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MP_G6_WAVES))) pt_roots6_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                              const int *samples, double *cand, int *ncand,
                                                              int cand_stride) {
     __shared__ Group6Shared sh;
@@ -97,40 +111,42 @@ __global__ void __launch_bounds__(64) pt_roots6_group_kernel(PairData D, PairCon
     const int idx = blockIdx.x * kGrpPerWg + g;
     const bool active = idx < nlist;
     const int *s = samples + (size_t)list[active ? idx : nlist - 1] * kSampleStride;
+    G6_START;
 
-    // ---- null space of the epipolar constraints (every lane) ----
-    double N[3][9];
-    {
-        double b0[6][3], b1[6][3];
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const int i = s[j];
-            const double a[3] = {D.x0u[i], D.x0v[i], 1.0}, c[3] = {D.x1u[i], D.x1v[i], 1.0};
-            const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                b0[j][q] = a[q] * na;
-                b1[j][q] = c[q] * nc;
-            }
-        }
-        double Q[6][9];
-        epipolar_rows<6>(b0, b1, Q);
-        nullspace_kx9<6>(Q, N);
-    }
-    // ---- row r of the pencil ----
+    // ---- null space of the epipolar constraints (every lane), row r of the pencil ----
     double m0[10], m1[10], m2[10];
+    {
+        double N[3][9];
+        {
+            double b0[6][3], b1[6][3];
 #pragma unroll
-    for (int c = 0; c < 10; ++c) m0[c] = m1[c] = m2[c] = 0.0;
-    sixpt_rows(N, [&](int row, const double *t0, const double *t1, const double *t2) {
-        if (row != r) return;
+            for (int j = 0; j < 6; ++j) {
+                const int i = s[j];
+                const double a[3] = {D.x0u[i], D.x0v[i], 1.0}, c[3] = {D.x1u[i], D.x1v[i], 1.0};
+                const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
 #pragma unroll
-        for (int c = 0; c < 10; ++c) {
-            m0[c] = t0[c];
-            m1[c] = t1 ? t1[c] : 0.0;
-            m2[c] = t2 ? t2[c] : 0.0;
+                for (int q = 0; q < 3; ++q) {
+                    b0[j][q] = a[q] * na;
+                    b1[j][q] = c[q] * nc;
+                }
+            }
+            double Q[6][9];
+            epipolar_rows<6>(b0, b1, Q);
+            nullspace_kx9<6>(Q, N);
         }
-    });
-
+#pragma unroll
+        for (int q = 0; q < 27; ++q)
+            if (q % kGrp == r) sh.N[g][q / 9][q % 9] = N[q / 9][q % 9];
+    }
+    __syncthreads();
+    if (r < 10) {
+        const double(*Nl)[9] = sh.N[g];
+        sixpt_row([&](int e) { return Lin2{{Nl[0][e], Nl[1][e], Nl[2][e]}}; }, r, m0, m1, m2);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 10; ++c) m0[c] = m1[c] = m2[c] = 0.0;
+    }
+    G6_MARK(0);
     // ---- q(u) on |u| = 1, then on |u| = rho (pencil_poly15 / sixpt_roots) ----
     double poly[kSixDeg + 1];
     double rho = 1.0;
@@ -151,12 +167,13 @@ __global__ void __launch_bounds__(64) pt_roots6_group_kernel(PairData D, PairCon
             }
         }
         __syncthreads();
+        G6_MARK(1 + 2 * pass);
         // coefficient k = r of this lane
         {
             const int k = r;
             double acc = 0.0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
+#pragma unroll 1
+            for (int j = 0; j < 16; ++j) { // (rolled: one cos/sin in flight keeps registers low)
                 const int jj = (j <= 8) ? j : 16 - j;
                 const Cx q = (j <= 8) ? Cx{sh.qv[g][jj][0], sh.qv[g][jj][1]} : Cx{sh.qv[g][jj][0], -sh.qv[g][jj][1]};
                 const double th = -2.0 * 3.14159265358979323846 * j * k / 16.0;
@@ -174,22 +191,25 @@ __global__ void __launch_bounds__(64) pt_roots6_group_kernel(PairData D, PairCon
                 if (!(rho > 0.0) || !(rho < 1e300)) rho = 1.0;
             }
         }
+        G6_MARK(2 + 2 * pass);
     }
 
     // ---- real roots of q, keep u > 0 ----
     double u = 0.0;
-    const int nr = group_sturm_roots<kSixDeg>(poly, r, sh.st[g], true, &u);
-    const bool keep = r < nr && u > 0.0;
+    const bool has_root = group_sturm_roots<kSixDeg>(poly, r, sh.st[g], true, &u);
+    G6_MARK(5);
+    const bool keep = has_root && u > 0.0;
     int nk;
-    const int at = gscan(keep ? 1 : 0, r, &nk);
+    const int at = gscan(keep ? 1 : 0, &nk);
     if (active) {
         double *out = cand + (size_t)idx * cand_stride;
 #pragma unroll
         for (int q = 0; q < 27; ++q)
-            if (q % kGrp == r) out[q] = N[q / 9][q % 9];
+            if (q % kGrp == r) out[q] = sh.N[g][q / 9][q % 9];
         if (keep) out[27 + at] = u;
         if (r == 0) ncand[idx] = nk;
     }
+    G6_MARK(6);
 }
 
 } // namespace
