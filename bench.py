@@ -6,7 +6,11 @@ calibrated, N = 2000 correspondences, 100k iterations (min = max = per-solver ca
 the adaptive bound never stops early).  Every rank runs its own pairs (weak scaling);
 the only collective is the final gather of per-rank counters.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cal|sf|tf]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cal|sf|tf|scannet]
+
+--workload scannet runs configs[4] instead: a fixed set of 1500 shared-focal pairs
+split over the ranks, many pairs in flight per GPU; value = pairs/s, plus pose
+AUC@5/10/20 over all pairs.
 
 Prints ONE JSON line on rank 0.  `value` = hypotheses scored per second by the whole
 job; `roofline` prices the score_batch kernel at the algorithmic 48*N bytes per
@@ -35,6 +39,11 @@ WORKLOADS = {
                name="configs[2]: shared-focal solver, 2000 synthetic correspondences, 100k hypotheses"),
     "tf": dict(kind="two_focal", variant=2, config=4, n=4000, iterations=200000,
                name="configs[3]: two-focal solver, 4000 synthetic correspondences, 200k hypotheses"),
+    # configs[4]: a fixed set of pairs split over the ranks (strong scaling), many pairs
+    # in flight per GPU (host workers x HIP streams, mp_estimate_batch)
+    "scannet": dict(kind="shared_focal", variant=1, config="scannet", n=2000, iterations=1000, pairs=1500,
+                    name="configs[4]: ScanNet-1500 stand-in, 1500 synthetic shared-focal pairs "
+                         "(N ~ U{1500..2500}), example options (100..1000 iterations), pairs split over the ranks"),
 }
 
 
@@ -171,6 +180,98 @@ def summarize(allv, wl, steps, warmup, world):
     }
 
 
+def pair_errors(results, pairs):
+    """max(rotation error, translation angle error) in degrees per pair
+    (madpose/utils.py:70-78 compute_pose_error), the quantity pose AUC integrates."""
+    from madpose_amd import utils
+
+    return [max(utils.compute_pose_error(p["T_0to1"], m.R(), m.t())) for (m, _), p in zip(results, pairs)]
+
+
+def summarize_scannet(allv, errs, wl, steps, warmup, world, total):
+    """Whole-job record of the ScanNet-1500 stand-in: value = pairs per second of all
+    ranks over the slowest rank's time (total work fixed: strong scaling); AUC@5/10/20
+    over the per-pair errors of every rank."""
+    from madpose_amd import utils
+
+    t_max = float(allv[:, 0].max())
+    done = float(allv[:, 1].sum())
+    e = np.asarray(errs, dtype=np.float64)
+    e = e[np.isfinite(e)]
+    auc = utils.pose_auc(e, (5, 10, 20)) if len(e) else [None] * 3
+    return {
+        "metric": "image-pairs/sec on 1xMI355X (ScanNet-1500 stand-in) + pose AUC@5/10/20",
+        "value": done / t_max,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": t_max / steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded shared-focal pairs per SURVEY.md §8d config 5; no datasets on the box)",
+        "config": {"workload": wl["name"], "pairs": total, "iterations": wl["iterations"],
+                   "parallelism": f"pairs split over {world} rank(s)"},
+        "hypotheses_per_s": float(allv[:, 2].sum()) / t_max,
+        "iterations_per_s": float(allv[:, 3].sum()) / t_max,
+        "pose_auc": {"5": auc[0], "10": auc[1], "20": auc[2], "pairs": int(len(e))},
+        "cpu_baseline": None,
+    }
+
+
+def cpu_baseline_pairs(wl, pairs, budget_s):
+    """The scalar CPU oracle on as many of the rank's pairs as fit in budget_s."""
+    try:
+        import oracle
+        from tests.helpers import oracle_cfg, oracle_opts
+        from madpose_amd import synthetic
+    except Exception as e:
+        return {"value": None, "unit": "pairs/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+    o, c = synthetic.example_options(wl["kind"], iterations=wl["iterations"])
+    t0 = time.perf_counter()
+    k = 0
+    for p in pairs:
+        oracle.estimate(wl["variant"], *_pair_args(p, wl["variant"]), oracle_opts(o), oracle_cfg(c))
+        k += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": k / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"first {k} pairs of the set, single thread, {dt:.1f} s"}
+
+
+def run_scannet(a, wl, world, rank, dev, barrier):
+    import madpose_amd as madpose
+    from madpose_amd import synthetic
+
+    total = a.pairs or wl["pairs"]
+    seeds = list(range(rank, total, world))
+    pairs = [synthetic.scannet_pair(s) for s in seeds]
+    o, c = synthetic.example_options(wl["kind"], iterations=wl["iterations"])
+    for _ in range(a.warmup):
+        madpose.estimate_batch(wl["variant"], pairs[: min(len(pairs), 2 * a.streams)], o, c, device=dev,
+                               num_streams=a.streams)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = madpose.estimate_batch(wl["variant"], pairs, o, c, device=dev, num_streams=a.streams)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    errs = pair_errors(res, pairs)
+    local = [elapsed, float(len(pairs) * a.steps), float(sum(st.num_hypotheses for _, st in res) * a.steps),
+             float(sum(st.num_iterations_total for _, st in res) * a.steps)]
+    allv = gather_counters(local, world)
+    per = (total + world - 1) // world
+    errs_all = gather_counters(errs + [np.nan] * (per - len(errs)), world).reshape(-1)
+    if rank == 0:
+        out = summarize_scannet(allv, errs_all, wl, a.steps, a.warmup, world, total)
+        if world == 1 and a.cpu_budget > 0:
+            out["cpu_baseline"] = cpu_baseline_pairs(wl, pairs, a.cpu_budget)
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -178,6 +279,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cal")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (0 = skip)")
+    ap.add_argument("--pairs", type=int, default=0, help="scannet: total pairs (default 1500)")
+    ap.add_argument("--streams", type=int, default=8, help="scannet: pairs in flight per GPU")
     a = ap.parse_args()
     wl = WORKLOADS[a.workload]
 
@@ -203,6 +306,12 @@ def main():
             dist.barrier()
         if torch.cuda.is_available():
             torch.cuda.synchronize()
+
+    if a.workload == "scannet":
+        run_scannet(a, wl, world, rank, dev, barrier)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # per-rank pairs, generated before timing (weak scaling: one pair per rank per step)
     n_pairs = a.warmup + a.steps

@@ -91,6 +91,14 @@ def config_pair(config, seed=0):
     raise ValueError(config)
 
 
+def scannet_pair(seed, n_range=(1500, 2500)):
+    """configs[4] stand-in (ScanNet-1500): a shared-focal pair
+    with ScanNet intrinsics (f = 577.87, pp = ((W-1)/2, (H-1)/2)) and N ~ U{1500..2500}
+    correspondences; the pair of seed s is the same whatever rank or batch draws it."""
+    n = int(np.random.default_rng([7, seed]).integers(n_range[0], n_range[1] + 1))
+    return make_pair(seed, n=n)
+
+
 def example_options(kind="calibrated", iterations=1000, min_iterations=100):
     """Options of examples/{calibrated,shared_focal,two_focal}.py (reference)."""
     from .api import EstimatorConfig, HybridLORansacOptions

@@ -63,3 +63,19 @@ def test_single_rank_summary_fields():
     rf = res["roofline"]
     assert abs(rf["achieved"] - 3e5 * 2000 * 48 / 0.1 / 1e9) < 1e-6
     assert abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-12
+
+
+def test_scannet_summary_and_gathered_errors():
+    """configs[4] record: pairs/s of all ranks over the slowest rank (strong scaling);
+    AUC over every rank's per-pair errors, padding (NaN) dropped."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from madpose_amd import utils
+
+    allv = np.array([[2.0, 10.0, 500.0, 900.0], [4.0, 9.0, 400.0, 800.0]])
+    errs = np.array([1.0, 3.0, 30.0, 2.0, 7.0, np.nan])
+    res = bench.summarize_scannet(allv, errs, bench.WORKLOADS["scannet"], 1, 0, 2, 19)
+    assert res["value"] == 19.0 / 4.0 and res["unit"] == "pairs/s" and res["scaling"] == "strong"
+    assert res["pose_auc"]["pairs"] == 5
+    ref = utils.pose_auc(errs[:5], (5, 10, 20))
+    assert [res["pose_auc"][k] for k in ("5", "10", "20")] == ref

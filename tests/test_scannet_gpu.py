@@ -1,0 +1,41 @@
+"""configs[4] (ScanNet-1500 stand-in) through the batched path: many pairs in flight
+on one device (mp_estimate_batch) must give every pair the oracle's result, so the
+per-pair pose errors and the pose AUC@5/10/20 equal the CPU oracle's (BASELINE.json:
+"pose AUC@5 parity").  Smaller pairs than the bench (N ~ U{300..500}) keep the oracle
+fast; the pose-error and AUC code is pinned by tests/test_utils_cpu.py."""
+import numpy as np
+import pytest
+
+import madpose
+import oracle
+from madpose_amd import synthetic, utils
+from tests.helpers import oracle_cfg, oracle_opts, rot_angle_deg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def require_gpu():
+    if madpose.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X")
+
+
+def test_batch_pose_auc_matches_oracle():
+    pairs = [synthetic.scannet_pair(s, n_range=(300, 500)) for s in range(16)]
+    o, c = synthetic.example_options("shared_focal", iterations=300)
+    res = madpose.estimate_batch(1, pairs, o, c, num_streams=6)
+    e_dev, e_orc = [], []
+    for p, (m, st) in zip(pairs, res):
+        ref, rst, inl = oracle.estimate(1, p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], p["pp0"],
+                                        p["pp1"], oracle_opts(o), oracle_cfg(c))
+        assert st.num_iterations_total == rst.num_iterations_total
+        assert rot_angle_deg(m.R(), ref["R"]) <= 1e-6
+        for t in range(3):
+            assert np.array_equal(np.sort(st.inlier_indices[t]), np.sort(inl[t]))
+        e_dev.append(max(utils.compute_pose_error(p["T_0to1"], m.R(), m.t())))
+        e_orc.append(max(utils.compute_pose_error(p["T_0to1"], ref["R"], ref["t"])))
+    assert np.allclose(e_dev, e_orc, rtol=0, atol=1e-6)
+    auc_dev = utils.pose_auc(e_dev, (5, 10, 20))
+    auc_orc = utils.pose_auc(e_orc, (5, 10, 20))
+    assert np.allclose(auc_dev, auc_orc, rtol=0, atol=1e-6), (auc_dev, auc_orc)
+    assert auc_dev[2] > 0.5  # the synthetic set is solvable
