@@ -98,7 +98,7 @@ def pmc_traffic_model():
 
 COUNTERS = ["elapsed_s", "hypotheses", "iterations", "lo_runs", "lo_s", "score_ms", "solve_ms", "prof_hypotheses",
             "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms", "prof_iterations",
-            "sample_ms", "wait_ms", "run_ms"]
+            "sample_ms", "wait_ms", "run_ms", "lm_blocks", "lm_big_calls", "lm_big_ms"]
 
 
 def gather_counters(local, world):
@@ -157,6 +157,8 @@ def summarize(allv, wl, steps, warmup, world):
         "lo_runs": int(c["lo_runs"].sum()),
         "lo_share": float(c["lo_s"].sum() / c["elapsed_s"].sum()),
         "lo_breakdown": {"lm_calls": int(c["lm_calls"].sum()), "lm_ms": float(c["lm_ms"].sum()),
+                         "lm_blocks": int(c["lm_blocks"].sum()), "lm_big_calls": int(c["lm_big_calls"].sum()),
+                         "lm_big_ms": float(c["lm_big_ms"].sum()),
                          "sweeps": int(c["prof_sweeps"].sum()), "sweep_ms": float(c["sweep_ms"].sum())},
         # where one pair's wall time goes (host clocks; GPU solve/score from HIP events)
         "ms_per_pair": {k: float(c[src].sum()) / (world * steps) for k, src in
@@ -341,7 +343,7 @@ def main():
     local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
              prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
              prof["sweep_wall_ms"], prof["iterations"], prof["sample_wall_ms"], prof["wait_wall_ms"],
-             prof["run_wall_ms"]]
+             prof["run_wall_ms"], prof["lm_blocks"], prof["lm_big_calls"], prof["lm_big_wall_ms"]]
     allv = gather_counters(local, world)
     if rank == 0:
         res = summarize(allv, wl, a.steps, a.warmup, world)

@@ -198,6 +198,9 @@ typedef struct mp_kernel_profile {
     double sample_wall_ms;    /* host minimal-sample generation + rewinds   */
     double wait_wall_ms;      /* host wait for speculative batch results    */
     double run_wall_ms;       /* whole estimator runs                       */
+    uint64_t lm_blocks;       /* residual blocks over all LM solves         */
+    uint64_t lm_big_calls;    /* LM solves with >= 1024 residual blocks     */
+    double lm_big_wall_ms;    /* host wall time of those                    */
 } mp_kernel_profile;
 int mp_profile_enable(int on);
 int mp_profile_reset(void);

@@ -102,6 +102,9 @@ class mp_kernel_profile(ctypes.Structure):
         ("sample_wall_ms", ctypes.c_double),
         ("wait_wall_ms", ctypes.c_double),
         ("run_wall_ms", ctypes.c_double),
+        ("lm_blocks", ctypes.c_uint64),
+        ("lm_big_calls", ctypes.c_uint64),
+        ("lm_big_wall_ms", ctypes.c_double),
     ]
 
 

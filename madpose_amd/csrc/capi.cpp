@@ -355,6 +355,9 @@ int mp_profile_read(mp_kernel_profile *out) {
     out->sample_wall_ms = p.sample_wall_ms;
     out->wait_wall_ms = p.wait_wall_ms;
     out->run_wall_ms = p.run_wall_ms;
+    out->lm_blocks = p.lm_blocks;
+    out->lm_big_calls = p.lm_big_calls;
+    out->lm_big_wall_ms = p.lm_big_wall_ms;
     return MP_OK;
 }
 

@@ -731,9 +731,16 @@ class Run {
         lm_refine(P_.H, sample, S, m);
         if (g_prof_on.load(std::memory_order_relaxed)) {
             const double dt = secs(t_lm);
+            const size_t nb = (S.use_reproj ? sample[0].size() + sample[1].size() : 0) +
+                              (S.use_sampson ? sample[2].size() : 0);
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.lm_calls += 1;
             g_prof.lm_wall_ms += 1e3 * dt;
+            g_prof.lm_blocks += nb;
+            if (nb >= kBigLM) {
+                g_prof.lm_big_calls += 1;
+                g_prof.lm_big_wall_ms += 1e3 * dt;
+            }
         }
     }
 

@@ -94,7 +94,11 @@ struct KernelProfile {
     double sample_wall_ms = 0.0;   // host minimal-sample generation (incl. LO rewinds)
     double wait_wall_ms = 0.0;     // host wait for batch results
     double run_wall_ms = 0.0;      // whole estimator runs
+    uint64_t lm_blocks = 0;        // residual blocks over all LM solves
+    uint64_t lm_big_calls = 0;     // LM solves with >= kBigLM residual blocks
+    double lm_big_wall_ms = 0.0;   // host wall time of those
 };
+constexpr size_t kBigLM = 1024;
 void profile_enable(bool on);
 void profile_reset();
 KernelProfile profile_read();

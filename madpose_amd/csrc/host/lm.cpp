@@ -95,9 +95,13 @@ struct Acc {
 
 // Evaluates cost (and, when H != nullptr, normal equations) at parameters p.
 // Small persistent pool for the residual loop of large LM problems (the LO's
-// all-inlier fits).  MADPOSE_LO_THREADS sets its size (default 1 = off: an LM
-// iteration is ~10-100 us of work, comparable to a thread wake-up).
+// all-inlier fits, >= kPoolBlocks residual blocks: ~100-500 us per evaluation on one
+// core, on the critical path of every LO); smaller problems (~10-100 us of work,
+// comparable to a thread wake-up) run inline.  MADPOSE_LO_THREADS sets the pool size
+// (default 4; 1 = off).  The blocks are reduced in fixed chunks in chunk order either
+// way, so the result does not depend on the pool.
 constexpr size_t kChunk = 256;
+constexpr size_t kPoolBlocks = 2048;
 class Pool {
   public:
     explicit Pool(int n) {
@@ -165,7 +169,7 @@ class Pool {
 Pool &lo_pool() {
     static Pool pool([] {
         const char *e = std::getenv("MADPOSE_LO_THREADS");
-        const int n = e ? std::atoi(e) : 1;
+        const int n = e ? std::atoi(e) : 4;
         return std::max(1, std::min(n, 64));
     }());
     return pool;
@@ -810,10 +814,14 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
         range(0, nb, total);
     } else {
         std::vector<Acc> parts(nchunks);
-        lo_pool().run(nchunks, [&](size_t k) {
+        auto chunk = [&](size_t k) {
             parts[k].clear();
             range(k * kChunk, std::min(nb, (k + 1) * kChunk), parts[k]);
-        });
+        };
+        if (nb >= kPoolBlocks)
+            lo_pool().run(nchunks, chunk);
+        else
+            for (size_t k = 0; k < nchunks; ++k) chunk(k);
         for (size_t k = 0; k < nchunks; ++k) total.merge(parts[k]);
     }
     if (jac) total.scatter(C, H, g);

@@ -29,7 +29,7 @@ def _worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     # rank r: elapsed 1 + r seconds, 1000 * (r + 1) hypotheses, ...
     local = [1.0 + rank, 1000.0 * (rank + 1), 500.0, 2.0, 0.5, 10.0, 5.0, 1000.0 * (rank + 1),
-             2000.0 * 1000.0 * (rank + 1), 4.0, 7.0, 3.0, 1.0, 2.0, 400.0, 0.3, 0.4, 900.0]
+             2000.0 * 1000.0 * (rank + 1), 4.0, 7.0, 3.0, 1.0, 2.0, 400.0, 0.3, 0.4, 900.0, 5000.0, 1.0, 0.5]
     allv = bench.gather_counters(local, world)
     if rank == 0:
         res = bench.summarize(allv, bench.WORKLOADS["cal"], 3, 1, world)
@@ -53,7 +53,8 @@ def test_single_rank_summary_fields():
     sys.path.insert(0, ROOT)
     import bench
 
-    allv = np.array([[2.0, 3e5, 3e5, 30, 1.0, 100.0, 50.0, 3e5, 3e5 * 2000, 30, 90, 10, 5.0, 6.0, 3e5, 1.0, 2.0, 2000.0]])
+    allv = np.array([[2.0, 3e5, 3e5, 30, 1.0, 100.0, 50.0, 3e5, 3e5 * 2000, 30, 90, 10, 5.0, 6.0, 3e5, 1.0, 2.0, 2000.0,
+                      5e4, 3, 2.0]])
     assert allv.shape[1] == len(bench.COUNTERS)
     res = bench.summarize(allv, bench.WORKLOADS["cal"], 3, 1, 1)
     for k in ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
