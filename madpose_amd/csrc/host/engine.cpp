@@ -108,9 +108,13 @@ class Sampler {
         th_.join();
     }
     // starts drawing B iterations from `from` into *g (the caller must not touch *g
-    // or the slot memory until finish()/cancel() returned)
-    void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp, int *md, int *pt) {
+    // or the slot memory until finish()/cancel() returned); `after` runs on the worker
+    // once the batch is drawn (the post-LO speculation launches it on the GPU there)
+    void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp, int *md, int *pt,
+               std::function<void()> after = nullptr) {
         std::lock_guard<std::mutex> lk(mu_);
+        after_ = std::move(after);
+        err_ = nullptr;
         rs_ = from;
         g_ = g;
         B_ = B;
@@ -128,6 +132,7 @@ class Sampler {
     bool finish(IterationStream *rs) {
         std::unique_lock<std::mutex> lk(mu_);
         done_cv_.wait(lk, [this] { return !busy_; });
+        if (err_) std::rethrow_exception(err_);
         if (ok_) *rs = rs_;
         return ok_;
     }
@@ -147,7 +152,16 @@ class Sampler {
             seen = gen_;
             lk.unlock();
             const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, md_, pt_, &abort_);
+            std::exception_ptr err;
+            if (ok && after_) {
+                try {
+                    after_();
+                } catch (...) {
+                    err = std::current_exception();
+                }
+            }
             lk.lock();
+            err_ = err;
             ok_ = ok;
             busy_ = false;
             done_cv_.notify_all();
@@ -160,6 +174,8 @@ class Sampler {
     uint32_t B_ = 0;
     int slot_ = 0;
     int *smp_ = nullptr, *md_ = nullptr, *pt_ = nullptr;
+    std::function<void()> after_;
+    std::exception_ptr err_;
     std::atomic<bool> abort_{false};
     bool busy_ = false, ok_ = false, quit_ = false;
     uint64_t gen_ = 0;
@@ -380,7 +396,8 @@ struct DeviceCtx {
         MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_model1, sizeof(Model) * 64, hipHostMallocDefault));
-        sweep_slot[0].ensure(nn, stream);
+        // (a stream of its own: the post-LO batch runs on `stream` while LO sweeps)
+        sweep_slot[0].ensure(nn, nullptr);
         cap_n = nn;
         cap_b = bb;
         cap_m = mm;
@@ -834,7 +851,10 @@ class Run {
     // step's end position is checked against the next step's start, steps after a
     // mismatch are recomputed in order, and the steps' update_best calls are applied
     // in step order -- the result is the serial one in every case.
-    void local_opt(int st, Model *best_min, double *best_min_score, int *best_st) {
+    // predicted(sel): called once the LO stream's end state is predicted (parallel
+    // steps), before the steps run -- the estimator speculates the next batch on it.
+    void local_opt(int st, Model *best_min, double *best_min_score, int *best_st,
+                   const std::function<void(const Mt19937 &)> &predicted = nullptr) {
         auto t0 = Clock::now();
         Lane &L0 = lanes_[0];
         double thr[3], upd[3];
@@ -873,6 +893,11 @@ class Run {
                     if (!step_skipped(r == 0 ? sample0 : sample1)) pos += per_step;
                 }
                 const Mt19937 base_sel = sel;
+                if (predicted) {
+                    Mt19937 end = base_sel;
+                    end.discard(pos - base_sel.draws());
+                    predicted(end);
+                }
                 X_.lo_workers->run(R, [&](int r, int lane) {
                     if (lane != 0) MP_HIP(hipSetDevice(X_.device));
                     Mt19937 my = base_sel;
@@ -933,6 +958,43 @@ class Run {
         int scratch[8];
         for (uint32_t r = k * kSnap; r <= j; ++r) rs_.next(scratch);
         sample_s_ += secs(t0);
+    }
+
+    // Solves and scores batch g on the GPU (asynchronous, X_.stream): sample upload,
+    // MD solver on the side stream, the point-solver stages, score_batch, and the
+    // per-iteration best scores / slots / model counts back to pinned host memory.
+    bool batch_prof_ = false;
+    void launch_batch(const Batch &g) {
+        const uint32_t B = g.B;
+        const int nmd = g.nmd, npt = g.npt;
+        hipStream_t s = X_.stream;
+        const bool prof = g_prof_on.load(std::memory_order_relaxed);
+        batch_prof_ = prof;
+        const size_t so = (size_t)g.slot * max_batch_;
+        MP_HIP(hipMemcpyAsync(X_.d_samples, X_.h_samples + 8 * so, sizeof(int) * 8 * B, hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(X_.d_md_list, X_.h_md_list + so, sizeof(int) * std::max(nmd, 1), hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list + so, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
+        if (prof) MP_HIP(hipEventRecord(X_.ev[0], s));
+        // MD iterations on the side stream, point iterations on the main one (they
+        // write disjoint model slots); scoring waits for both
+        if (nmd > 0) {
+            MP_HIP(hipEventRecord(X_.ev_fork, s));
+            MP_HIP(hipStreamWaitEvent(X_.md_stream, X_.ev_fork, 0));
+            MP_HIP(launch_md_solve(X_.md_stream, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs,
+                                   X_.d_counts, maxm_));
+            MP_HIP(hipEventRecord(X_.ev_join, X_.md_stream));
+        }
+        const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid};
+        MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
+                               maxm_));
+        if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
+        if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
+        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_best,
+                                  X_.d_best_slot));
+        if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
+        MP_HIP(hipMemcpyAsync(X_.h_best, X_.d_best, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+        MP_HIP(hipMemcpyAsync(X_.h_best_slot, X_.d_best_slot, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        MP_HIP(hipMemcpyAsync(X_.h_counts, X_.d_counts, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     }
 
     Model fetch_model(int b, int slot) {
@@ -1010,6 +1072,16 @@ void Run::run(Model *best, Stats *S) {
     } cancel_on_exit{X_.sampler.get()};
     int cur = 0;
     bool have_next = false; // gen[cur] already holds the batch starting at `it`
+    bool launched = false;  // ... and it is already on the GPU (post-LO speculation)
+    // Post-LO speculation (MADPOSE_LO_SPECULATE=0 disables): the batch after an LO
+    // depends on the LO only through the selection stream's end state, which the
+    // parallel LO predicts before its steps run.  The sampler draws that batch from the
+    // predicted state and launches it while the steps run; it is kept if the LO ends
+    // exactly there (else discarded), so results never depend on the speculation.
+    const bool speculate = [] {
+        const char *e = std::getenv("MADPOSE_LO_SPECULATE");
+        return !(e && e[0] == '0');
+    }();
     while (it < max_total && !done) {
         if (it == lo_start && best_min_score < kMax) {
             ++S->number_lo_iterations;
@@ -1026,34 +1098,9 @@ void Run::run(Model *best, Stats *S) {
         auto t_batch = Clock::now();
         const Batch &g = gen[cur];
         const uint32_t B = g.B;
-        const int nmd = g.nmd, npt = g.npt;
-        hipStream_t s = X_.stream;
-        const bool prof = g_prof_on.load(std::memory_order_relaxed);
-        const size_t so = (size_t)g.slot * max_batch_;
-        MP_HIP(hipMemcpyAsync(X_.d_samples, X_.h_samples + 8 * so, sizeof(int) * 8 * B, hipMemcpyHostToDevice, s));
-        MP_HIP(hipMemcpyAsync(X_.d_md_list, X_.h_md_list + so, sizeof(int) * std::max(nmd, 1), hipMemcpyHostToDevice, s));
-        MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list + so, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
-        if (prof) MP_HIP(hipEventRecord(X_.ev[0], s));
-        // MD iterations on the side stream, point iterations on the main one (they
-        // write disjoint model slots); scoring waits for both
-        if (nmd > 0) {
-            MP_HIP(hipEventRecord(X_.ev_fork, s));
-            MP_HIP(hipStreamWaitEvent(X_.md_stream, X_.ev_fork, 0));
-            MP_HIP(launch_md_solve(X_.md_stream, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs,
-                                   X_.d_counts, maxm_));
-            MP_HIP(hipEventRecord(X_.ev_join, X_.md_stream));
-        }
-        const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid};
-        MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
-                               maxm_));
-        if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
-        if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
-        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_best,
-                                  X_.d_best_slot));
-        if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
-        MP_HIP(hipMemcpyAsync(X_.h_best, X_.d_best, sizeof(double) * B, hipMemcpyDeviceToHost, s));
-        MP_HIP(hipMemcpyAsync(X_.h_best_slot, X_.d_best_slot, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-        MP_HIP(hipMemcpyAsync(X_.h_counts, X_.d_counts, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        if (!launched) launch_batch(g);
+        launched = false;
+        const bool prof = batch_prof_;
         // While the batch is in flight, the sampler thread draws the next one into the
         // other slot.  It is kept if this batch neither triggers LO nor terminates (both
         // rewind the streams); never across lo_start, where an LO runs before the next
@@ -1067,7 +1114,7 @@ void Run::run(Model *best, Stats *S) {
         if (Bn > 0) X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(0, cur ^ 1), slot_ptr(1, cur ^ 1),
                                       slot_ptr(2, cur ^ 1));
         auto tw = Clock::now();
-        MP_HIP(hipStreamSynchronize(s));
+        MP_HIP(hipStreamSynchronize(X_.stream));
         S->seconds_gpu_wait += secs(tw);
         batch_s_ = 0.5 * batch_s_ + 0.5 * secs(t_batch);
         S->num_batches++;
@@ -1087,6 +1134,8 @@ void Run::run(Model *best, Stats *S) {
         }
 
         bool invalidated = false;
+        bool spec = false; // the sampler holds the post-LO speculation, not the Bn batch
+        uint64_t spec_draws = 0;
         uint32_t j = 0;
         for (; j < B; ++j) {
             const uint32_t iter = it + j;
@@ -1112,7 +1161,22 @@ void Run::run(Model *best, Stats *S) {
                             rewind(g, j);
                             ++S->number_lo_iterations;
                             double sc = best_min_score;
-                            local_opt(S->best_solver_type, &best_min, &sc, &S->best_solver_type);
+                            const uint32_t at = iter + 1;
+                            auto predicted = [&](const Mt19937 &sel_end) {
+                                if (!speculate || at >= max_total) return;
+                                if (Bn > 0) X_.sampler->cancel(); // the no-LO continuation
+                                IterationStream from = rs_;
+                                from.sel = sel_end;
+                                const uint32_t bc = (uint32_t)std::min<uint64_t>(
+                                    (uint64_t)max_batch_, std::max<uint64_t>((uint64_t)min_batch_, 4ull * at));
+                                const int slot = cur ^ 1;
+                                Batch *gs = &gen[slot];
+                                X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(0, slot),
+                                                  slot_ptr(1, slot), slot_ptr(2, slot), [this, gs] { launch_batch(*gs); });
+                                spec = true;
+                                spec_draws = sel_end.draws();
+                            };
+                            local_opt(S->best_solver_type, &best_min, &sc, &S->best_solver_type, predicted);
                             if (trace_) std::fprintf(stderr, "[engine] it=%u LO %.17g -> %.17g\n", iter, best_min_score, sc);
                             update_best(sc, best_min, st, &S->best_model_score, best, &S->best_solver_type);
                             lo_here = true;
@@ -1144,6 +1208,19 @@ void Run::run(Model *best, Stats *S) {
                 if (have_next) cur ^= 1;
             }
             // (otherwise rs_ stands at the end of this batch)
+        } else if (spec) {
+            have_next = false;
+            if (!done && rs_.sel.draws() == spec_draws) {
+                // the LO ended where predicted: the speculative batch comes next
+                have_next = X_.sampler->finish(&rs_);
+                if (have_next) {
+                    cur ^= 1;
+                    launched = true;
+                }
+            } else {
+                X_.sampler->cancel();
+                MP_HIP(hipStreamSynchronize(X_.stream)); // a launched speculation drains
+            }
         } else {
             if (Bn > 0) X_.sampler->cancel();
             have_next = false;
