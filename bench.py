@@ -277,8 +277,8 @@ def run_scannet(a, wl, world, rank, dev, barrier):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cal")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (0 = skip)")
     ap.add_argument("--pairs", type=int, default=0, help="scannet: total pairs (default 1500)")

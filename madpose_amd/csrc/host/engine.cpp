@@ -62,7 +62,7 @@ const double kMax = DBL_MAX;
 // Minimal-sample batches (host).  One batch holds its iterations' solver types and
 // samples (in a pinned host slot), plus snapshots of both random streams every
 // kSnap iterations so a rewind to iteration j replays fewer than kSnap iterations.
-constexpr uint32_t kSnap = 2048;
+constexpr uint32_t kSnap = 512;
 struct Batch {
     uint32_t B = 0;
     int nmd = 0, npt = 0, slot = 0;
@@ -592,7 +592,7 @@ class Run {
         w_[1] = P.C.w[1];
         w_[2] = P.C.w[2];
         const char *env = std::getenv("MADPOSE_MAX_BATCH");
-        max_batch_ = env ? std::max(1, std::atoi(env)) : 65536;
+        max_batch_ = env ? std::max(1, std::atoi(env)) : 32768;
         const char *env2 = std::getenv("MADPOSE_MIN_BATCH");
         min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 128;
         min_batch_ = std::min(min_batch_, max_batch_);
