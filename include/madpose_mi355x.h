@@ -142,6 +142,16 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
                     const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
                     double *errors, int device);
 
+/* get_depths (madpose/utils.py:4-22) for many pairs in one launch: pair p's depth map
+ * (dims[4p] x dims[4p+1], row-major, float32 for dtype 0 or float64 for dtype 1) is
+ * stored after the previous pairs' maps in depth_maps; dims[4p+2], dims[4p+3] are the
+ * image height and width the keypoints refer to; its keypoints (x, y pairs, float64)
+ * are keypoints[2 pt_offsets[p] .. 2 pt_offsets[p+1]) and the depths go to
+ * out[pt_offsets[p] ..] (dtype of the maps).  Same rounding (half to even), clipping
+ * and [y, x] lookup as the reference's numpy code, so results are bit-identical. */
+int mp_get_depths(int dtype, int32_t num_pairs, const void *depth_maps, const int64_t *dims, const int64_t *pt_offsets,
+                  const double *keypoints, void *out, int device);
+
 /* Point minimal solver (PoseLib relpose_5pt, src/hybrid_pose_estimator.cpp:134) on unit bearings
  * (5 points, point-major 3 doubles each).  Returns count or -code. */
 int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device);

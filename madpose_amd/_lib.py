@@ -118,6 +118,8 @@ EXPORTS = {
                                          ctypes.POINTER(mp_ransac_options), ctypes.POINTER(mp_estimator_config),
                                          ctypes.POINTER(mp_model), ctypes.POINTER(mp_stats), c_int32_p, ctypes.c_int,
                                          ctypes.c_int]),
+    "mp_get_depths": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_void_p, c_int64_p, c_int64_p, c_double_p,
+                                     ctypes.c_void_p, ctypes.c_int]),
     "mp_estimate_scale_and_pose": (ctypes.c_int, [c_double_p, c_double_p, c_double_p, ctypes.c_int64,
                                                   ctypes.POINTER(mp_model), ctypes.c_int]),
     "mp_solve_scale_and_shift": (ctypes.c_int, [ctypes.c_int, c_double_p, c_double_p, c_double_p, c_double_p,

@@ -415,6 +415,43 @@ def estimate_batch(variant, pairs, options, est_config=None, device=None, num_st
     return out
 
 
+def get_depths_batch(images, depth_maps, mkpts, device=None):
+    """madpose.utils.get_depths (madpose/utils.py:4-22) for many pairs in one device
+    launch.  images: the images (only their shapes are used) or (h, w) tuples;
+    depth_maps: 2-D float32 or float64 arrays (one dtype for the batch); mkpts: n_p x 2
+    keypoints per map.  Returns one array of depths per map (the maps' dtype),
+    bit-identical to the numpy reference."""
+    if not (len(images) == len(depth_maps) == len(mkpts)):
+        raise ValueError("images, depth_maps and mkpts must have the same length")
+    P = len(depth_maps)
+    if P == 0:
+        return []
+    dt = np.result_type(*[np.asarray(d).dtype for d in depth_maps])
+    if dt not in (np.float32, np.float64):
+        dt = np.dtype(np.float64)
+    maps, dims, pts, offs = [], [], [], [0]
+    for img, dm, kp in zip(images, depth_maps, mkpts):
+        dm = np.asarray(dm)
+        if dm.ndim != 2:
+            raise ValueError("depth maps must be 2-D")
+        ih, iw = (img if isinstance(img, tuple) else np.shape(img))[:2]
+        kp = np.ascontiguousarray(kp, dtype=np.float64).reshape(-1, 2)
+        maps.append(np.ascontiguousarray(dm, dtype=dt).reshape(-1))
+        dims.append([dm.shape[0], dm.shape[1], ih, iw])
+        pts.append(kp)
+        offs.append(offs[-1] + len(kp))
+    M = np.ascontiguousarray(np.concatenate(maps))
+    D = np.ascontiguousarray(np.asarray(dims, dtype=np.int64).reshape(-1))
+    O = np.asarray(offs, dtype=np.int64)
+    X = np.ascontiguousarray(np.concatenate(pts).reshape(-1)) if offs[-1] else np.zeros(2)
+    out = np.zeros(max(offs[-1], 1), dtype=dt)
+    L.check(L.lib().mp_get_depths(0 if dt == np.float32 else 1, P, M.ctypes.data_as(ctypes.c_void_p),
+                                  D.ctypes.data_as(L.c_int64_p), O.ctypes.data_as(L.c_int64_p), _dp(X),
+                                  out.ctypes.data_as(ctypes.c_void_p),
+                                  _DEFAULT_DEVICE if device is None else int(device)))
+    return [out[offs[p]:offs[p + 1]].copy() for p in range(P)]
+
+
 # ---------------------------------------------------------------------------
 # standalone solver bindings (src/bindings.cpp:156-166)
 def _homog_pm(a, k, name):

@@ -183,6 +183,16 @@ int mp_estimate_batch(int variant, int32_t num_pairs, const int64_t *offsets, co
     });
 }
 
+int mp_get_depths(int dtype, int32_t num_pairs, const void *depth_maps, const int64_t *dims, const int64_t *pt_offsets,
+                  const double *keypoints, void *out, int device) {
+    return guarded([&]() {
+        if (num_pairs < 0 || (num_pairs > 0 && (!depth_maps || !dims || !pt_offsets || !out)))
+            throw std::invalid_argument("bad get_depths arguments");
+        mp::get_depths_batch(dtype, num_pairs, depth_maps, dims, pt_offsets, keypoints, out, device);
+        return MP_OK;
+    });
+}
+
 int mp_estimate_scale_and_pose(const double *X, const double *Y, const double *W, int64_t n, mp_model *out,
                                int device) {
     return guarded([&]() {

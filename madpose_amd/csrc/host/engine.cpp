@@ -1449,6 +1449,51 @@ void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const
     for (void *p : {(void *)d_pair, (void *)d_cand, (void *)d_smp, (void *)d_list, (void *)d_n}) hipFree(p);
 }
 
+void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *dims, const int64_t *pt_off,
+                      const double *pts, void *out, int device) {
+    if (dtype != 0 && dtype != 1) throw std::invalid_argument("dtype must be 0 (float32) or 1 (float64)");
+    if (num <= 0) return;
+    const size_t es = dtype == 0 ? sizeof(float) : sizeof(double);
+    std::vector<int64_t> map_off(num + 1), hw(2 * (size_t)num);
+    std::vector<double> fac(2 * (size_t)num);
+    map_off[0] = 0;
+    for (int p = 0; p < num; ++p) {
+        const int64_t h = dims[4 * p], w = dims[4 * p + 1], ih = dims[4 * p + 2], iw = dims[4 * p + 3];
+        if (h <= 0 || w <= 0 || ih <= 0 || iw <= 0) throw std::invalid_argument("bad depth-map or image size");
+        if (pt_off[p + 1] < pt_off[p]) throw std::invalid_argument("keypoint offsets must not decrease");
+        map_off[p + 1] = map_off[p] + h * w;
+        hw[2 * p] = h;
+        hw[2 * p + 1] = w;
+        fac[2 * p] = (double)w / (double)iw; // factor = [dm_w / im_w, dm_h / im_h]
+        fac[2 * p + 1] = (double)h / (double)ih;
+    }
+    const int64_t total = pt_off[num], cells = map_off[num];
+    CtxLease lease(device);
+    hipStream_t s = lease.c->stream;
+    char *d_maps, *d_out;
+    int64_t *d_map_off, *d_hw, *d_pt_off;
+    double *d_fac, *d_pts;
+    MP_HIP(hipMalloc(&d_maps, es * (size_t)std::max<int64_t>(cells, 1)));
+    MP_HIP(hipMalloc(&d_out, es * (size_t)std::max<int64_t>(total, 1)));
+    MP_HIP(hipMalloc(&d_map_off, sizeof(int64_t) * (num + 1)));
+    MP_HIP(hipMalloc(&d_hw, sizeof(int64_t) * 2 * num));
+    MP_HIP(hipMalloc(&d_pt_off, sizeof(int64_t) * (num + 1)));
+    MP_HIP(hipMalloc(&d_fac, sizeof(double) * 2 * num));
+    MP_HIP(hipMalloc(&d_pts, sizeof(double) * 2 * (size_t)std::max<int64_t>(total, 1)));
+    MP_HIP(hipMemcpyAsync(d_maps, maps, es * (size_t)cells, hipMemcpyHostToDevice, s));
+    MP_HIP(hipMemcpyAsync(d_map_off, map_off.data(), sizeof(int64_t) * (num + 1), hipMemcpyHostToDevice, s));
+    MP_HIP(hipMemcpyAsync(d_hw, hw.data(), sizeof(int64_t) * 2 * num, hipMemcpyHostToDevice, s));
+    MP_HIP(hipMemcpyAsync(d_pt_off, pt_off, sizeof(int64_t) * (num + 1), hipMemcpyHostToDevice, s));
+    MP_HIP(hipMemcpyAsync(d_fac, fac.data(), sizeof(double) * 2 * num, hipMemcpyHostToDevice, s));
+    if (total > 0) MP_HIP(hipMemcpyAsync(d_pts, pts, sizeof(double) * 2 * total, hipMemcpyHostToDevice, s));
+    MP_HIP(launch_get_depths(s, dtype, d_maps, d_map_off, d_hw, d_fac, d_pt_off, num, total, d_pts, d_out));
+    if (total > 0) MP_HIP(hipMemcpyAsync(out, d_out, es * (size_t)total, hipMemcpyDeviceToHost, s));
+    MP_HIP(hipStreamSynchronize(s));
+    for (void *p : {(void *)d_maps, (void *)d_out, (void *)d_map_off, (void *)d_hw, (void *)d_pt_off, (void *)d_fac,
+                    (void *)d_pts})
+        hipFree(p);
+}
+
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device) {
     CtxLease lease(device);
     DeviceCtx &C = *lease.c;

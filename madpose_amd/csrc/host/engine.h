@@ -75,6 +75,10 @@ void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const
 
 // estimate_scale_and_pose (src/solver.cpp:5-33) on the device; X, Y point-major n x 3
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device);
+// get_depths of num pairs on the device (see launch_get_depths); dims: num x 4
+// (depth-map h, w, image h, w); host buffers in and out
+void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *dims, const int64_t *pt_off,
+                      const double *pts, void *out, int device);
 
 int device_count();
 

@@ -57,4 +57,11 @@ hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model 
 // estimate_scale_and_pose over n points (in = X(3n) Y(3n) W(n)), one thread
 hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out);
 
+// get_depths of num pairs in one launch (dtype 0 float32, 1 float64 maps): map p at
+// maps + map_off[p] (dims[2p] x dims[2p+1]), size ratios fac[2p] (x), fac[2p+1] (y),
+// its keypoints at pts[2 pt_off[p] ..], results at out[pt_off[p] ..]; total = pt_off[num]
+hipError_t launch_get_depths(hipStream_t s, int dtype, const void *maps, const int64_t *map_off, const int64_t *dims,
+                             const double *fac, const int64_t *pt_off, int32_t num, int64_t total, const double *pts,
+                             void *out);
+
 } // namespace mp

@@ -833,6 +833,45 @@ hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *i
     return hipGetLastError();
 }
 
+// get_depths over many pairs (madpose/utils.py:4-22): keypoint i of pair p is scaled by
+// the pair's (depth-map / image) size ratios, rounded half to even (rint under the
+// default rounding mode, as np.round), clipped to the map and looked up at [y, x].
+// One lane per keypoint; the pair is found by binary search over the keypoint offsets.
+template <typename T>
+__global__ void get_depths_kernel(const T *maps, const int64_t *map_off, const int64_t *dims, const double *fac,
+                                  const int64_t *pt_off, int32_t num, const double *pts, T *out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= pt_off[num]) return;
+    int lo = 0, hi = num - 1; // last pair with pt_off[p] <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) / 2;
+        if (pt_off[mid] <= i)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const int p = lo;
+    const int64_t h = dims[2 * p], w = dims[2 * p + 1];
+    int64_t c = (int64_t)rint(pts[2 * i] * fac[2 * p]), r = (int64_t)rint(pts[2 * i + 1] * fac[2 * p + 1]);
+    c = c < 0 ? 0 : (c > w - 1 ? w - 1 : c);
+    r = r < 0 ? 0 : (r > h - 1 ? h - 1 : r);
+    out[i] = maps[map_off[p] + r * w + c];
+}
+
+hipError_t launch_get_depths(hipStream_t s, int dtype, const void *maps, const int64_t *map_off, const int64_t *dims,
+                             const double *fac, const int64_t *pt_off, int32_t num, int64_t total, const double *pts,
+                             void *out) {
+    if (total <= 0) return hipSuccess;
+    const int grid = (int)((total + 255) / 256);
+    if (dtype == 0)
+        get_depths_kernel<float><<<grid, 256, 0, s>>>((const float *)maps, map_off, dims, fac, pt_off, num, pts,
+                                                      (float *)out);
+    else
+        get_depths_kernel<double><<<grid, 256, 0, s>>>((const double *)maps, map_off, dims, fac, pt_off, num, pts,
+                                                       (double *)out);
+    return hipGetLastError();
+}
+
 hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out) {
     scale_and_pose_kernel<<<1, 64, 0, s>>>(in, n, out);
     return hipGetLastError();

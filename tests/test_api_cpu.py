@@ -53,7 +53,9 @@ def test_python_surface_matches_reference_bindings():
 
 
 def test_input_validation_raises_before_device():
-    o, c = madpose_amd.synthetic.example_options()
+    from madpose_amd import synthetic
+
+    o, c = synthetic.example_options()
     with pytest.raises(ValueError):
         madpose.HybridEstimatePoseScaleOffset(np.zeros((5, 2)), np.zeros((4, 2)), np.ones(5), np.ones(5), [0, 0],
                                               np.eye(3), np.eye(3), o, c)
