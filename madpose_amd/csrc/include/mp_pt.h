@@ -464,15 +464,24 @@ MP_HD void triangulate(const double *R, const double *t, double fa, double fb, c
     X[2] = v[2] / v[3];
 }
 
-MP_HD void ls_affine(const double *d, const double *z, int k, double *a, double *b) {
+// Least-squares z ~ a d + b over the points with use[i] (src/hybrid_pose_estimator.cpp
+// :160-167, the 2x2 normal equations solved in closed form).  Local sums go through
+// sum() (identity for one lane holding all n points, a group all-reduce when every
+// lane holds one point).
+template <int K, class Sum>
+MP_HD void ls_affine(const double *d, const double *z, const bool *use, double n, Sum &&sum, double *a, double *b) {
     double sdd = 0, sd = 0, sz = 0, sdz = 0;
-    for (int i = 0; i < k; ++i) {
-        sdd += d[i] * d[i];
-        sd += d[i];
-        sz += z[i];
-        sdz += d[i] * z[i];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        sdd += use[i] ? d[i] * d[i] : 0.0;
+        sd += use[i] ? d[i] : 0.0;
+        sz += use[i] ? z[i] : 0.0;
+        sdz += use[i] ? d[i] * z[i] : 0.0;
     }
-    const double n = (double)k;
+    sdd = sum(sdd);
+    sd = sum(sd);
+    sz = sum(sz);
+    sdz = sum(sdz);
     const double det = sdd * n - sd * sd;
     *a = (n * sdz - sd * sz) / det;
     *b = (sdd * sz - sd * sdz) / det;
@@ -480,11 +489,13 @@ MP_HD void ls_affine(const double *d, const double *z, int k, double *a, double 
 
 // Triangulate the sample with a candidate pose and fit (scale, offsets) to the depth
 // priors (src/hybrid_pose_estimator.cpp:136-182; sf :93-126; tf :148-181).
-// p0/p1: 2-D image coordinates (calibrated for cal, normalized pixels for sf/tf).
-template <int K>
-MP_HD bool point_model_tail(const double (&p0)[K][2], const double (&p1)[K][2], const double *dd0, const double *dd1,
-                            double fa, double fb, bool use_shift, bool min_depth_constraint, const double *min_depth,
-                            Model &m) {
+// p0/p1: 2-D image coordinates (calibrated for cal, normalized pixels for sf/tf) of
+// the K points this lane holds (use[i]: point present), n: points of the sample over
+// all lanes, sum(): the reduction of local sums over the lanes holding the sample.
+template <int K, class Sum>
+MP_HD bool point_model_tail_r(const double (&p0)[K][2], const double (&p1)[K][2], const double *dd0, const double *dd1,
+                              const bool *use, double n, double fa, double fb, bool use_shift,
+                              bool min_depth_constraint, const double *min_depth, Model &m, Sum &&sum) {
     double X[K][3], z[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) triangulate(m.R, m.t, fa, fb, p0[j], p1[j], X[j]);
@@ -493,10 +504,10 @@ MP_HD bool point_model_tail(const double (&p0)[K][2], const double (&p1)[K][2], 
         double num = 0, den = 0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            num += dd0[j] * X[j][2];
-            den += dd0[j] * dd0[j];
+            num += use[j] ? dd0[j] * X[j][2] : 0.0;
+            den += use[j] ? dd0[j] * dd0[j] : 0.0;
         }
-        const double s0 = num / den;
+        const double s0 = sum(num) / sum(den);
 #pragma unroll
         for (int c = 0; c < 3; ++c) t[c] /= s0;
         num = den = 0;
@@ -504,16 +515,16 @@ MP_HD bool point_model_tail(const double (&p0)[K][2], const double (&p1)[K][2], 
         for (int j = 0; j < K; ++j) {
             const double q[3] = {X[j][0] / s0, X[j][1] / s0, X[j][2] / s0};
             const double zz = m.R[6] * q[0] + m.R[7] * q[1] + m.R[8] * q[2] + t[2];
-            num += dd1[j] * zz;
-            den += dd1[j] * dd1[j];
+            num += use[j] ? dd1[j] * zz : 0.0;
+            den += use[j] ? dd1[j] * dd1[j] : 0.0;
         }
-        m.scale = num / den;
+        m.scale = sum(num) / sum(den);
         m.offset0 = m.offset1 = 0.0;
     } else {
 #pragma unroll
         for (int j = 0; j < K; ++j) z[j] = X[j][2];
         double s0, b0;
-        ls_affine(dd0, z, K, &s0, &b0);
+        ls_affine<K>(dd0, z, use, n, sum, &s0, &b0);
         const double offset0 = b0 / s0;
         if (min_depth_constraint && offset0 < -min_depth[0]) return false;
 #pragma unroll
@@ -524,7 +535,7 @@ MP_HD bool point_model_tail(const double (&p0)[K][2], const double (&p1)[K][2], 
             z[j] = m.R[6] * q[0] + m.R[7] * q[1] + m.R[8] * q[2] + t[2];
         }
         double sc, b1;
-        ls_affine(dd1, z, K, &sc, &b1);
+        ls_affine<K>(dd1, z, use, n, sum, &sc, &b1);
         const double offset1 = b1 / sc;
         if (min_depth_constraint && offset1 < -min_depth[1]) return false;
         m.scale = sc;
@@ -535,6 +546,18 @@ MP_HD bool point_model_tail(const double (&p0)[K][2], const double (&p1)[K][2], 
     m.t[1] = t[1];
     m.t[2] = t[2];
     return true;
+}
+
+// all K points in this lane
+template <int K>
+MP_HD bool point_model_tail(const double (&p0)[K][2], const double (&p1)[K][2], const double *dd0, const double *dd1,
+                            double fa, double fb, bool use_shift, bool min_depth_constraint, const double *min_depth,
+                            Model &m) {
+    bool use[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) use[j] = true;
+    return point_model_tail_r<K>(p0, p1, dd0, dd1, use, (double)K, fa, fb, use_shift, min_depth_constraint, min_depth,
+                                 m, [](double v) { return v; });
 }
 
 } // namespace mp

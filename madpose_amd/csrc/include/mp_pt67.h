@@ -203,11 +203,15 @@ MP_HD void jacobi_eig3(double (&A)[3][3], double (&V)[3][3]) {
     }
 }
 
-// cv::recoverPose(E, p0, p1, I, R, t, dist) with the candidate order of OpenCV's
-// decomposeEssentialMat; returns the number of good points of the chosen pose.
-template <int K>
-MP_HD int recover_pose_cv(const double *E_in, const double (&p0)[K][2], const double (&p1)[K][2], double dist,
-                          double *R, double *t) {
+// cv::recoverPose(E, p0, p1, I, R, t, dist) in three parts: the candidate poses of E
+// (OpenCV's decomposeEssentialMat order: (R1, t), (R2, t), (R1, -t), (R2, -t)), the
+// per-point DLT test of a candidate, and the choice of the candidate with the most
+// good points (first maximum).  recover_pose_cv runs them over K points in one lane;
+// the group tail kernel (group_tail.h) runs one point per lane.
+struct RecoverCands {
+    double R1[9], R2[9], u2[3];
+};
+MP_HD void recover_pose_candidates(const double *E_in, RecoverCands &rc) {
     // canonical sign of E (largest-magnitude entry positive), as in the oracle
     double emax = E_in[0];
 #pragma unroll
@@ -274,51 +278,53 @@ MP_HD int recover_pose_cv(const double *E_in, const double (&p0)[K][2], const do
         for (int r = 0; r < 3; ++r) u[1][r] *= n1;
     }
     cross3(u[0], u[1], u[2]);
-    double R1[9], R2[9];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            R1[3 * r + c] = -u[1][r] * v[0][c] + u[0][r] * v[1][c] + u[2][r] * v[2][c];
-            R2[3 * r + c] = u[1][r] * v[0][c] - u[0][r] * v[1][c] + u[2][r] * v[2][c];
+            rc.R1[3 * r + c] = -u[1][r] * v[0][c] + u[0][r] * v[1][c] + u[2][r] * v[2][c];
+            rc.R2[3 * r + c] = u[1][r] * v[0][c] - u[0][r] * v[1][c] + u[2][r] * v[2][c];
         }
-    int good[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const double *Rk = (k & 1) ? R2 : R1;
-        const double ts = (k < 2) ? 1.0 : -1.0;
-        double P1[3][4];
+    for (int r = 0; r < 3; ++r) rc.u2[r] = u[2][r];
+}
+
+// cheirality of one point under candidate k (OpenCV: DLT triangulation, positive and
+// finite depth in both views)
+MP_HD bool recover_pose_good(const RecoverCands &rc, int k, const double *p0, const double *p1, double dist) {
+    const double ts = (k < 2) ? 1.0 : -1.0;
+    double P1[3][4];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < 3; ++r) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) P1[r][c] = Rk[3 * r + c];
-            P1[r][3] = ts * u[2][r];
-        }
-        for (int i = 0; i < K; ++i) {
-            double A[4][4];
-            A[0][0] = -1.0;
-            A[0][1] = 0.0;
-            A[0][2] = p0[i][0];
-            A[0][3] = 0.0;
-            A[1][0] = 0.0;
-            A[1][1] = -1.0;
-            A[1][2] = p0[i][1];
-            A[1][3] = 0.0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                A[2][j] = p1[i][0] * P1[2][j] - P1[0][j];
-                A[3][j] = p1[i][1] * P1[2][j] - P1[1][j];
-            }
-            double Qh[4];
-            smallest_right_sv4(A, Qh);
-            bool ok = Qh[2] * Qh[3] > 0;
-            const double X0 = Qh[0] / Qh[3], X1 = Qh[1] / Qh[3], X2 = Qh[2] / Qh[3];
-            ok = ok && X2 < dist;
-            const double z1 = P1[2][0] * X0 + P1[2][1] * X1 + P1[2][2] * X2 + P1[2][3];
-            ok = ok && z1 > 0 && z1 < dist;
-            good[k] += ok ? 1 : 0;
-        }
+        for (int c = 0; c < 3; ++c) P1[r][c] = (k & 1) ? rc.R2[3 * r + c] : rc.R1[3 * r + c];
+        P1[r][3] = ts * rc.u2[r];
     }
+    double A[4][4];
+    A[0][0] = -1.0;
+    A[0][1] = 0.0;
+    A[0][2] = p0[0];
+    A[0][3] = 0.0;
+    A[1][0] = 0.0;
+    A[1][1] = -1.0;
+    A[1][2] = p0[1];
+    A[1][3] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        A[2][j] = p1[0] * P1[2][j] - P1[0][j];
+        A[3][j] = p1[1] * P1[2][j] - P1[1][j];
+    }
+    double Qh[4];
+    smallest_right_sv4(A, Qh);
+    bool ok = Qh[2] * Qh[3] > 0;
+    const double X0 = Qh[0] / Qh[3], X1 = Qh[1] / Qh[3], X2 = Qh[2] / Qh[3];
+    ok = ok && X2 < dist;
+    const double z1 = P1[2][0] * X0 + P1[2][1] * X1 + P1[2][2] * X2 + P1[2][3];
+    return ok && z1 > 0 && z1 < dist;
+}
+
+// the candidate with the most good points (ties: the first); returns its count
+MP_HD int recover_pose_select(const RecoverCands &rc, const int (&good)[4], double *R, double *t) {
     int best = 3;
     if (good[0] >= good[1] && good[0] >= good[2] && good[0] >= good[3])
         best = 0;
@@ -326,13 +332,25 @@ MP_HD int recover_pose_cv(const double *E_in, const double (&p0)[K][2], const do
         best = 1;
     else if (good[2] >= good[0] && good[2] >= good[1] && good[2] >= good[3])
         best = 2;
-    const double *Rb = (best & 1) ? R2 : R1;
     const double ts = (best < 2) ? 1.0 : -1.0;
 #pragma unroll
-    for (int e = 0; e < 9; ++e) R[e] = Rb[e];
+    for (int e = 0; e < 9; ++e) R[e] = (best & 1) ? rc.R2[e] : rc.R1[e]; // (selects: rc stays in registers)
 #pragma unroll
-    for (int r = 0; r < 3; ++r) t[r] = ts * u[2][r];
+    for (int r = 0; r < 3; ++r) t[r] = ts * rc.u2[r];
     return (best == 0) ? good[0] : ((best == 1) ? good[1] : ((best == 2) ? good[2] : good[3]));
+}
+
+// cv::recoverPose(E, p0, p1, I, R, t, dist); returns the good-point count of the pose
+template <int K>
+MP_HD int recover_pose_cv(const double *E_in, const double (&p0)[K][2], const double (&p1)[K][2], double dist,
+                          double *R, double *t) {
+    RecoverCands rc;
+    recover_pose_candidates(E_in, rc);
+    int good[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int i = 0; i < K; ++i) good[k] += recover_pose_good(rc, k, p0[i], p1[i], dist) ? 1 : 0;
+    return recover_pose_select(rc, good, R, t);
 }
 
 // ---------------------------------------------------------------------------

@@ -17,6 +17,7 @@
 #include "../include/mp_score.h"
 #include "group_5pt.h"
 #include "group_6pt.h"
+#include "group_tail.h"
 #include "kernels.h"
 
 namespace mp {
@@ -757,9 +758,16 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                                                                                       W.cand, W.ncand, kCandStride);
         else
             pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
+        // two-focal tail: one 8-lane group per (root, sample) (group_tail.h);
+        // MADPOSE_TAIL7_LANE=1 selects the one-lane kernel
+        static const bool lane7 = std::getenv("MADPOSE_TAIL7_LANE") != nullptr;
         const long lanes = (long)nlist * PtTraits<v>::kRoots;
-        pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
-                                                                  W.slots, W.valid);
+        if (v == kTF && !lane7)
+            pt_tail7_group_kernel<<<(int)((lanes * kTail + 63) / 64), 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand,
+                                                                                 samples, W.slots, W.valid);
+        else
+            pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
+                                                                      W.slots, W.valid);
         pt_compact_kernel<v><<<grid, 64, 0, s>>>(C, list, nlist, W.ncand, W.slots, W.valid, models, recs, counts,
                                                  maxm);
         return hipGetLastError();
