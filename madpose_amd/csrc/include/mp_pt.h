@@ -20,10 +20,13 @@
 namespace mp {
 
 // motion_from_essential (src/solver.cpp:1219-1285): up to 4 candidate poses, kept
-// when all np points pass cheirality.  Returns number of poses appended at out[k..].
-template <int NP>
-MP_HD int motion_from_essential(const double *E, const double (&x1)[NP][3], const double (&x2)[NP][3], Model *out,
-                                int k, int kmax) {
+// when all points pass cheirality.  Returns number of poses appended at out[k..].
+// This lane tests its NP points (use[i]: present); all_ok() combines the verdicts of
+// the lanes holding the sample (identity when one lane holds them all); emit(m, q)
+// receives the q-th kept pose, for q < cap.
+template <int NP, class All, class Emit>
+MP_HD int motion_from_essential_r(const double *E, const double (&x1)[NP][3], const double (&x2)[NP][3],
+                                  const bool *use, int cap, All &&all_ok, Emit &&emit) {
     const double c0[3] = {E[0], E[3], E[6]}, c1[3] = {E[1], E[4], E[7]}, c2[3] = {E[2], E[5], E[8]};
     double u12[3], u13[3], u23[3];
     cross3(c0, c1, u12);
@@ -66,27 +69,39 @@ MP_HD int motion_from_essential(const double *E, const double (&x1)[NP][3], cons
     for (int j = 0; j < 3; ++j) V1[j] /= n1;
     cross3(V0, V1, V2);
     int added = 0;
-    const double sr[4] = {1.0, 1.0, -1.0, -1.0}, st[4] = {1.0, -1.0, -1.0, 1.0};
     for (int c = 0; c < 4; ++c) {
+        // signs of the candidates (c: R sign, t sign) = (+,+), (+,-), (-,-), (-,+)
+        const double sr_c = c < 2 ? 1.0 : -1.0, st_c = (c == 0 || c == 3) ? 1.0 : -1.0;
         Model m;
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
-            for (int q = 0; q < 3; ++q) m.R[3 * r + q] = sr[c] * (U0[r] * V0[q] + U1[r] * V1[q]) + U2[r] * V2[q];
+            for (int q = 0; q < 3; ++q) m.R[3 * r + q] = sr_c * (U0[r] * V0[q] + U1[r] * V1[q]) + U2[r] * V2[q];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) m.t[r] = st[c] * U2[r];
+        for (int r = 0; r < 3; ++r) m.t[r] = st_c * U2[r];
         bool ok = true;
 #pragma unroll
-        for (int i = 0; i < NP; ++i) ok = ok && check_cheirality(m.R, m.t, x1[i], x2[i], 0.0);
-        if (ok && k + added < kmax) {
+        for (int i = 0; i < NP; ++i) ok = ok && (!use[i] || check_cheirality(m.R, m.t, x1[i], x2[i], 0.0));
+        ok = all_ok(ok);
+        if (ok && added < cap) {
             m.scale = 1.0;
             m.offset0 = m.offset1 = 0.0;
             m.focal0 = m.focal1 = 1.0;
-            out[k + added] = m;
+            emit(m, added);
             ++added;
         }
     }
     return added;
+}
+
+template <int NP>
+MP_HD int motion_from_essential(const double *E, const double (&x1)[NP][3], const double (&x2)[NP][3], Model *out,
+                                int k, int kmax) {
+    bool use[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) use[i] = true;
+    return motion_from_essential_r<NP>(E, x1, x2, use, kmax - k, [](bool b) { return b; },
+                                       [&](const Model &m, int q) { out[k + q] = m; });
 }
 
 // ---- monomials of degree <= 3 in (x, y, z), Nister's column order ----

@@ -1,4 +1,5 @@
-// Point-solver tail of the two-focal estimator with one 8-lane group per (root, sample)
+// Point-solver tails with one 8-lane group per (root, sample): two-focal below, then
+// calibrated.  Two-focal
 // (src/hybrid_pose_two_focal_estimator.cpp:118-181): Bougnoux focals of the root's F,
 // E = K1^T F K0, cv::recoverPose on the seven points, triangulation and the affine
 // depth fits.
@@ -79,6 +80,57 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
         const size_t q = (size_t)idx * kPtSlotStride + k; // PtTraits<kTF>::kPosesPerRoot == 1
         if (ok) slots[q] = m;
         valid[q] = ok ? 1 : 0;
+    }
+}
+
+// Calibrated tail (src/hybrid_pose_estimator.cpp:134-182) with one 8-lane group per
+// (root, sample), lane j < 5 holding point j: the cheirality tests of
+// motion_from_essential (AND over the group), then for each of the at most two poses
+// the triangulation and depth fit with the group's sums.
+__global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                            const double *cand, const int *ncand, const int *samples,
+                                                            Model *slots, int *valid) {
+    constexpr int K = 5, kRoots = 10, kPoses = 2;
+    const int lane = threadIdx.x % kTail;
+    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kTail);
+    const int k = gid / nlist, idx = gid - k * nlist;
+    if (k >= kRoots || k >= ncand[idx]) return; // the whole group leaves together
+    const int *s = samples + (size_t)list[idx] * kSampleStride;
+    const bool has = lane < K;
+    const int i = s[has ? lane : K - 1];
+    // one point of load_cal_sample: calibrated ray, unit bearings, depth priors
+    const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+    double a[3], c[3];
+    matvec3(C.K0i, xa, a);
+    matvec3(C.K1i, xb, c);
+    const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+    const double b1[1][3] = {{a[0] * na, a[1] * na, a[2] * na}}, b2[1][3] = {{c[0] * nc, c[1] * nc, c[2] * nc}};
+    const double p0[1][2] = {{a[0], a[1]}}, p1[1][2] = {{c[0], c[1]}};
+    const double dd0[1] = {D.d0[i]}, dd1[1] = {D.d1[i]};
+    const bool use[1] = {has};
+    Model poses[kPoses];
+    const int np = motion_from_essential_r<1>(
+        cand + (size_t)idx * kPtCandStride + 9 * k, b1, b2, use, kPoses,
+        [](bool ok) { return gsum8(ok ? 0 : 1) == 0; },
+        [&](const Model &m, int q) { // (static slots: poses[] stays in registers)
+            if (q == 0) poses[0] = m;
+            if (q == 1) poses[1] = m;
+        });
+    const bool shift = C.use_shift != 0 && !C.scale_only, mdc = C.min_depth_constraint != 0;
+#pragma unroll
+    for (int j = 0; j < kPoses; ++j) {
+        bool ok = false;
+        Model m;
+        if (j < np) { // (uniform over the group)
+            m = poses[j];
+            ok = point_model_tail_r<1>(p0, p1, dd0, dd1, use, (double)K, 1.0, 1.0, shift, mdc, C.min_depth, m,
+                                       [](double v) { return gsum8(v); });
+        }
+        if (lane == 0) {
+            const size_t q = (size_t)idx * kPtSlotStride + kPoses * k + j;
+            if (ok) slots[q] = m;
+            valid[q] = ok ? 1 : 0;
+        }
     }
 }
 

@@ -758,13 +758,15 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                                                                                       W.cand, W.ncand, kCandStride);
         else
             pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
-        // two-focal tail: one 8-lane group per (root, sample) (group_tail.h);
-        // MADPOSE_TAIL7_LANE=1 selects the one-lane kernel
-        static const bool lane7 = std::getenv("MADPOSE_TAIL7_LANE") != nullptr;
+        // calibrated / two-focal tails: one 8-lane group per (root, sample)
+        // (group_tail.h); MADPOSE_TAIL_LANE=1 selects the one-lane kernels
+        static const bool lane_tail = std::getenv("MADPOSE_TAIL_LANE") != nullptr;
         const long lanes = (long)nlist * PtTraits<v>::kRoots;
-        if (v == kTF && !lane7)
-            pt_tail7_group_kernel<<<(int)((lanes * kTail + 63) / 64), 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand,
-                                                                                 samples, W.slots, W.valid);
+        const int tgrid = (int)((lanes * kTail + 63) / 64);
+        if (v == kTF && !lane_tail)
+            pt_tail7_group_kernel<<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots, W.valid);
+        else if (v == kCal && !lane_tail)
+            pt_tail5_group_kernel<<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots, W.valid);
         else
             pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                       W.slots, W.valid);
