@@ -18,6 +18,16 @@
 
 namespace mp {
 
+// a[i] for a runtime i by selects (keeps a small array in registers; indexing it
+// with a runtime index would move it to scratch)
+template <int N> MP_HD double pick(const double (&a)[N], int i) {
+    double v = a[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k) v = (i == k) ? a[k] : v;
+    return v;
+}
+
+
 struct PairTerms {
     double A[3], B[3], dz0, dz1;
 };
@@ -150,8 +160,9 @@ template <int K, int KIND> MP_HD void md_polish(const PairTerms *T, double *z) {
 
 // solve_scale_and_shift (calibrated): x, y are 3 homogeneous calibrated rays.
 // sols[k] = (1, b1, a2, b2*a2); returns count (<= 4), ascending in b1.
-MP_HD int md_sols_cal(const double (&x)[3][3], const double (&y)[3][3], const double *dx, const double *dy,
-                      double (&sols)[4][6]) {
+template <class Emit>
+MP_HD int md_sols_cal_e(const double (&x)[3][3], const double (&y)[3][3], const double *dx, const double *dy,
+                        Emit &&emit) {
     PairTerms T[3];
     T[0] = pair_terms<false>(x[0], x[1], y[0], y[1], dx[0], dx[1], dy[0], dy[1]);
     T[1] = pair_terms<false>(x[0], x[2], y[0], y[2], dx[0], dx[2], dy[0], dy[2]);
@@ -177,19 +188,27 @@ MP_HD int md_sols_cal(const double (&x)[3][3], const double (&y)[3][3], const do
     const int nr = sturm_real_roots<4>(quart, roots);
     int n = 0;
     for (int r = 0; r < nr; ++r) {
-        const double b1 = roots[r];
+        const double b1 = pick(roots, r);
         const double s = peval<2>(l2, b1);
         double z[5] = {b1, peval<2>(l1, b1) / s, s, 1.0, 1.0};
         md_polish<3, 0>(T, z);
         if (!(z[2] > 0.0)) continue;
         const double a2 = sqrt(z[2]);
-        sols[n][0] = 1.0;
-        sols[n][1] = z[0];
-        sols[n][2] = a2;
-        sols[n][3] = z[1] * a2;
+        const double sol[6] = {1.0, z[0], a2, z[1] * a2, 1.0, 1.0};
+        emit(sol);
         ++n;
     }
     return n;
+}
+
+// solutions into sols[] (count <= 4)
+MP_HD int md_sols_cal(const double (&x)[3][3], const double (&y)[3][3], const double *dx, const double *dy,
+                      double (&sols)[4][6]) {
+    int n = 0;
+    return md_sols_cal_e(x, y, dx, dy, [&](const double (&sol)[6]) {
+        for (int c = 0; c < 6; ++c) sols[n][c] = sol[c];
+        ++n;
+    });
 }
 
 MP_HD double mean_abs_xy(const double (&x)[4][3]) {
@@ -200,8 +219,9 @@ MP_HD double mean_abs_xy(const double (&x)[4][3]) {
 }
 
 // solve_scale_and_shift_shared_focal: sols[k] = (1, b1, a2, b2*a2, f); count <= 8
-MP_HD int md_sols_sf(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
-                     double (&sols)[8][6]) {
+template <class Emit>
+MP_HD int md_sols_sf_e(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                       Emit &&emit) {
     const double f0 = 0.5 * (mean_abs_xy(x0) + mean_abs_xy(y0)); // src/solver.cpp:134-138
     double x[4][3], y[4][3];
 #pragma unroll
@@ -266,7 +286,7 @@ MP_HD int md_sols_sf(const double (&x0)[4][3], const double (&y0)[4][3], const d
     const int nr = sturm_real_roots<8>(R, roots);
     int n = 0;
     for (int r = 0; r < nr; ++r) {
-        const double w = roots[r];
+        const double w = pick(roots, r);
         const double s = -peval<4>(X, w) / peval<4>(Y, w);
         const double wb1 = peval<1>(q0[1], w) + s * peval<1>(q1[1], w);
         const double tb = peval<1>(q0[3], w) + s * peval<1>(q1[3], w);
@@ -275,19 +295,28 @@ MP_HD int md_sols_sf(const double (&x0)[4][3], const double (&y0)[4][3], const d
         if (z[3] < 0.0) continue; // src/solver.cpp:283
         if (!(z[2] > 0.0)) continue;
         const double a2 = sqrt(z[2]);
-        sols[n][0] = 1.0;
-        sols[n][1] = z[0];
-        sols[n][2] = a2;
-        sols[n][3] = z[1] * a2;
-        sols[n][4] = f0 / sqrt(z[3]);
+        const double f = f0 / sqrt(z[3]);
+        const double sol[6] = {1.0, z[0], a2, z[1] * a2, f, f};
+        emit(sol);
         ++n;
     }
     return n;
 }
 
+// solutions into sols[] (count <= 8)
+MP_HD int md_sols_sf(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                     double (&sols)[8][6]) {
+    int n = 0;
+    return md_sols_sf_e(x0, y0, dx, dy, [&](const double (&sol)[6]) {
+        for (int c = 0; c < 6; ++c) sols[n][c] = sol[c];
+        ++n;
+    });
+}
+
 // solve_scale_and_shift_two_focal: sols[k] = (1, b1, a2, b2*a2, f1, f2); count <= 4
-MP_HD int md_sols_tf(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
-                     double (&sols)[4][6]) {
+template <class Emit>
+MP_HD int md_sols_tf_e(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                       Emit &&emit) {
     const double f1 = mean_abs_xy(x0), f2 = mean_abs_xy(y0); // src/solver.cpp:302-305
     double x[4][3], y[4][3];
 #pragma unroll
@@ -348,7 +377,7 @@ MP_HD int md_sols_tf(const double (&x0)[4][3], const double (&y0)[4][3], const d
     const int nr = sturm_real_roots<4>(R, roots); // resultant has degree 4 here
     int n = 0;
     for (int r = 0; r < nr; ++r) {
-        const double w1 = roots[r];
+        const double w1 = pick(roots, r);
         const double t = -peval<4>(X, w1) / peval<4>(Y, w1);
         double m[5];
 #pragma unroll
@@ -359,15 +388,21 @@ MP_HD int md_sols_tf(const double (&x0)[4][3], const double (&y0)[4][3], const d
         if (z[3] < 0.0 || z[4] < 0.0) continue; // src/solver.cpp:470
         if (!(z[2] > 0.0)) continue;
         const double a2 = sqrt(z[2]);
-        sols[n][0] = 1.0;
-        sols[n][1] = z[0];
-        sols[n][2] = a2;
-        sols[n][3] = z[1] * a2;
-        sols[n][4] = f1 / sqrt(z[3]);
-        sols[n][5] = f2 / sqrt(z[4]);
+        const double sol[6] = {1.0, z[0], a2, z[1] * a2, f1 / sqrt(z[3]), f2 / sqrt(z[4])};
+        emit(sol);
         ++n;
     }
     return n;
+}
+
+// solutions into sols[] (count <= 4)
+MP_HD int md_sols_tf(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                     double (&sols)[4][6]) {
+    int n = 0;
+    return md_sols_tf_e(x0, y0, dx, dy, [&](const double (&sol)[6]) {
+        for (int c = 0; c < 6; ++c) sols[n][c] = sol[c];
+        ++n;
+    });
 }
 
 // Pose stage of solve_scale_shift_pose* (scale_on_x = false): positive corrected

@@ -58,17 +58,6 @@ __global__ void prep_pair_kernel(PairConst C, PairData D, double *r0, double *r1
     r1[i] = 1.0 / sqrt(dot3(b, b));
 }
 
-__device__ inline void write_models(const PairConst &C, const Model *out, int n, int b, int maxm, Model *models,
-                                    ScoreRec *recs, int *counts) {
-    for (int k = 0; k < n; ++k) {
-        models[(size_t)b * maxm + k] = out[k];
-        ScoreRec r;
-        prepare_score_rec(C, out[k], r);
-        recs[(size_t)b * maxm + k] = r;
-    }
-    counts[b] = n;
-}
-
 // estimator-level min-depth filter of the MD branch (src/hybrid_pose_estimator.cpp:80-85)
 __device__ inline bool md_accept(const PairConst &C, Model &m) {
     if (!C.min_depth_constraint || (m.offset0 > -C.min_depth[0] && m.offset1 > -C.min_depth[1] * m.scale)) {
@@ -78,7 +67,17 @@ __device__ inline bool md_accept(const PairConst &C, Model &m) {
     return false;
 }
 
-template <int V>
+__device__ inline void put_model(const PairConst &C, const Model &m, int b, int slot, int maxm, Model *models,
+                                 ScoreRec *recs) {
+    models[(size_t)b * maxm + slot] = m;
+    ScoreRec r;
+    prepare_score_rec(C, m, r);
+    recs[(size_t)b * maxm + slot] = r;
+}
+
+// ALT: instantiated with the option-gated alternate solvers (use_ours / use_4p4d);
+// the default instantiation leaves them out, and with them their scratch use.
+template <int V, bool ALT>
 __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                       const int *samples, Model *models, ScoreRec *recs, int *counts,
                                                       int maxm) {
@@ -86,8 +85,13 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
     if (idx >= nlist) return;
     const int b = list[idx];
     const int *s = samples + (size_t)b * kSampleStride;
-    Model out[8];
+    // accepted models go straight to their slots (no per-lane model array: indexing
+    // one with the running count would put it in scratch)
     int n = 0;
+    auto put = [&](const Model &m) {
+        if (n < maxm) put_model(C, m, b, n, maxm, models, recs);
+        ++n;
+    };
     if (V == kCal) {
         double x[3][3], y[3][3], dx[3], dy[3];
 #pragma unroll
@@ -106,25 +110,24 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
             m.focal0 = m.focal1 = 1.0;
             scale_and_pose<3>(x, y, W, m);
             m.scale = 1.0 / m.scale;
-            out[n++] = m;
+            put(m);
         } else if (!C.use_shift) {
             Model m;
             m.focal0 = m.focal1 = 1.0;
             md_pose_noshift_cal(x, y, dx, dy, m);
-            out[n++] = m;
-        } else if (C.md_alt == 1) {
+            put(m);
+        } else if (ALT && C.md_alt == 1) {
             Model tmp[4];
             const int ns = md_pose_cal_ours(x, y, dx, dy, tmp);
-            for (int k = 0; k < ns; ++k)
-                if (md_accept(C, tmp[k])) out[n++] = tmp[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < ns && md_accept(C, tmp[k])) put(tmp[k]);
         } else {
-            double sols[4][6];
-            const int ns = md_sols_cal(x, y, dx, dy, sols);
-            for (int k = 0; k < ns; ++k) {
+            md_sols_cal_e(x, y, dx, dy, [&](const double (&sol)[6]) {
                 Model m;
                 m.focal0 = m.focal1 = 1.0;
-                if (md_pose_from_sol<3>(x, y, dx, dy, sols[k], 1.0, 1.0, m) && md_accept(C, m)) out[n++] = m;
-            }
+                if (md_pose_from_sol<3>(x, y, dx, dy, sol, 1.0, 1.0, m) && md_accept(C, m)) put(m);
+            });
         }
     } else {
         double x[4][3], y[4][3], dx[4], dy[4];
@@ -140,39 +143,29 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
             dx[j] = D.d0[i];
             dy[j] = D.d1[i];
         }
-        if (C.md_alt != 0) {
+        if (ALT && C.md_alt != 0) {
             Model tmp[4];
             const int ns = (V == kSF) ? md_pose_sf_ours(x, y, dx, dy, tmp)
                                       : (C.md_alt == 1 ? md_pose_tf_ours(x, y, dx, dy, tmp)
                                                        : md_pose_tf_4p4d(x, y, dx, dy, tmp));
-            for (int k = 0; k < ns; ++k)
-                if (md_accept(C, tmp[k])) out[n++] = tmp[k];
-            write_models(C, out, n, b, maxm, models, recs, counts);
-            return;
-        }
-        double sols[8][6];
-        int ns;
-        if (V == kSF)
-            ns = md_sols_sf(x, y, dx, dy, sols);
-        else
-            ns = md_sols_tf(x, y, dx, dy, *reinterpret_cast<double(*)[4][6]>(&sols[0][0]));
-        for (int k = 0; k < ns; ++k) {
-            Model m;
-            const double fa = sols[k][4], fb = (V == kSF) ? sols[k][4] : sols[k][5];
-            m.focal0 = fa;
-            m.focal1 = fb;
-            if (md_pose_from_sol<4>(x, y, dx, dy, sols[k], fa, fb, m) && md_accept(C, m)) out[n++] = m;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < ns && md_accept(C, tmp[k])) put(tmp[k]);
+        } else {
+            auto pose = [&](const double (&sol)[6]) {
+                Model m;
+                const double fa = sol[4], fb = (V == kSF) ? sol[4] : sol[5];
+                m.focal0 = fa;
+                m.focal1 = fb;
+                if (md_pose_from_sol<4>(x, y, dx, dy, sol, fa, fb, m) && md_accept(C, m)) put(m);
+            };
+            if (V == kSF)
+                md_sols_sf_e(x, y, dx, dy, pose);
+            else
+                md_sols_tf_e(x, y, dx, dy, pose);
         }
     }
-    write_models(C, out, n, b, maxm, models, recs, counts);
-}
-
-__device__ inline void put_model(const PairConst &C, const Model &m, int b, int slot, int maxm, Model *models,
-                                 ScoreRec *recs) {
-    models[(size_t)b * maxm + slot] = m;
-    ScoreRec r;
-    prepare_score_rec(C, m, r);
-    recs[(size_t)b * maxm + slot] = r;
+    counts[b] = n < maxm ? n : maxm;
 }
 
 template <int K>
@@ -733,7 +726,12 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
     if (nlist <= 0) return hipSuccess;
     const int grid = (nlist + 63) / 64;
     return by_variant(C.variant, [&](auto V) {
-        md_solve_kernel<decltype(V)::value><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+        if (C.md_alt != 0)
+            md_solve_kernel<decltype(V)::value, true><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                          counts, maxm);
+        else
+            md_solve_kernel<decltype(V)::value, false><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                           counts, maxm);
         return hipGetLastError();
     });
 }
