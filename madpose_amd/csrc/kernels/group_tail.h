@@ -13,6 +13,7 @@
 // every lane.  Per value the operations are those of recover_pose_cv /
 // point_model_tail, except that the fit's sums run as a tree over the points.
 #pragma once
+#include "../include/mp_md.h"
 #include "../include/mp_pt67.h"
 #include "group_sturm.h"
 
@@ -130,6 +131,192 @@ __global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairCons
             const size_t q = (size_t)idx * kPtSlotStride + kPoses * k + j;
             if (ok) slots[q] = m;
             valid[q] = ok ? 1 : 0;
+        }
+    }
+}
+
+// Shared-focal tail (src/hybrid_pose_shared_focal_estimator.cpp:87-126, the per-root
+// part of sixpt_poses_for_root in mp_pt67.h) with one 16-lane group per (root,
+// sample): lane r < 10 holds row r of the pencil A(w) = M0 + w M1 + w^2 M2 at the root
+// w = 1 / u; the null vector of A comes from a group Gaussian elimination with
+// complete pivoting (pivot = group maximum over the remaining rows and columns; the
+// pivot rows go to LDS for the back substitution), the Gauss-Newton polish of
+// (x, y, w) sums the ten rows' normal equations over the group, and lane j < 6 holds
+// point j for motion_from_essential and the depth fit.
+struct Tail6Shared {
+    double U[kGrpPerWg][9][10]; // pivot rows
+    double z[kGrpPerWg][10];    // null vector (original column order)
+    int pc[kGrpPerWg][9];       // pivot columns
+};
+
+__device__ inline double gsum16(double v) {
+    v += dpp_d<dpp::kXor1>(v);
+    v += dpp_d<dpp::kXor2>(v);
+    v += dpp_d<dpp::kHalfMirror>(v);
+    return v + dpp_d<dpp::kMirror>(v);
+}
+__device__ inline int gsum16(int v) {
+    v += dpp_i<dpp::kXor1>(v);
+    v += dpp_i<dpp::kXor2>(v);
+    v += dpp_i<dpp::kHalfMirror>(v);
+    return v + dpp_i<dpp::kMirror>(v);
+}
+
+__global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                            const double *cand, const int *ncand, const int *samples,
+                                                            Model *slots, int *valid) {
+    constexpr int K = 6, kRoots = 15, kPoses = 2;
+    __shared__ Tail6Shared sh;
+    const int g = threadIdx.x / kGrp, r = threadIdx.x % kGrp;
+    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kGrp);
+    const int k = gid / nlist, idx = gid - k * nlist;
+    if (k >= kRoots || k >= ncand[idx]) return; // the whole group leaves together
+    const double *cd = cand + (size_t)idx * kPtCandStride;
+    const bool row_lane = r < 10;
+    double w = 1.0 / cd[27 + k];
+
+    // ---- row r of the pencil and of A(w) ----
+    double m0[10], m1[10], m2[10], a[10];
+    if (row_lane) {
+        sixpt_row([&](int e) { return Lin2{{cd[e], cd[9 + e], cd[18 + e]}}; }, r, m0, m1, m2);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 10; ++c) m0[c] = m1[c] = m2[c] = 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < 10; ++c) a[c] = m0[c] + w * (m1[c] + w * m2[c]);
+
+    // ---- null vector: complete pivoting over the group (null_vector10) ----
+    bool used = !row_lane, ok = true;
+    unsigned cols = 0; // eliminated columns
+#pragma unroll
+    for (int kk = 0; kk < 9; ++kk) {
+        double bv = -1.0;
+        int bc = 0;
+        if (!used) {
+#pragma unroll
+            for (int c = 0; c < 10; ++c)
+                if (!(cols >> c & 1u) && fabs(a[c]) > bv) {
+                    bv = fabs(a[c]);
+                    bc = c;
+                }
+        }
+        double vmax;
+        int key;
+        gargmax(bv, r * 16 + bc, &vmax, &key); // ties: lowest row, then lowest column
+        if (!(vmax > 0.0)) ok = false;
+        const int prow = key / 16, pcol = key % 16;
+        if (r == prow) {
+#pragma unroll
+            for (int c = 0; c < 10; ++c) sh.U[g][kk][c] = a[c];
+            sh.pc[g][kk] = pcol;
+            used = true;
+        }
+        __syncthreads();
+        if (!used) {
+            const double l = pick(a, pcol) / sh.U[g][kk][pcol];
+#pragma unroll
+            for (int c = 0; c < 10; ++c)
+                if (!(cols >> c & 1u) && c != pcol) a[c] -= l * sh.U[g][kk][c];
+        }
+        cols |= 1u << pcol;
+        __syncthreads();
+    }
+    if (!ok) return; // (uniform)
+    // back substitution (lane 0): free column = the one never pivoted, z = 1 there
+    if (r == 0) {
+        const int fc = __ffs(~cols & 0x3ffu) - 1;
+        for (int c = 0; c < 10; ++c) sh.z[g][c] = 0.0;
+        sh.z[g][fc] = 1.0;
+        for (int kk = 8; kk >= 0; --kk) {
+            double s = 0.0;
+            for (int q = kk + 1; q < 9; ++q) s += sh.U[g][kk][sh.pc[g][q]] * sh.z[g][sh.pc[g][q]];
+            s += sh.U[g][kk][fc] * sh.z[g][fc];
+            sh.z[g][sh.pc[g][kk]] = -s / sh.U[g][kk][sh.pc[g][kk]];
+        }
+    }
+    __syncthreads();
+    const double v9 = sh.z[g][9];
+    if (v9 == 0.0) return; // (uniform)
+    double x = sh.z[g][7] / v9, y = sh.z[g][8] / v9;
+
+    // ---- Gauss-Newton polish of (x, y, w), rows summed over the group ----
+    for (int it = 0; it < 5; ++it) {
+        double mv[10], dxv[10], dyv[10];
+        mono2(x, y, mv, dxv, dyv);
+        double res = 0, jx = 0, jy = 0, jw = 0;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            const double m = m0[c] + w * (m1[c] + w * m2[c]);
+            res += m * mv[c];
+            jx += m * dxv[c];
+            jy += m * dyv[c];
+            jw += (m1[c] + 2.0 * w * m2[c]) * mv[c];
+        }
+        const double J[3] = {jx, jy, jw};
+        double JtJ[3][3], Jtr[3][1];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            Jtr[p][0] = gsum16(J[p] * res);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) JtJ[p][q] = q < p ? JtJ[q][p] : gsum16(J[p] * J[q]);
+        }
+        if (!gauss_solve<3, 1>(JtJ, Jtr)) break;
+        x -= Jtr[0][0];
+        y -= Jtr[1][0];
+        w -= Jtr[2][0];
+    }
+    if (!(w > 0.0)) return;
+    const double foc = 1.0 / sqrt(w);
+    double Fm[9], nn = 0.0;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        Fm[e] = x * cd[e] + y * cd[9 + e] + cd[18 + e];
+        nn += Fm[e] * Fm[e];
+    }
+    nn = 1.0 / sqrt(nn);
+    double E[9];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) E[3 * p + q] = Fm[3 * p + q] * nn * (p < 2 ? foc : 1.0) * (q < 2 ? foc : 1.0);
+
+    // ---- poses and depth tail, point j = lane j (< 6) ----
+    const int *s = samples + (size_t)list[idx] * kSampleStride;
+    const bool has = r < K;
+    const int i = s[has ? r : K - 1];
+    const double pa[3] = {D.x0u[i], D.x0v[i], 1.0}, pb[3] = {D.x1u[i], D.x1v[i], 1.0};
+    const double ia = 1.0 / sqrt(dot3(pa, pa)), ib = 1.0 / sqrt(dot3(pb, pb));
+    // the bearing's xy divided by the focal, re-normalised (sixpt_poses_for_root)
+    const double ba[3] = {pa[0] * ia / foc, pa[1] * ia / foc, pa[2] * ia},
+                 bb[3] = {pb[0] * ib / foc, pb[1] * ib / foc, pb[2] * ib};
+    const double na = 1.0 / sqrt(dot3(ba, ba)), nb = 1.0 / sqrt(dot3(bb, bb));
+    const double c1[1][3] = {{ba[0] * na, ba[1] * na, ba[2] * na}}, c2[1][3] = {{bb[0] * nb, bb[1] * nb, bb[2] * nb}};
+    const double p0[1][2] = {{pa[0], pa[1]}}, p1[1][2] = {{pb[0], pb[1]}};
+    const double dd0[1] = {D.d0[i]}, dd1[1] = {D.d1[i]};
+    const bool use[1] = {has};
+    Model poses[kPoses];
+    const int np = motion_from_essential_r<1>(
+        E, c1, c2, use, kPoses, [](bool okp) { return gsum16(okp ? 0 : 1) == 0; },
+        [&](const Model &m, int q) {
+            if (q == 0) poses[0] = m;
+            if (q == 1) poses[1] = m;
+        });
+    const bool shift = C.use_shift != 0 && !C.scale_only, mdc = C.min_depth_constraint != 0;
+#pragma unroll
+    for (int j = 0; j < kPoses; ++j) {
+        bool okm = false;
+        Model m;
+        if (j < np) { // (uniform over the group)
+            m = poses[j];
+            m.focal0 = m.focal1 = foc;
+            okm = point_model_tail_r<1>(p0, p1, dd0, dd1, use, (double)K, foc, foc, shift, mdc, C.min_depth, m,
+                                        [](double v) { return gsum16(v); });
+        }
+        if (r == 0) {
+            const size_t q = (size_t)idx * kPtSlotStride + kPoses * k + j;
+            if (okm) slots[q] = m;
+            valid[q] = okm ? 1 : 0;
         }
     }
 }

@@ -756,8 +756,8 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                                                                                       W.cand, W.ncand, kCandStride);
         else
             pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
-        // calibrated / two-focal tails: one 8-lane group per (root, sample)
-        // (group_tail.h); MADPOSE_TAIL_LANE=1 selects the one-lane kernels
+        // point-solver tails on lane groups per (root, sample) (group_tail.h: 8 lanes
+        // for cal / tf, 16 for sf); MADPOSE_TAIL_LANE=1 selects the one-lane kernels
         static const bool lane_tail = std::getenv("MADPOSE_TAIL_LANE") != nullptr;
         const long lanes = (long)nlist * PtTraits<v>::kRoots;
         const int tgrid = (int)((lanes * kTail + 63) / 64);
@@ -765,6 +765,9 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
             pt_tail7_group_kernel<<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots, W.valid);
         else if (v == kCal && !lane_tail)
             pt_tail5_group_kernel<<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots, W.valid);
+        else if (v == kSF && !lane_tail)
+            pt_tail6_group_kernel<<<(int)((lanes * kGrp + 63) / 64), 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand,
+                                                                                samples, W.slots, W.valid);
         else
             pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                       W.slots, W.valid);
