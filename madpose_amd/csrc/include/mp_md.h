@@ -158,12 +158,18 @@ template <int K, int KIND> MP_HD void md_polish(const PairTerms *T, double *z) {
     for (int i = 0; i < 5; ++i) z[i] = best[i];
 }
 
-// solve_scale_and_shift (calibrated): x, y are 3 homogeneous calibrated rays.
-// sols[k] = (1, b1, a2, b2*a2); returns count (<= 4), ascending in b1.
-template <class Emit>
-MP_HD int md_sols_cal_e(const double (&x)[3][3], const double (&y)[3][3], const double *dx, const double *dy,
-                        Emit &&emit) {
+// The solvers in two parts: md_setup_* builds the per-sample system and its
+// univariate polynomial (degree 4 / 8 / 4), md_root_* turns one real root into a
+// solution (sol = (1, b1, a2, b2*a2, f0, f1)), false if rejected.  md_sols_*_e runs
+// both in one lane; the group kernel (group_md.h) runs one root per lane.
+struct MdCal {
     PairTerms T[3];
+    double l1[3], l2[3];
+    double poly[5];
+};
+MP_HD bool md_setup_cal(const double (&x)[3][3], const double (&y)[3][3], const double *dx, const double *dy,
+                        MdCal &S) {
+    PairTerms *T = S.T;
     T[0] = pair_terms<false>(x[0], x[1], y[0], y[1], dx[0], dx[1], dy[0], dy[1]);
     T[1] = pair_terms<false>(x[0], x[2], y[0], y[2], dx[0], dx[2], dy[0], dy[2]);
     T[2] = pair_terms<false>(x[1], x[2], y[1], y[2], dx[1], dx[2], dy[1], dy[2]);
@@ -175,26 +181,48 @@ MP_HD int md_sols_cal_e(const double (&x)[3][3], const double (&y)[3][3], const 
             Q[k][c] = T[k].B[c];
             L[k][c] = T[k].A[c];
         }
-    if (!gauss_solve<3, 3>(Q, L)) return 0;
+    if (!gauss_solve<3, 3>(Q, L)) return false;
     // (s beta)^2 = (s beta^2) s, each monomial linear in (b1^2, b1, 1)
-    const double l0[3] = {L[0][2], L[0][1], L[0][0]}, l1[3] = {L[1][2], L[1][1], L[1][0]},
-                 l2[3] = {L[2][2], L[2][1], L[2][0]};
-    double a[5], b[5], quart[5];
-    pmul<2, 2>(l1, l1, a);
-    pmul<2, 2>(l0, l2, b);
+    const double l0[3] = {L[0][2], L[0][1], L[0][0]};
 #pragma unroll
-    for (int k = 0; k < 5; ++k) quart[k] = a[k] - b[k];
+    for (int c = 0; c < 3; ++c) {
+        S.l1[c] = L[1][2 - c];
+        S.l2[c] = L[2][2 - c];
+    }
+    double a[5], b[5];
+    pmul<2, 2>(S.l1, S.l1, a);
+    pmul<2, 2>(l0, S.l2, b);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) S.poly[k] = a[k] - b[k];
+    return true;
+}
+MP_HD bool md_root_cal(const MdCal &S, double b1, double (&sol)[6]) {
+    const double s = peval<2>(S.l2, b1);
+    double z[5] = {b1, peval<2>(S.l1, b1) / s, s, 1.0, 1.0};
+    md_polish<3, 0>(S.T, z);
+    if (!(z[2] > 0.0)) return false;
+    const double a2 = sqrt(z[2]);
+    sol[0] = 1.0;
+    sol[1] = z[0];
+    sol[2] = a2;
+    sol[3] = z[1] * a2;
+    sol[4] = sol[5] = 1.0;
+    return true;
+}
+
+// solve_scale_and_shift (calibrated): x, y are 3 homogeneous calibrated rays.
+// Solutions ascending in b1; returns their count (<= 4).
+template <class Emit>
+MP_HD int md_sols_cal_e(const double (&x)[3][3], const double (&y)[3][3], const double *dx, const double *dy,
+                        Emit &&emit) {
+    MdCal S;
+    if (!md_setup_cal(x, y, dx, dy, S)) return 0;
     double roots[4];
-    const int nr = sturm_real_roots<4>(quart, roots);
+    const int nr = sturm_real_roots<4>(S.poly, roots);
     int n = 0;
     for (int r = 0; r < nr; ++r) {
-        const double b1 = pick(roots, r);
-        const double s = peval<2>(l2, b1);
-        double z[5] = {b1, peval<2>(l1, b1) / s, s, 1.0, 1.0};
-        md_polish<3, 0>(T, z);
-        if (!(z[2] > 0.0)) continue;
-        const double a2 = sqrt(z[2]);
-        const double sol[6] = {1.0, z[0], a2, z[1] * a2, 1.0, 1.0};
+        double sol[6];
+        if (!md_root_cal(S, pick(roots, r), sol)) continue;
         emit(sol);
         ++n;
     }
@@ -218,11 +246,17 @@ MP_HD double mean_abs_xy(const double (&x)[4][3]) {
     return s / 8.0;
 }
 
-// solve_scale_and_shift_shared_focal: sols[k] = (1, b1, a2, b2*a2, f); count <= 8
-template <class Emit>
-MP_HD int md_sols_sf_e(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
-                       Emit &&emit) {
+// solve_scale_and_shift_shared_focal: sol = (1, b1, a2, b2*a2, f, f); count <= 8
+struct MdSF {
+    PairTerms T[4];
+    double q0[4][2], q1[4][2];
+    double X[5], Y[5], R[9];
+    double f0;
+};
+MP_HD bool md_setup_sf(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                       MdSF &S) {
     const double f0 = 0.5 * (mean_abs_xy(x0) + mean_abs_xy(y0)); // src/solver.cpp:134-138
+    S.f0 = f0;
     double x[4][3], y[4][3];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -234,7 +268,7 @@ MP_HD int md_sols_sf_e(const double (&x0)[4][3], const double (&y0)[4][3], const
         y[i][2] = y0[i][2];
     }
     const int pr[4][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}};
-    PairTerms T[4];
+    PairTerms *T = S.T;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         T[k] = pair_terms<true>(x[pr[k][0]], x[pr[k][1]], y[pr[k][0]], y[pr[k][1]], dx[pr[k][0]], dx[pr[k][1]],
@@ -251,52 +285,65 @@ MP_HD int md_sols_sf_e(const double (&x0)[4][3], const double (&y0)[4][3], const
         L[k][2] = T[k].dz1;
         L[k][3] = -T[k].dz0;
     }
-    if (!gauss_solve<4, 4>(M, L)) return 0;
+    if (!gauss_solve<4, 4>(M, L)) return false;
     // monomial_r = q0_r(w) + s q1_r(w)   (t = s w substituted)
-    double q0[4][2], q1[4][2];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        q0[r][0] = L[r][3];
-        q0[r][1] = L[r][0];
-        q1[r][0] = L[r][2];
-        q1[r][1] = L[r][1];
+        S.q0[r][0] = L[r][3];
+        S.q0[r][1] = L[r][0];
+        S.q1[r][0] = L[r][2];
+        S.q1[r][1] = L[r][1];
     }
     double al0[3], al1[3], al2[3], be0[3], be1[3], be2[3], t0[3], t1[3];
-    pmul<1, 1>(q0[1], q0[1], t0);
+    pmul<1, 1>(S.q0[1], S.q0[1], t0);
     al0[0] = t0[0];
-    al0[1] = t0[1] - q0[0][0];
-    al0[2] = t0[2] - q0[0][1];
-    pmul<1, 1>(q0[1], q1[1], t0);
+    al0[1] = t0[1] - S.q0[0][0];
+    al0[2] = t0[2] - S.q0[0][1];
+    pmul<1, 1>(S.q0[1], S.q1[1], t0);
     al1[0] = 2 * t0[0];
-    al1[1] = 2 * t0[1] - q1[0][0];
-    al1[2] = 2 * t0[2] - q1[0][1];
-    pmul<1, 1>(q1[1], q1[1], al2);
-    pmul<1, 1>(q0[3], q0[3], be0);
-    pmul<1, 1>(q0[3], q1[3], t0);
+    al1[1] = 2 * t0[1] - S.q1[0][0];
+    al1[2] = 2 * t0[2] - S.q1[0][1];
+    pmul<1, 1>(S.q1[1], S.q1[1], al2);
+    pmul<1, 1>(S.q0[3], S.q0[3], be0);
+    pmul<1, 1>(S.q0[3], S.q1[3], t0);
     be1[0] = 2 * t0[0];
-    be1[1] = 2 * t0[1] - q0[2][0];
-    be1[2] = 2 * t0[2] - q0[2][1];
-    pmul<1, 1>(q1[3], q1[3], t1);
+    be1[1] = 2 * t0[1] - S.q0[2][0];
+    be1[2] = 2 * t0[2] - S.q0[2][1];
+    pmul<1, 1>(S.q1[3], S.q1[3], t1);
     be2[0] = t1[0];
-    be2[1] = t1[1] - q1[2][0];
-    be2[2] = t1[2] - q1[2][1];
-    double X[5], Y[5], R[9];
-    quad_resultant(al0, al1, al2, be0, be1, be2, X, Y, R);
+    be2[1] = t1[1] - S.q1[2][0];
+    be2[2] = t1[2] - S.q1[2][1];
+    quad_resultant(al0, al1, al2, be0, be1, be2, S.X, S.Y, S.R);
+    return true;
+}
+MP_HD bool md_root_sf(const MdSF &S, double w, double (&sol)[6]) {
+    const double s = -peval<4>(S.X, w) / peval<4>(S.Y, w);
+    const double wb1 = peval<1>(S.q0[1], w) + s * peval<1>(S.q1[1], w);
+    const double tb = peval<1>(S.q0[3], w) + s * peval<1>(S.q1[3], w);
+    double z[5] = {wb1 / w, tb / (s * w), s, w, w};
+    md_polish<4, 1>(S.T, z);
+    if (z[3] < 0.0) return false; // src/solver.cpp:283
+    if (!(z[2] > 0.0)) return false;
+    const double a2 = sqrt(z[2]);
+    const double f = S.f0 / sqrt(z[3]);
+    sol[0] = 1.0;
+    sol[1] = z[0];
+    sol[2] = a2;
+    sol[3] = z[1] * a2;
+    sol[4] = sol[5] = f;
+    return true;
+}
+template <class Emit>
+MP_HD int md_sols_sf_e(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                       Emit &&emit) {
+    MdSF S;
+    if (!md_setup_sf(x0, y0, dx, dy, S)) return 0;
     double roots[8];
-    const int nr = sturm_real_roots<8>(R, roots);
+    const int nr = sturm_real_roots<8>(S.R, roots);
     int n = 0;
     for (int r = 0; r < nr; ++r) {
-        const double w = pick(roots, r);
-        const double s = -peval<4>(X, w) / peval<4>(Y, w);
-        const double wb1 = peval<1>(q0[1], w) + s * peval<1>(q1[1], w);
-        const double tb = peval<1>(q0[3], w) + s * peval<1>(q1[3], w);
-        double z[5] = {wb1 / w, tb / (s * w), s, w, w};
-        md_polish<4, 1>(T, z);
-        if (z[3] < 0.0) continue; // src/solver.cpp:283
-        if (!(z[2] > 0.0)) continue;
-        const double a2 = sqrt(z[2]);
-        const double f = f0 / sqrt(z[3]);
-        const double sol[6] = {1.0, z[0], a2, z[1] * a2, f, f};
+        double sol[6];
+        if (!md_root_sf(S, pick(roots, r), sol)) continue;
         emit(sol);
         ++n;
     }
@@ -313,11 +360,18 @@ MP_HD int md_sols_sf(const double (&x0)[4][3], const double (&y0)[4][3], const d
     });
 }
 
-// solve_scale_and_shift_two_focal: sols[k] = (1, b1, a2, b2*a2, f1, f2); count <= 4
-template <class Emit>
-MP_HD int md_sols_tf_e(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
-                       Emit &&emit) {
+// solve_scale_and_shift_two_focal: sol = (1, b1, a2, b2*a2, f1, f2); count <= 4
+struct MdTF {
+    PairTerms T[5];
+    double q0[5][2], q1[5];
+    double X[5], Y[5], R[9]; // (R has degree 4 here)
+    double f1, f2;
+};
+MP_HD bool md_setup_tf(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                       MdTF &S) {
     const double f1 = mean_abs_xy(x0), f2 = mean_abs_xy(y0); // src/solver.cpp:302-305
+    S.f1 = f1;
+    S.f2 = f2;
     double x[4][3], y[4][3];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -329,7 +383,7 @@ MP_HD int md_sols_tf_e(const double (&x0)[4][3], const double (&y0)[4][3], const
         y[i][2] = y0[i][2];
     }
     const int pr[5][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}, {1, 3}};
-    PairTerms T[5];
+    PairTerms *T = S.T;
 #pragma unroll
     for (int k = 0; k < 5; ++k)
         T[k] = pair_terms<true>(x[pr[k][0]], x[pr[k][1]], y[pr[k][0]], y[pr[k][1]], dx[pr[k][0]], dx[pr[k][1]],
@@ -346,49 +400,63 @@ MP_HD int md_sols_tf_e(const double (&x0)[4][3], const double (&y0)[4][3], const
         L[k][1] = T[k].B[2];
         L[k][2] = -T[k].dz0;
     }
-    if (!gauss_solve<5, 3>(M, L)) return 0;
+    if (!gauss_solve<5, 3>(M, L)) return false;
     // monomial_r = q0_r(w1) + t q1_r   (q1 constant)
-    double q0[5][2], q1[5];
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
-        q0[r][0] = L[r][2];
-        q0[r][1] = L[r][0];
-        q1[r] = L[r][1];
+        S.q0[r][0] = L[r][2];
+        S.q0[r][1] = L[r][0];
+        S.q1[r] = L[r][1];
     }
     double al0[3], al1[3], al2[3], be0[3], be1[3], be2[3], t0[3];
-    pmul<1, 1>(q0[1], q0[1], t0);
+    pmul<1, 1>(S.q0[1], S.q0[1], t0);
     al0[0] = t0[0];
-    al0[1] = t0[1] - q0[0][0];
-    al0[2] = t0[2] - q0[0][1];
-    al1[0] = 2 * q0[1][0] * q1[1];
-    al1[1] = 2 * q0[1][1] * q1[1] - q1[0];
+    al0[1] = t0[1] - S.q0[0][0];
+    al0[2] = t0[2] - S.q0[0][1];
+    al1[0] = 2 * S.q0[1][0] * S.q1[1];
+    al1[1] = 2 * S.q0[1][1] * S.q1[1] - S.q1[0];
     al1[2] = 0.0;
-    al2[0] = q1[1] * q1[1];
+    al2[0] = S.q1[1] * S.q1[1];
     al2[1] = al2[2] = 0.0;
-    pmul<1, 1>(q0[3], q0[3], be0);
-    be1[0] = 2 * q0[3][0] * q1[3] - q0[2][0];
-    be1[1] = 2 * q0[3][1] * q1[3] - q0[2][1];
+    pmul<1, 1>(S.q0[3], S.q0[3], be0);
+    be1[0] = 2 * S.q0[3][0] * S.q1[3] - S.q0[2][0];
+    be1[1] = 2 * S.q0[3][1] * S.q1[3] - S.q0[2][1];
     be1[2] = 0.0;
-    be2[0] = q1[3] * q1[3] - q1[2];
+    be2[0] = S.q1[3] * S.q1[3] - S.q1[2];
     be2[1] = be2[2] = 0.0;
-    double X[5], Y[5], R[9];
-    quad_resultant(al0, al1, al2, be0, be1, be2, X, Y, R);
+    quad_resultant(al0, al1, al2, be0, be1, be2, S.X, S.Y, S.R);
+    return true;
+}
+MP_HD bool md_root_tf(const MdTF &S, double w1, double (&sol)[6]) {
+    const double t = -peval<4>(S.X, w1) / peval<4>(S.Y, w1);
+    double m[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) m[k] = peval<1>(S.q0[k], w1) + t * S.q1[k];
+    const double s = m[4];
+    double z[5] = {m[1] / w1, m[3] / t, s, w1, t / s};
+    md_polish<5, 2>(S.T, z);
+    if (z[3] < 0.0 || z[4] < 0.0) return false; // src/solver.cpp:470
+    if (!(z[2] > 0.0)) return false;
+    const double a2 = sqrt(z[2]);
+    sol[0] = 1.0;
+    sol[1] = z[0];
+    sol[2] = a2;
+    sol[3] = z[1] * a2;
+    sol[4] = S.f1 / sqrt(z[3]);
+    sol[5] = S.f2 / sqrt(z[4]);
+    return true;
+}
+template <class Emit>
+MP_HD int md_sols_tf_e(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                       Emit &&emit) {
+    MdTF S;
+    if (!md_setup_tf(x0, y0, dx, dy, S)) return 0;
     double roots[4];
-    const int nr = sturm_real_roots<4>(R, roots); // resultant has degree 4 here
+    const int nr = sturm_real_roots<4>(S.R, roots); // resultant has degree 4 here
     int n = 0;
     for (int r = 0; r < nr; ++r) {
-        const double w1 = pick(roots, r);
-        const double t = -peval<4>(X, w1) / peval<4>(Y, w1);
-        double m[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) m[k] = peval<1>(q0[k], w1) + t * q1[k];
-        const double s = m[4];
-        double z[5] = {m[1] / w1, m[3] / t, s, w1, t / s};
-        md_polish<5, 2>(T, z);
-        if (z[3] < 0.0 || z[4] < 0.0) continue; // src/solver.cpp:470
-        if (!(z[2] > 0.0)) continue;
-        const double a2 = sqrt(z[2]);
-        const double sol[6] = {1.0, z[0], a2, z[1] * a2, f1 / sqrt(z[3]), f2 / sqrt(z[4])};
+        double sol[6];
+        if (!md_root_tf(S, pick(roots, r), sol)) continue;
         emit(sol);
         ++n;
     }

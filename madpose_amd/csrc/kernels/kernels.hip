@@ -168,6 +168,99 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
     counts[b] = n < maxm ? n : maxm;
 }
 
+// The default MD solvers (shift on, no alternates) on 16-lane groups, 4 samples per
+// wave: every lane builds the sample's system (md_setup_*), the resultant's real roots
+// are isolated over the group (group_sturm_roots), and each root is polished, turned
+// into a pose and filtered on its own lane; accepted models are compacted in root
+// order with a group scan, so slots and counts equal md_solve_kernel's.
+template <int V> struct MdGroup;
+template <> struct MdGroup<kCal> {
+    static constexpr int NR = 4, K = 3;
+    using Sys = MdCal;
+};
+template <> struct MdGroup<kSF> {
+    static constexpr int NR = 8, K = 4;
+    using Sys = MdSF;
+};
+template <> struct MdGroup<kTF> {
+    static constexpr int NR = 4, K = 4;
+    using Sys = MdTF;
+};
+
+template <int V>
+__global__ void __launch_bounds__(64) md_solve_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                            const int *samples, Model *models, ScoreRec *recs,
+                                                            int *counts, int maxm) {
+    using G = MdGroup<V>;
+    constexpr int NR = G::NR, K = G::K;
+    __shared__ GroupSturm<NR> st[kGrpPerWg];
+    const int g = threadIdx.x / kGrp, r = threadIdx.x % kGrp;
+    const int idx = blockIdx.x * kGrpPerWg + g;
+    const bool active = idx < nlist;
+    const int b = list[active ? idx : nlist - 1];
+    const int *s = samples + (size_t)b * kSampleStride;
+    double x[K][3], y[K][3], dx[K], dy[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const int i = s[j];
+        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+        if (V == kCal) {
+            matvec3(C.K0i, xa, x[j]);
+            matvec3(C.K1i, xb, y[j]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                x[j][q] = xa[q];
+                y[j][q] = xb[q];
+            }
+        }
+        dx[j] = D.d0[i];
+        dy[j] = D.d1[i];
+    }
+    typename G::Sys S;
+    bool ok;
+    double p[NR + 1];
+    if constexpr (V == kCal) {
+        ok = md_setup_cal(x, y, dx, dy, S);
+#pragma unroll
+        for (int k = 0; k <= NR; ++k) p[k] = S.poly[k];
+    } else if constexpr (V == kSF) {
+        ok = md_setup_sf(x, y, dx, dy, S);
+#pragma unroll
+        for (int k = 0; k <= NR; ++k) p[k] = S.R[k];
+    } else {
+        ok = md_setup_tf(x, y, dx, dy, S);
+#pragma unroll
+        for (int k = 0; k <= NR; ++k) p[k] = S.R[k];
+    }
+    double root = 0.0;
+    const bool has = group_sturm_roots<NR>(p, r, st[g], ok, &root);
+    bool keep = false;
+    Model m;
+    if (has) {
+        double sol[6];
+        bool good;
+        if constexpr (V == kCal)
+            good = md_root_cal(S, root, sol);
+        else if constexpr (V == kSF)
+            good = md_root_sf(S, root, sol);
+        else
+            good = md_root_tf(S, root, sol);
+        if (good) {
+            const double fa = sol[4], fb = sol[5];
+            m.focal0 = fa;
+            m.focal1 = fb;
+            keep = md_pose_from_sol<K>(x, y, dx, dy, sol, fa, fb, m) && md_accept(C, m);
+        }
+    }
+    int total;
+    const int pos = gscan(keep ? 1 : 0, &total);
+    if (active) {
+        if (keep && pos < maxm) put_model(C, m, b, pos, maxm, models, recs);
+        if (r == 0) counts[b] = total < maxm ? total : maxm;
+    }
+}
+
 template <int K>
 __device__ inline void load_uncal_sample(const PairData &D, const int *s, double (&b0)[K][3], double (&b1)[K][3],
                                          double (&p0)[K][2], double (&p1)[K][2], double (&dd0)[K], double (&dd1)[K]) {
@@ -726,6 +819,15 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
     if (nlist <= 0) return hipSuccess;
     const int grid = (nlist + 63) / 64;
     return by_variant(C.variant, [&](auto V) {
+        constexpr int v = decltype(V)::value;
+        // default solvers on 16-lane groups (MADPOSE_MD_LANE: one sample per lane)
+        static const bool lane_md = std::getenv("MADPOSE_MD_LANE") != nullptr;
+        const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
+        if (plain && !lane_md) {
+            md_solve_group_kernel<v><<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, C, list, nlist, samples,
+                                                                                     models, recs, counts, maxm);
+            return hipGetLastError();
+        }
         if (C.md_alt != 0)
             md_solve_kernel<decltype(V)::value, true><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
                                                                           counts, maxm);
