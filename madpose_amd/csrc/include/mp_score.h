@@ -78,16 +78,65 @@ MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r) {
     r.pad = 0.0;
 }
 
+// One correspondence as the sweeps read it.  For the calibrated estimator the
+// model-independent rays are formed once per correspondence (corr_rays), outside the
+// loops over models: a = K0^-1 x0, b = K1^-1 x1 (xy; the Sampson terms) and the unit
+// bearings n0, n1 (the cheirality test).
 struct Corr {
     double x0u, x0v, x1u, x1v, d0, d1, r0, r1;
+    double a0, a1, b0, b1, n0[3], n1[3];
 };
+
+MP_HD void corr_rays(const PairConst &C, Corr &p) {
+    const double *Ki = C.K0i, *Kj = C.K1i;
+    const double a0 = Ki[0] * p.x0u + Ki[1] * p.x0v + Ki[2];
+    const double a1 = Ki[3] * p.x0u + Ki[4] * p.x0v + Ki[5];
+    const double a2 = Ki[6] * p.x0u + Ki[7] * p.x0v + Ki[8];
+    const double b0 = Kj[0] * p.x1u + Kj[1] * p.x1v + Kj[2];
+    const double b1 = Kj[3] * p.x1u + Kj[4] * p.x1v + Kj[5];
+    const double b2 = Kj[6] * p.x1u + Kj[7] * p.x1v + Kj[8];
+    p.a0 = a0;
+    p.a1 = a1;
+    p.b0 = b0;
+    p.b1 = b1;
+    p.n0[0] = a0 * p.r0;
+    p.n0[1] = a1 * p.r0;
+    p.n0[2] = a2 * p.r0;
+    p.n1[0] = b0 * p.r1;
+    p.n1[1] = b1 * p.r1;
+    p.n1[2] = b2 * p.r1;
+}
+
+// Reciprocals of the sweeps.  On the device, the hardware reciprocal refined by two
+// Newton steps (within about an ulp of the correctly rounded quotient; 5 FP64
+// instructions instead of the 11 of the IEEE division sequence) where x is finite and
+// normal; the IEEE results elsewhere (1/inf = 0, NaN stays NaN, 1/0 and denormal x by
+// division).
+MP_HD double rcp_newton(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
+// x >= 1e-2 or NaN (the reprojection depth after its z test)
+MP_HD double rcp_depth(double x) { return (x > DBL_MAX) ? 0.0 : rcp_newton(x); }
+// q / x for x >= 0 (the Sampson denominator)
+MP_HD double div_nonneg(double q, double x) {
+    if (__builtin_expect(x >= DBL_MIN && x <= DBL_MAX, 1)) return q * rcp_newton(x);
+    return q / x;
+}
 
 MP_HD double reproj_err(const double *M, const double *k, double u, double v, double a, double tu, double tv) {
     const double px = (M[0] * u + M[1] * v + M[2]) * a + k[0];
     const double py = (M[3] * u + M[4] * v + M[5]) * a + k[1];
     const double pz = (M[6] * u + M[7] * v + M[8]) * a + k[2];
     if (pz < 1e-2) return DBL_MAX;
-    const double iz = 1.0 / pz;
+    const double iz = rcp_depth(pz);
     const double ex = px * iz - tu, ey = py * iz - tv;
     return ex * ex + ey * ey;
 }
@@ -99,7 +148,7 @@ MP_HD double sampson_err(const double *G, double au, double av, double bu, doubl
     const double f0 = G[0] * bu + G[3] * bv + G[6];
     const double f1 = G[1] * bu + G[4] * bv + G[7];
     const double c = bu * e0 + bv * e1 + e2;
-    return c * c / (e0 * e0 + e1 * e1 + f0 * f0 + f1 * f1);
+    return div_nonneg(c * c, e0 * e0 + e1 * e1 + f0 * f0 + f1 * f1);
 }
 
 // Squared errors of the three data types for one correspondence.
@@ -120,20 +169,12 @@ MP_HD void eval_corr(const PairConst &C, const ScoreRec &r, const Corr &p, bool 
         return;
     }
     if (V == kCal) {
-        // calibrated rays and unit bearings
-        const double *Ki = C.K0i, *Kj = C.K1i;
-        const double a0 = Ki[0] * p.x0u + Ki[1] * p.x0v + Ki[2];
-        const double a1 = Ki[3] * p.x0u + Ki[4] * p.x0v + Ki[5];
-        const double a2 = Ki[6] * p.x0u + Ki[7] * p.x0v + Ki[8];
-        const double b0 = Kj[0] * p.x1u + Kj[1] * p.x1v + Kj[2];
-        const double b1 = Kj[3] * p.x1u + Kj[4] * p.x1v + Kj[5];
-        const double b2 = Kj[6] * p.x1u + Kj[7] * p.x1v + Kj[8];
-        const double n0[3] = {a0 * p.r0, a1 * p.r0, a2 * p.r0}, n1[3] = {b0 * p.r1, b1 * p.r1, b2 * p.r1};
-        if (!check_cheirality(r.R, r.t, n0, n1, 1e-2)) {
+        // calibrated rays and unit bearings (corr_rays)
+        if (!check_cheirality(r.R, r.t, p.n0, p.n1, 1e-2)) {
             e2 = DBL_MAX;
             return;
         }
-        e2 = sampson_err(r.G, a0, a1, b0, b1) * C.loss_scale;
+        e2 = sampson_err(r.G, p.a0, p.a1, p.b0, p.b1) * C.loss_scale;
     } else {
         e2 = sampson_err(r.G, p.x0u, p.x0v, p.x1u, p.x1v);
     }

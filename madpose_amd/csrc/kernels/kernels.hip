@@ -32,7 +32,7 @@ __device__ inline double wave_sum(double v) {
     return v;
 }
 
-__device__ inline Corr load_corr(const PairData &D, int i, bool cal) {
+__device__ inline Corr load_corr(const PairConst &C, const PairData &D, int i, bool cal) {
     Corr p;
     p.x0u = D.x0u[i];
     p.x0v = D.x0v[i];
@@ -42,6 +42,7 @@ __device__ inline Corr load_corr(const PairData &D, int i, bool cal) {
     p.d1 = D.d1[i];
     p.r0 = cal ? D.r0[i] : 0.0;
     p.r1 = cal ? D.r1[i] : 0.0;
+    if (cal) corr_rays(C, p);
     return p;
 }
 
@@ -482,7 +483,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     const double t0 = C.thr[0], t1 = C.thr[1], t2 = C.thr[2];
     const double w0 = C.w[0], w1 = C.w[1], w2 = C.w[2];
     for (int i = threadIdx.x; i < C.n; i += kBlock) {
-        const Corr p = load_corr(D, i, V == kCal);
+        const Corr p = load_corr(C, D, i, V == kCal);
 #pragma unroll
         for (int m = 0; m < MAXM; ++m) {
             if (m < nm) {
@@ -527,7 +528,7 @@ __global__ void __launch_bounds__(1024) sweep_kernel(PairData D, PairConst C, co
     double acc = 0.0;
     const bool gate_md = C.score_type == 1, gate_epi = C.score_type == 2;
     for (int i = threadIdx.x; i < C.n; i += blockDim.x) {
-        const Corr p = load_corr(D, i, V == kCal);
+        const Corr p = load_corr(C, D, i, V == kCal);
         double e0, e1, e2;
         eval_corr<V>(C, r, p, false, e0, e1, e2);
         err[i] = e0;
@@ -562,7 +563,7 @@ __global__ void __launch_bounds__(kSweepBlock) sweep_host_kernel(PairData D, Pai
     double acc = 0.0;
     const bool gate_md = C.score_type == 1, gate_epi = C.score_type == 2;
     for (int i = blockIdx.x * kSweepBlock + threadIdx.x; i < C.n; i += gridDim.x * kSweepBlock) {
-        const Corr p = load_corr(D, i, V == kCal);
+        const Corr p = load_corr(C, D, i, V == kCal);
         double e0, e1, e2;
         eval_corr<V>(C, r, p, false, e0, e1, e2);
         out[i] = e0;
@@ -602,7 +603,7 @@ __global__ void __launch_bounds__(kBlock) score_models_kernel(PairData D, PairCo
     const ScoreRec r = recs[blockIdx.x];
     double acc = 0.0;
     for (int i = threadIdx.x; i < C.n; i += kBlock) {
-        const Corr p = load_corr(D, i, V == kCal);
+        const Corr p = load_corr(C, D, i, V == kCal);
         double e0, e1, e2;
         eval_corr<V>(C, r, p, true, e0, e1, e2);
         acc += msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]) + msac(e2, C.thr[2], C.w[2]);

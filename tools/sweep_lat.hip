@@ -1,0 +1,159 @@
+// Round-trip latency of the LO sweep (launch -> host sees the completion flag) for a
+// few ways of returning its results, on a synthetic calibrated pair of n points:
+//   host   sweep_host_kernel as shipped: errors + score to pinned host memory
+//   dev    the same kernel with the error rows in device memory (flag still host)
+//   flag   a one-workgroup kernel that only raises the flag (the floor)
+// Build + run (on an MI355X):
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/sweep_lat.hip -o tools/sweep_lat
+//   tools/sweep_lat [n] [reps]
+#include "../madpose_amd/csrc/kernels/kernels.hip"
+
+#include <chrono>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+using namespace mp;
+
+#define CHECK(x)                                                                                                      \
+    do {                                                                                                               \
+        hipError_t e = (x);                                                                                            \
+        if (e != hipSuccess) {                                                                                         \
+            std::fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);                \
+            std::exit(1);                                                                                              \
+        }                                                                                                              \
+    } while (0)
+
+namespace {
+__global__ void flag_only_kernel(int *flag, int seq) {
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+// one workgroup for the whole sweep: no cross-workgroup counter, one fence per lane
+template <int V, int NT>
+__global__ void __launch_bounds__(NT) sweep1_kernel(PairData D, PairConst C, ScoreRec r, double *out, int *flag,
+                                                    int seq) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < C.n; i += NT) {
+        const Corr p = load_corr(C, D, i, V == kCal);
+        double e0, e1, e2;
+        eval_corr<V>(C, r, p, false, e0, e1, e2);
+        out[i] = e0;
+        out[C.n + i] = e1;
+        out[2 * C.n + i] = e2;
+        acc += msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]) + msac(e2, C.thr[2], C.w[2]);
+    }
+    __shared__ double wpart[NT / 64];
+    const double v = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = v;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sc = 0.0;
+        for (int w = 0; w < NT / 64; ++w) sc += wpart[w];
+        out[3 * C.n] = sc;
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+} // namespace
+
+using Clock = std::chrono::steady_clock;
+
+int main(int argc, char **argv) {
+    const int n = argc > 1 ? std::atoi(argv[1]) : 2000;
+    const int reps = argc > 2 ? std::atoi(argv[2]) : 2000;
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<double> U(-1, 1);
+    std::vector<double> x0u(n), x0v(n), x1u(n), x1v(n), d0(n), d1(n), r0(n), r1(n);
+    for (int i = 0; i < n; ++i) {
+        x0u[i] = 320 + 200 * U(rng);
+        x0v[i] = 240 + 200 * U(rng);
+        x1u[i] = 320 + 200 * U(rng);
+        x1v[i] = 240 + 200 * U(rng);
+        d0[i] = 3 + U(rng);
+        d1[i] = 3 + U(rng);
+        r0[i] = r1[i] = 0.9;
+    }
+    auto up = [&](const std::vector<double> &v) {
+        double *p;
+        CHECK(hipMalloc(&p, v.size() * 8));
+        CHECK(hipMemcpy(p, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+        return (const double *)p;
+    };
+    PairData D{up(x0u), up(x0v), up(x1u), up(x1v), up(d0), up(d1), up(r0), up(r1)};
+    PairConst C{};
+    C.variant = kCal;
+    C.n = n;
+    const double K[9] = {500, 0, 320, 0, 500, 240, 0, 0, 1}, Ki[9] = {1 / 500., 0, -320 / 500., 0, 1 / 500., -240 / 500., 0, 0, 1};
+    for (int k = 0; k < 9; ++k) {
+        C.K0[k] = C.K1[k] = K[k];
+        C.K0i[k] = C.K1i[k] = Ki[k];
+    }
+    for (int t = 0; t < 3; ++t) {
+        C.thr[t] = 4.0;
+        C.w[t] = 1.0;
+    }
+    Model m{};
+    m.R[0] = m.R[4] = m.R[8] = 1.0;
+    m.t[0] = 0.3;
+    m.scale = 1.0;
+    m.focal0 = m.focal1 = 1.0;
+    ScoreRec rec;
+    prepare_score_rec(C, m, rec);
+
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    double *h_out, *d_out_h, *d_out_dev, *part;
+    int *h_flag, *d_flag;
+    unsigned *cnt;
+    CHECK(hipHostMalloc(&h_out, sizeof(double) * (3 * n + 1), hipHostMallocMapped | hipHostMallocCoherent));
+    CHECK(hipHostMalloc(&h_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    CHECK(hipHostGetDevicePointer((void **)&d_out_h, h_out, 0));
+    CHECK(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
+    CHECK(hipMalloc(&d_out_dev, sizeof(double) * (3 * n + 1)));
+    CHECK(hipMalloc(&part, sizeof(double) * sweep_blocks(n)));
+    CHECK(hipMalloc(&cnt, sizeof(unsigned)));
+    CHECK(hipMemset(cnt, 0, sizeof(unsigned)));
+    *h_flag = 0;
+    int seq = 0;
+
+    auto run = [&](const char *name, int mode) {
+        double t_launch = 0, t_wait = 0;
+        for (int r = 0; r < reps + 50; ++r) {
+            const int q = ++seq;
+            auto t0 = Clock::now();
+            if (mode == 0)
+                CHECK(launch_sweep_host(s, D, C, rec, d_out_h, d_flag, q, part, cnt));
+            else if (mode == 1)
+                CHECK(launch_sweep_host(s, D, C, rec, d_out_dev, d_flag, q, part, cnt));
+            else if (mode == 2)
+                flag_only_kernel<<<1, 64, 0, s>>>(d_flag, q);
+            else if (mode == 3)
+                sweep1_kernel<kCal, 1024><<<1, 1024, 0, s>>>(D, C, rec, d_out_h, d_flag, q);
+            else
+                sweep1_kernel<kCal, 256><<<1, 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q);
+            auto t1 = Clock::now();
+            while (__atomic_load_n(h_flag, __ATOMIC_ACQUIRE) != q) {
+            }
+            auto t2 = Clock::now();
+            if (r >= 50) {
+                t_launch += std::chrono::duration<double>(t1 - t0).count();
+                t_wait += std::chrono::duration<double>(t2 - t1).count();
+            }
+        }
+        CHECK(hipStreamSynchronize(s));
+        std::printf("%-6s n=%d: launch %.2f us, wait %.2f us, round trip %.2f us\n", name, n, 1e6 * t_launch / reps,
+                    1e6 * t_wait / reps, 1e6 * (t_launch + t_wait) / reps);
+    };
+    run("host", 0);
+    run("dev", 1);
+    run("flag", 2);
+    run("1wg1024", 3);
+    run("1wg256", 4);
+    run("host", 0);
+    std::printf("score %.6f\n", h_out[3 * n]);
+    return 0;
+}
