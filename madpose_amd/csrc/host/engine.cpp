@@ -185,11 +185,15 @@ class Sampler {
 // ---------------------------------------------------------------------------
 // Zero-copy LO sweep resources of one issuing thread: errors (3 x n) and the score
 // land in host-coherent pinned memory, completion is a flag raised by the kernel.
+// Two result buffers used alternately: the issuer reads a result in place while the
+// next sweep writes the other buffer, so nothing is copied out.
 struct SweepSlot {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int64_t cap = 0;
     double *h_out = nullptr, *d_out = nullptr;
+    double *h_out2 = nullptr, *d_out2 = nullptr;
+    int flip = 0;
     int *h_flag = nullptr, *d_flag = nullptr;
     int seq = 0;
     double *d_part = nullptr; // per-workgroup partial scores
@@ -199,10 +203,12 @@ struct SweepSlot {
         if (d_part) hipFree(d_part);
         if (d_cnt) hipFree(d_cnt);
         if (h_out) hipHostFree(h_out);
+        if (h_out2) hipHostFree(h_out2);
         if (h_flag) hipHostFree(h_flag);
         d_part = nullptr;
         d_cnt = nullptr;
         h_out = d_out = nullptr;
+        h_out2 = d_out2 = nullptr;
         h_flag = d_flag = nullptr;
         cap = 0;
     }
@@ -222,8 +228,10 @@ struct SweepSlot {
         MP_HIP(hipMalloc(&d_cnt, sizeof(unsigned)));
         MP_HIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned), stream));
         MP_HIP(hipHostMalloc(&h_out, sizeof(double) * (3 * nn + 1), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostMalloc(&h_out2, sizeof(double) * (3 * nn + 1), hipHostMallocMapped | hipHostMallocCoherent));
         MP_HIP(hipHostMalloc(&h_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
         MP_HIP(hipHostGetDevicePointer((void **)&d_out, h_out, 0));
+        MP_HIP(hipHostGetDevicePointer((void **)&d_out2, h_out2, 0));
         MP_HIP(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
         *h_flag = seq;
         MP_HIP(hipStreamSynchronize(stream));
@@ -627,7 +635,7 @@ class Run {
         Model model;
         bool valid = false;
         double score = 0.0;
-        std::vector<double> err;
+        const double *err = nullptr; // the slot buffer holding the last result
         uint64_t count = 0;
         double t[3] = {0, 0, 0}; // launch / wait / copy seconds (MADPOSE_SWEEP_TIMING)
     };
@@ -637,14 +645,17 @@ class Run {
     const double *sweep(Lane &L, const Model &m, double *score) {
         if (L.valid && std::memcmp(&m, &L.model, sizeof(Model)) == 0) {
             *score = L.score;
-            return L.err.data();
+            return L.err;
         }
         auto t_sw = Clock::now();
         ScoreRec rec;
         prepare_score_rec(P_.C, m, rec);
         SweepSlot &sl = *L.slot;
         const int seq = ++sl.seq;
-        MP_HIP(launch_sweep_host(sl.stream, D_, P_.C, rec, sl.d_out, sl.d_flag, seq, sl.d_part, sl.d_cnt));
+        sl.flip ^= 1;
+        double *d_out = sl.flip ? sl.d_out2 : sl.d_out;
+        const double *h_out = sl.flip ? sl.h_out2 : sl.h_out;
+        MP_HIP(launch_sweep_host(sl.stream, D_, P_.C, rec, d_out, sl.d_flag, seq, sl.d_part, sl.d_cnt));
         const double t_launched = secs(t_sw);
         // poll the completion flag; after 2 s fall back to a stream sync, which also
         // surfaces any kernel error
@@ -656,12 +667,12 @@ class Run {
             }
         }
         const double t_done = secs(t_sw);
-        L.err.assign(sl.h_out, sl.h_out + 3 * n_);
+        L.err = h_out;
         L.t[0] += t_launched;
         L.t[1] += t_done - t_launched;
         L.t[2] += secs(t_sw) - t_done;
         L.model = m;
-        L.score = sl.h_out[3 * n_];
+        L.score = h_out[3 * n_];
         L.valid = true;
         L.count++;
         if (g_prof_on.load(std::memory_order_relaxed)) {
@@ -671,7 +682,7 @@ class Run {
             g_prof.sweep_wall_ms += 1e3 * dt;
         }
         *score = L.score;
-        return L.err.data();
+        return L.err;
     }
     double score(Lane &L, const Model &m) {
         double s;
