@@ -194,19 +194,13 @@ struct SweepSlot {
     double *h_out = nullptr, *d_out = nullptr;
     double *h_out2 = nullptr, *d_out2 = nullptr;
     int flip = 0;
-    int *h_flag = nullptr, *d_flag = nullptr;
+    int *h_flag = nullptr, *d_flag = nullptr; // one completion flag per workgroup
     int seq = 0;
-    double *d_part = nullptr; // per-workgroup partial scores
-    unsigned *d_cnt = nullptr;
 
     void release() {
-        if (d_part) hipFree(d_part);
-        if (d_cnt) hipFree(d_cnt);
         if (h_out) hipHostFree(h_out);
         if (h_out2) hipHostFree(h_out2);
         if (h_flag) hipHostFree(h_flag);
-        d_part = nullptr;
-        d_cnt = nullptr;
         h_out = d_out = nullptr;
         h_out2 = d_out2 = nullptr;
         h_flag = d_flag = nullptr;
@@ -224,16 +218,14 @@ struct SweepSlot {
         }
         if (nn <= cap) return;
         release();
-        MP_HIP(hipMalloc(&d_part, sizeof(double) * sweep_blocks(nn)));
-        MP_HIP(hipMalloc(&d_cnt, sizeof(unsigned)));
-        MP_HIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned), stream));
-        MP_HIP(hipHostMalloc(&h_out, sizeof(double) * (3 * nn + 1), hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostMalloc(&h_out2, sizeof(double) * (3 * nn + 1), hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostMalloc(&h_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        const int nb = sweep_blocks(nn);
+        MP_HIP(hipHostMalloc(&h_out, sizeof(double) * (3 * nn + nb), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostMalloc(&h_out2, sizeof(double) * (3 * nn + nb), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostMalloc(&h_flag, sizeof(int) * nb, hipHostMallocMapped | hipHostMallocCoherent));
         MP_HIP(hipHostGetDevicePointer((void **)&d_out, h_out, 0));
         MP_HIP(hipHostGetDevicePointer((void **)&d_out2, h_out2, 0));
         MP_HIP(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
-        *h_flag = seq;
+        for (int b = 0; b < nb; ++b) h_flag[b] = seq;
         MP_HIP(hipStreamSynchronize(stream));
         cap = nn;
     }
@@ -655,24 +647,29 @@ class Run {
         sl.flip ^= 1;
         double *d_out = sl.flip ? sl.d_out2 : sl.d_out;
         const double *h_out = sl.flip ? sl.h_out2 : sl.h_out;
-        MP_HIP(launch_sweep_host(sl.stream, D_, P_.C, rec, d_out, sl.d_flag, seq, sl.d_part, sl.d_cnt));
+        MP_HIP(launch_sweep_host(sl.stream, D_, P_.C, rec, d_out, sl.d_flag, seq));
         const double t_launched = secs(t_sw);
-        // poll the completion flag; after 2 s fall back to a stream sync, which also
-        // surfaces any kernel error
-        for (uint64_t spin = 0; __atomic_load_n(sl.h_flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
-            if ((spin & 1023) == 1023 && secs(t_sw) > 2.0) {
-                MP_HIP(hipStreamSynchronize(sl.stream));
-                if (__atomic_load_n(sl.h_flag, __ATOMIC_ACQUIRE) != seq)
-                    throw std::runtime_error("LO sweep did not signal completion");
+        // poll the workgroups' completion flags; after 2 s fall back to a stream sync,
+        // which also surfaces any kernel error
+        const int nb = sweep_blocks(n_);
+        for (int b = 0; b < nb; ++b) {
+            for (uint64_t spin = 0; __atomic_load_n(sl.h_flag + b, __ATOMIC_ACQUIRE) != seq; ++spin) {
+                if ((spin & 1023) == 1023 && secs(t_sw) > 2.0) {
+                    MP_HIP(hipStreamSynchronize(sl.stream));
+                    if (__atomic_load_n(sl.h_flag + b, __ATOMIC_ACQUIRE) != seq)
+                        throw std::runtime_error("LO sweep did not signal completion");
+                }
             }
         }
+        double total = 0.0; // partial scores in workgroup order
+        for (int b = 0; b < nb; ++b) total += h_out[3 * n_ + b];
         const double t_done = secs(t_sw);
         L.err = h_out;
         L.t[0] += t_launched;
         L.t[1] += t_done - t_launched;
         L.t[2] += secs(t_sw) - t_done;
         L.model = m;
-        L.score = h_out[3 * n_];
+        L.score = total;
         L.valid = true;
         L.count++;
         if (g_prof_on.load(std::memory_order_relaxed)) {

@@ -34,17 +34,18 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
 // single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);
-// the same sweep writing errors + score (out[3n]) to host-mapped memory and raising
-// *flag = seq (system scope) when done; the host polls the flag
 // point-solver root stage alone, C.variant kCal (5pt) or kSF (6pt); impl 0: lane
 // per sample, 1: 16-lane groups.  cand: kPtCandStride doubles per sample (cal: 9 per
 // essential matrix; sf: null-space basis N (27), then the positive roots u)
 hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, double *cand, int *ncand, int impl);
-// part: sweep_blocks(n) doubles, cnt: one zero-initialised counter (device memory)
+// the single-model sweep writing straight to host-mapped memory: out[0, 3n) the errors,
+// out[3n + b] workgroup b's partial score, flags[b] = seq (system scope) once
+// workgroup b is done, for b < sweep_blocks(n); the score is the sum of the partials
+// in workgroup order
 int sweep_blocks(int64_t n);
 hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
-                            int *flag, int seq, double *part, unsigned *cnt);
+                            int *flags, int seq);
 // scores of many explicit models (one workgroup per model) -- used by mp_score_models
 hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
                                double *scores);

@@ -1,8 +1,12 @@
 // Round-trip latency of the LO sweep (launch -> host sees the completion flag) for a
 // few ways of returning its results, on a synthetic calibrated pair of n points:
-//   host   sweep_host_kernel as shipped: errors + score to pinned host memory
-//   dev    the same kernel with the error rows in device memory (flag still host)
+//   host   the earlier protocol: errors to pinned host memory, the last workgroup to
+//          arrive (system-scope counter) sums the partials and raises one flag
+//   dev    the same with the error rows in device memory (flag still host)
+//   flags  sweep_host_kernel as shipped: one flag per workgroup, host sums
 //   flag   a one-workgroup kernel that only raises the flag (the floor)
+//   noeval / nofence / neither   the shipped protocol without the residuals, without
+//          the per-workgroup system fence, without both
 // Build + run (on an MI355X):
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/sweep_lat.hip -o tools/sweep_lat
 //   tools/sweep_lat [n] [reps]
@@ -56,6 +60,45 @@ __global__ void __launch_bounds__(NT) sweep1_kernel(PairData D, PairConst C, Sco
         out[3 * C.n] = sc;
         __threadfence_system();
         __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+// variants of sweep_host_kernel: EVAL = false replaces the residuals by the loaded
+// coordinates (isolates the cross-workgroup completion protocol), FENCE = false drops
+// each workgroup's system-scope fence before its arrival
+template <int V, bool EVAL, bool FENCE>
+__global__ void __launch_bounds__(256) sweep_var_kernel(PairData D, PairConst C, ScoreRec r, double *out, int *flag,
+                                                        int seq, double *part, unsigned *cnt) {
+    double acc = 0.0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < C.n; i += gridDim.x * 256) {
+        const Corr p = load_corr(C, D, i, V == kCal);
+        double e0 = p.x0u, e1 = p.x1u, e2 = p.d0;
+        if (EVAL) eval_corr<V>(C, r, p, false, e0, e1, e2);
+        out[i] = e0;
+        out[C.n + i] = e1;
+        out[2 * C.n + i] = e2;
+        acc += msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]) + msac(e2, C.thr[2], C.w[2]);
+    }
+    __shared__ double wpart[4];
+    __shared__ bool last;
+    const double v = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = v;
+    if (FENCE) __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sc = 0.0;
+        for (int w = 0; w < 4; ++w) sc += wpart[w];
+        part[blockIdx.x] = sc;
+        const unsigned arrived = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = arrived == gridDim.x - 1;
+        if (last) {
+            double tot = 0.0;
+            for (unsigned b = 0; b < gridDim.x; ++b)
+                tot += __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            out[3 * C.n] = tot;
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 } // namespace
@@ -114,6 +157,14 @@ int main(int argc, char **argv) {
     CHECK(hipHostGetDevicePointer((void **)&d_out_h, h_out, 0));
     CHECK(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
     CHECK(hipMalloc(&d_out_dev, sizeof(double) * (3 * n + 1)));
+    double *h_out8, *d_out8;
+    int *h_flags, *d_flags;
+    const int nbk = sweep_blocks(n);
+    CHECK(hipHostMalloc(&h_out8, sizeof(double) * (3 * n + 64), hipHostMallocMapped | hipHostMallocCoherent));
+    CHECK(hipHostMalloc(&h_flags, sizeof(int) * 64, hipHostMallocMapped | hipHostMallocCoherent));
+    CHECK(hipHostGetDevicePointer((void **)&d_out8, h_out8, 0));
+    CHECK(hipHostGetDevicePointer((void **)&d_flags, h_flags, 0));
+    for (int b = 0; b < 64; ++b) h_flags[b] = 0;
     CHECK(hipMalloc(&part, sizeof(double) * sweep_blocks(n)));
     CHECK(hipMalloc(&cnt, sizeof(unsigned)));
     CHECK(hipMemset(cnt, 0, sizeof(unsigned)));
@@ -126,17 +177,34 @@ int main(int argc, char **argv) {
             const int q = ++seq;
             auto t0 = Clock::now();
             if (mode == 0)
-                CHECK(launch_sweep_host(s, D, C, rec, d_out_h, d_flag, q, part, cnt));
+                sweep_var_kernel<kCal, true, true><<<nbk, 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q, part, cnt);
             else if (mode == 1)
-                CHECK(launch_sweep_host(s, D, C, rec, d_out_dev, d_flag, q, part, cnt));
+                sweep_var_kernel<kCal, true, true><<<nbk, 256, 0, s>>>(D, C, rec, d_out_dev, d_flag, q, part, cnt);
             else if (mode == 2)
                 flag_only_kernel<<<1, 64, 0, s>>>(d_flag, q);
+            else if (mode == 8)
+                CHECK(launch_sweep_host(s, D, C, rec, d_out8, d_flags, q));
+            else if (mode == 5)
+                sweep_var_kernel<kCal, false, true><<<sweep_blocks(n), 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q, part, cnt);
+            else if (mode == 6)
+                sweep_var_kernel<kCal, true, false><<<sweep_blocks(n), 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q, part, cnt);
+            else if (mode == 7)
+                sweep_var_kernel<kCal, false, false><<<sweep_blocks(n), 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q, part, cnt);
             else if (mode == 3)
                 sweep1_kernel<kCal, 1024><<<1, 1024, 0, s>>>(D, C, rec, d_out_h, d_flag, q);
             else
                 sweep1_kernel<kCal, 256><<<1, 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q);
             auto t1 = Clock::now();
-            while (__atomic_load_n(h_flag, __ATOMIC_ACQUIRE) != q) {
+            if (mode == 8) {
+                for (int b = 0; b < nbk; ++b)
+                    while (__atomic_load_n(h_flags + b, __ATOMIC_ACQUIRE) != q) {
+                    }
+                double tot = 0.0;
+                for (int b = 0; b < nbk; ++b) tot += h_out8[3 * n + b];
+                h_out[3 * n] = tot;
+            } else {
+                while (__atomic_load_n(h_flag, __ATOMIC_ACQUIRE) != q) {
+                }
             }
             auto t2 = Clock::now();
             if (r >= 50) {
@@ -151,9 +219,13 @@ int main(int argc, char **argv) {
     run("host", 0);
     run("dev", 1);
     run("flag", 2);
-    run("1wg1024", 3);
-    run("1wg256", 4);
+    run("flags", 8);
+    run("noeval", 5);
+    run("nofence", 6);
+    run("neither", 7);
     run("host", 0);
+    std::printf("score %.6f\n", h_out[3 * n]);
+    run("flags", 8);
     std::printf("score %.6f\n", h_out[3 * n]);
     return 0;
 }
