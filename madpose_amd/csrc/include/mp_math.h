@@ -59,21 +59,21 @@ template <int N, int M> MP_HD bool gauss_solve(double (&A)[N][N], double (&B)[N]
                 p = r;
             }
         }
+        // (swaps as selects between opaque values: see opaque() in mp_types.h)
 #pragma unroll
         for (int r = k + 1; r < N; ++r) {
-            if (r == p) {
+            const bool sw = r == p;
 #pragma unroll
-                for (int c = 0; c < N; ++c) {
-                    double t = A[k][c];
-                    A[k][c] = A[r][c];
-                    A[r][c] = t;
-                }
+            for (int c = 0; c < N; ++c) {
+                const double akc = opaque(A[k][c]), arc = opaque(A[r][c]);
+                A[k][c] = sw ? arc : akc;
+                A[r][c] = sw ? akc : arc;
+            }
 #pragma unroll
-                for (int c = 0; c < M; ++c) {
-                    double t = B[k][c];
-                    B[k][c] = B[r][c];
-                    B[r][c] = t;
-                }
+            for (int c = 0; c < M; ++c) {
+                const double bkc = opaque(B[k][c]), brc = opaque(B[r][c]);
+                B[k][c] = sw ? brc : bkc;
+                B[r][c] = sw ? bkc : brc;
             }
         }
         if (best == 0.0) ok = false;
@@ -484,18 +484,22 @@ MP_HD void smallest_right_sv4(const double (&A0)[4][4], double *v) {
     double nrm[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) nrm[j] = A[0][j] * A[0][j] + A[1][j] * A[1][j] + A[2][j] * A[2][j] + A[3][j] * A[3][j];
+    // column of the smallest norm (first minimum); picked by one-hot weights rather
+    // than an index or a select chain, either of which leaves V in scratch (a select
+    // of loads becomes a load of a select of addresses before V is promoted)
     int k = 0;
+    double best = nrm[0];
 #pragma unroll
     for (int j = 1; j < 4; ++j)
-        if (nrm[j] < nrm[k]) k = j;
+        if (nrm[j] < best) {
+            best = nrm[j];
+            k = j;
+        }
+    double w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        double val = V[i][0];
+    for (int j = 0; j < 4; ++j) w[j] = (k == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int j = 1; j < 4; ++j)
-            if (k == j) val = V[i][j];
-        v[i] = val;
-    }
+    for (int i = 0; i < 4; ++i) v[i] = w[0] * V[i][0] + w[1] * V[i][1] + w[2] * V[i][2] + w[3] * V[i][3];
 }
 
 } // namespace mp

@@ -19,11 +19,12 @@
 namespace mp {
 
 // a[i] for a runtime i by selects (keeps a small array in registers; indexing it
-// with a runtime index would move it to scratch)
+// with a runtime index would move it to scratch).  The elements pass through opaque()
+// so the select chain is not folded back into a load from a selected address.
 template <int N> MP_HD double pick(const double (&a)[N], int i) {
-    double v = a[0];
+    double v = opaque(a[0]);
 #pragma unroll
-    for (int k = 1; k < N; ++k) v = (i == k) ? a[k] : v;
+    for (int k = 1; k < N; ++k) v = (i == k) ? opaque(a[k]) : v;
     return v;
 }
 

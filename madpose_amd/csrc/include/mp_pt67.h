@@ -110,17 +110,21 @@ MP_HD int relpose_7pt_F(const double (&x1)[7][3], const double (&x2)[7][3], doub
     c[0] = det_rows(B, B + 3, B + 6);
     double roots[3];
     const int nr = sturm_real_roots<3>(c, roots);
-    for (int k = 0; k < nr; ++k) {
-        double nn = 0.0;
+    // (constant indices from the front end on: F and roots stay in registers)
+    static_for<3>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if (k < nr) {
+            double nn = 0.0;
 #pragma unroll
-        for (int e = 0; e < 9; ++e) {
-            F[k][e] = roots[k] * A[e] + B[e];
-            nn += F[k][e] * F[k][e];
+            for (int e = 0; e < 9; ++e) {
+                F[k][e] = roots[k] * A[e] + B[e];
+                nn += F[k][e] * F[k][e];
+            }
+            nn = 1.0 / sqrt(nn);
+#pragma unroll
+            for (int e = 0; e < 9; ++e) F[k][e] *= nn;
         }
-        nn = 1.0 / sqrt(nn);
-#pragma unroll
-        for (int e = 0; e < 9; ++e) F[k][e] *= nn;
-    }
+    });
     return nr;
 }
 
@@ -297,7 +301,7 @@ MP_HD bool recover_pose_good(const RecoverCands &rc, int k, const double *p0, co
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) P1[r][c] = (k & 1) ? rc.R2[3 * r + c] : rc.R1[3 * r + c];
+        for (int c = 0; c < 3; ++c) P1[r][c] = (k & 1) ? opaque(rc.R2[3 * r + c]) : opaque(rc.R1[3 * r + c]);
         P1[r][3] = ts * rc.u2[r];
     }
     double A[4][4];
@@ -334,7 +338,7 @@ MP_HD int recover_pose_select(const RecoverCands &rc, const int (&good)[4], doub
         best = 2;
     const double ts = (best < 2) ? 1.0 : -1.0;
 #pragma unroll
-    for (int e = 0; e < 9; ++e) R[e] = (best & 1) ? rc.R2[e] : rc.R1[e]; // (selects: rc stays in registers)
+    for (int e = 0; e < 9; ++e) R[e] = (best & 1) ? opaque(rc.R2[e]) : opaque(rc.R1[e]); // (rc stays in registers)
 #pragma unroll
     for (int r = 0; r < 3; ++r) t[r] = ts * rc.u2[r];
     return (best == 0) ? good[0] : ((best == 1) ? good[1] : ((best == 2) ? good[2] : good[3]));

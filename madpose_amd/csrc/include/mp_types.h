@@ -15,6 +15,17 @@
 
 namespace mp {
 
+// A value the optimiser cannot trace back to the load that produced it.  For selects
+// between elements of a local array / struct: select(c, load a, load b) is folded
+// into load(select(c, &a, &b)), which keeps the whole aggregate in scratch; selecting
+// between opaque values keeps it in registers.
+MP_HD double opaque(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x));
+#endif
+    return x;
+}
+
 enum Variant : int { kCal = 0, kSF = 1, kTF = 2, kScaleOnly = 3 }; // kScaleOnly: host-side only
 
 // Model layout == mp_model of include/madpose_mi355x.h (src/pose.h:7-56).

@@ -375,9 +375,12 @@ __global__ void __launch_bounds__(64) pt_roots_kernel(PairData D, PairConst C, c
         load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
         double F[3][9];
         n = relpose_7pt_F(b0, b1, F);
-        for (int k = 0; k < n; ++k)
+        static_for<3>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            if (k < n)
 #pragma unroll
-            for (int e = 0; e < 9; ++e) out[9 * k + e] = F[k][e];
+                for (int e = 0; e < 9; ++e) out[9 * k + e] = F[k][e];
+        });
     }
     ncand[idx] = n;
 }
