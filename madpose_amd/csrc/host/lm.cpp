@@ -813,7 +813,10 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
     if (nchunks <= 1) {
         range(0, nb, total);
     } else {
-        std::vector<Acc> parts(nchunks);
+        // (on the stack up to 64 chunks = 16k blocks: no allocation per evaluation)
+        Acc stack_parts[64];
+        std::vector<Acc> heap_parts(nchunks > 64 ? nchunks : 0);
+        Acc *parts = nchunks > 64 ? heap_parts.data() : stack_parts;
         auto chunk = [&](size_t k) {
             parts[k].clear();
             range(k * kChunk, std::min(nb, (k + 1) * kChunk), parts[k]);
@@ -828,7 +831,9 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
     return total.cost;
 }
 
-bool chol_solve(std::vector<double> A, int n, std::vector<double> b, std::vector<double> *x) {
+// Solves A x = b (n x n, symmetric positive definite) by Cholesky; A and b are
+// overwritten (factor, solution).  Returns false if A is not positive definite.
+bool chol_solve(double *A, int n, double *b) {
     for (int j = 0; j < n; ++j) {
         double d = A[j * n + j];
         for (int k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
@@ -851,7 +856,6 @@ bool chol_solve(std::vector<double> A, int n, std::vector<double> b, std::vector
         for (int k = i + 1; k < n; ++k) s -= A[k * n + i] * b[k];
         b[i] = s / A[i * n + i];
     }
-    *x = b;
     return true;
 }
 
@@ -954,33 +958,35 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
         return p.q[0] * p.q[0] + p.q[1] * p.q[1] + p.q[2] * p.q[2] + p.q[3] * p.q[3] + p.t[0] * p.t[0] +
                p.t[1] * p.t[1] + p.t[2] * p.t[2] + p.s * p.s + p.o0 * p.o0 + p.o1 * p.o1 + p.f0 * p.f0 + p.f1 * p.f1;
     };
-    std::vector<double> H(n * n), g(n), Hc(n * n), gc(n);
-    double cost = evaluate(C, x, H.data(), g.data());
+    // (fixed-size storage: n <= kNFull, no allocation inside the iterations)
+    double Hbuf[2][kNFull * kNFull], gbuf[2][kNFull];
+    double *H = Hbuf[0], *g = gbuf[0], *Hc = Hbuf[1], *gc = gbuf[1];
+    double cost = evaluate(C, x, H, g);
     auto gmax = [&]() {
         double v = 0;
-        for (double e : g) v = std::max(v, std::fabs(e));
+        for (int a = 0; a < n; ++a) v = std::max(v, std::fabs(g[a]));
         return v;
     };
     double radius = 1e4, decrease = 2.0;
     if (!(gmax() <= S.gtol)) {
         for (int iter = 0; iter < S.max_iter; ++iter) {
-            std::vector<double> sc(n), A(n * n), rhs(n), y;
+            double sc[kNFull], A[kNFull * kNFull], y[kNFull];
             for (int j = 0; j < n; ++j) sc[j] = 1.0 / (1.0 + std::sqrt(H[j * n + j]));
             for (int a = 0; a < n; ++a) {
-                rhs[a] = -g[a] * sc[a];
+                y[a] = -g[a] * sc[a];
                 for (int b = 0; b < n; ++b) A[a * n + b] = H[a * n + b] * sc[a] * sc[b];
             }
             for (int j = 0; j < n; ++j) {
                 const double dg = std::min(std::max(A[j * n + j], 1e-6), 1e32);
                 A[j * n + j] += dg / radius;
             }
-            if (!chol_solve(A, n, rhs, &y)) {
+            if (!chol_solve(A, n, y)) {
                 radius /= decrease;
                 decrease *= 2.0;
                 if (radius < 1e-32) break;
                 continue;
             }
-            std::vector<double> d(n);
+            double d[kNFull];
             for (int j = 0; j < n; ++j) d[j] = y[j] * sc[j];
             // candidate = Plus(x, d), projected onto the bounds
             Params c = x;
@@ -1019,7 +1025,7 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
             const double step_norm = std::sqrt(step2), xnorm = std::sqrt(amb_norm2(x));
             // the candidate is evaluated with its normal equations: accepted steps
             // (the common case) then need no second pass
-            const double cand_cost = evaluate(C, c, Hc.data(), gc.data());
+            const double cand_cost = evaluate(C, c, Hc, gc);
             if (step_norm <= S.ptol * (xnorm + S.ptol)) break;
             if (std::fabs(cost - cand_cost) <= S.ftol * cost) break;
             double gd = 0, jd2 = 0;
@@ -1032,8 +1038,8 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
             if (rho > 1e-3) {
                 x = c;
                 cost = cand_cost;
-                H.swap(Hc);
-                g.swap(gc);
+                std::swap(H, Hc);
+                std::swap(g, gc);
                 radius = std::min(1e16, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3)));
                 decrease = 2.0;
                 if (gmax() <= S.gtol) break;
