@@ -692,6 +692,7 @@ class Run {
         int c = 0;
         for (int t = 0; t < 3; ++t) {
             out[t].clear();
+            out[t].reserve(n_); // (one allocation instead of a growth sequence)
             for (int i = 0; i < n_; ++i)
                 if (e[(size_t)t * n_ + i] < thr[t]) {
                     out[t].push_back(i);
@@ -770,7 +771,10 @@ class Run {
     }
 
     static void split(const std::vector<int> &all, int n, std::vector<int> out[3]) {
-        for (int t = 0; t < 3; ++t) out[t].clear();
+        for (int t = 0; t < 3; ++t) {
+            out[t].clear();
+            out[t].reserve(all.size());
+        }
         for (int idx : all) {
             int t = 0;
             while (idx >= n) {
@@ -807,6 +811,7 @@ class Run {
         }
         const int total = (k[0] + k[1] + k[2]) * o_.min_sample_multiplicator;
         std::vector<int> all;
+        all.reserve(inl[0].size() + inl[1].size() + inl[2].size());
         for (int t = 0; t < 3; ++t)
             for (int idx : inl[t]) all.push_back(idx + t * n_);
         shuffle_resize(*L.sel, total, &all);
