@@ -189,7 +189,7 @@ template <> struct MdGroup<kTF> {
 };
 
 template <int V>
-__global__ void __launch_bounds__(64) md_solve_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kCal ? 3 : 2))) md_solve_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                             const int *samples, Model *models, ScoreRec *recs,
                                                             int *counts, int maxm) {
     using G = MdGroup<V>;
