@@ -277,13 +277,19 @@ def run_scannet(a, wl, world, rank, dev, barrier):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # defaults: 40 / 4 pairs for the single-pair workloads (about 0.5 s timed, so the
+    # host LO's jitter averages out), 10 / 2 passes over the pair set for scannet
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cal")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (0 = skip)")
     ap.add_argument("--pairs", type=int, default=0, help="scannet: total pairs (default 1500)")
     ap.add_argument("--streams", type=int, default=8, help="scannet: pairs in flight per GPU")
     a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 10 if a.workload == "scannet" else 40
+    if a.warmup is None:
+        a.warmup = 2 if a.workload == "scannet" else 4
     wl = WORKLOADS[a.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
