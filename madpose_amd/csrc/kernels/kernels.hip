@@ -1,15 +1,20 @@
 // HIP kernels of the MI355X hybrid-RANSAC engine (gfx950, wave64).
 //
-//  prep_pair      per-pair bearing norms (once per pair)
-//  md_solve<V>    MD minimal solver, one iteration per thread (registers)
-//  pt_solve<V>    point minimal solver, one iteration per thread
-//  score_batch<V> THE hot loop: one workgroup per RANSAC iteration; each lane owns
-//                 correspondences i = lane, lane+256, ...; all models of the
-//                 iteration are scored from registers with model constants read
-//                 through the scalar cache; MSAC sums reduced in-wave (DPP shuffles)
-//                 and across the 4 waves in LDS in a fixed order (deterministic);
-//                 the workgroup also performs GetBestEstimatedModelId's argmin.
-//  sweep<V>       one model, all points: errors for GetInliers + gated score
+//  prep_pair          per-pair bearing norms (once per pair)
+//  md_solve_group<V>  MD minimal solvers, one 16-lane group per sample (side stream);
+//                     md_solve<V, ALT> keeps one sample per lane for the option-gated
+//                     paths and A/B runs
+//  pt_solve<V>        point minimal solvers in stages: root stage (group_5pt.h /
+//                     group_6pt.h / lane 7pt), tails per root (group_tail.h),
+//                     compaction into model slots
+//  score_batch<V>     THE hot loop: one workgroup per RANSAC iteration; each lane owns
+//                     correspondences i = lane, lane+256, ...; all models of the
+//                     iteration are scored from registers with model constants read
+//                     through the scalar cache; MSAC sums reduced in-wave (DPP shuffles)
+//                     and across the 4 waves in LDS in a fixed order (deterministic);
+//                     the workgroup also performs GetBestEstimatedModelId's argmin.
+//  sweep_host<V>      LO sweep: one model, all points, errors + partial scores straight
+//                     to pinned host memory, one completion flag per workgroup
 #include <cfloat>
 #include <cstdlib>
 
