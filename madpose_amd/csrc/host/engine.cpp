@@ -70,10 +70,13 @@ struct Batch {
     std::vector<IterationStream> snaps;
 };
 
-// Draws B iterations from rs into g (samples / md list / pt list of slot memory);
-// returns false if *abort was raised first (checked every 256 iterations).
-bool draw_batch(IterationStream &rs, Batch &g, uint32_t B, int slot, int *smp, int *md, int *pt,
-                const std::atomic<bool> *abort) {
+// Draws B iterations from rs into g and the slot memory at `smp`: the samples
+// (8 ints per iteration), then right behind them the iteration lists -- MD iterations
+// ascending from the front, point iterations from the back (descending) -- so the
+// batch is one contiguous block of 9B ints (one upload).  Returns false if *abort was
+// raised first (checked every 256 iterations).
+bool draw_batch(IterationStream &rs, Batch &g, uint32_t B, int slot, int *smp, const std::atomic<bool> *abort) {
+    int *lists = smp + 8 * (size_t)B;
     g.B = B;
     g.slot = slot;
     g.nmd = g.npt = 0;
@@ -85,9 +88,9 @@ bool draw_batch(IterationStream &rs, Batch &g, uint32_t B, int slot, int *smp, i
         const int st = rs.next(smp + 8 * j);
         g.types[j] = (uint8_t)st;
         if (st == 0)
-            md[g.nmd++] = (int)j;
+            lists[g.nmd++] = (int)j;
         else
-            pt[g.npt++] = (int)j;
+            lists[B - 1 - g.npt++] = (int)j;
     }
     return true;
 }
@@ -110,7 +113,7 @@ class Sampler {
     // starts drawing B iterations from `from` into *g (the caller must not touch *g
     // or the slot memory until finish()/cancel() returned); `after` runs on the worker
     // once the batch is drawn (the post-LO speculation launches it on the GPU there)
-    void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp, int *md, int *pt,
+    void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp,
                std::function<void()> after = nullptr) {
         std::lock_guard<std::mutex> lk(mu_);
         after_ = std::move(after);
@@ -120,8 +123,6 @@ class Sampler {
         B_ = B;
         slot_ = slot;
         smp_ = smp;
-        md_ = md;
-        pt_ = pt;
         abort_ = false;
         busy_ = true;
         ok_ = false;
@@ -151,7 +152,7 @@ class Sampler {
             if (quit_) return;
             seen = gen_;
             lk.unlock();
-            const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, md_, pt_, &abort_);
+            const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, &abort_);
             std::exception_ptr err;
             if (ok && after_) {
                 try {
@@ -173,7 +174,7 @@ class Sampler {
     Batch *g_ = nullptr;
     uint32_t B_ = 0;
     int slot_ = 0;
-    int *smp_ = nullptr, *md_ = nullptr, *pt_ = nullptr;
+    int *smp_ = nullptr;
     std::function<void()> after_;
     std::exception_ptr err_;
     std::atomic<bool> abort_{false};
@@ -311,10 +312,12 @@ struct DeviceCtx {
     int64_t cap_n = 0;
     int cap_b = 0, cap_m = 0;
     double *d_pair = nullptr; // 8 arrays of cap_n
-    int *d_samples = nullptr, *d_md_list = nullptr, *d_pt_list = nullptr, *d_counts = nullptr, *d_best_slot = nullptr;
+    int *d_samples = nullptr; // a batch's samples + iteration lists (draw_batch layout)
+    int *d_counts = nullptr;
+    IterResult *d_res = nullptr;
     Model *d_models = nullptr;
     ScoreRec *d_recs = nullptr;
-    double *d_scores = nullptr, *d_best = nullptr;
+    double *d_scores = nullptr;
     ScoreRec *d_rec1 = nullptr;
     double *d_err = nullptr, *d_score1 = nullptr;
     // staged point-solver workspace (kernels.h PtWorkspace)
@@ -326,8 +329,9 @@ struct DeviceCtx {
     SweepSlot sweep_slot[kLoLanes];
     std::unique_ptr<LoWorkers> lo_workers; // created on first parallel LO
     // pinned host mirrors
-    int *h_samples = nullptr, *h_md_list = nullptr, *h_pt_list = nullptr, *h_counts = nullptr, *h_best_slot = nullptr;
-    double *h_best = nullptr, *h_err = nullptr, *h_score1 = nullptr;
+    int *h_samples = nullptr; // two slots of 9 * max_batch ints
+    IterResult *h_res = nullptr;
+    double *h_err = nullptr, *h_score1 = nullptr;
     ScoreRec *h_rec1 = nullptr;
     Model *h_model1 = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr}; // solve start / score start / score end
@@ -338,23 +342,25 @@ struct DeviceCtx {
 
     void free_all() {
         hipSetDevice(device);
-        for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_md_list, (void *)d_pt_list, (void *)d_counts,
-                        (void *)d_best_slot, (void *)d_models, (void *)d_recs, (void *)d_scores, (void *)d_best,
+        for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_counts,
+                        (void *)d_res, (void *)d_models, (void *)d_recs, (void *)d_scores,
                         (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_ncand,
                         (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
-        for (void *p : {(void *)h_samples, (void *)h_md_list, (void *)h_pt_list, (void *)h_counts, (void *)h_best_slot,
-                        (void *)h_best, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1})
+        for (void *p : {(void *)h_samples, (void *)h_res, (void *)h_err,
+                        (void *)h_score1, (void *)h_rec1, (void *)h_model1})
             if (p) hipHostFree(p);
-        d_pair = d_err = d_scores = d_best = d_score1 = nullptr;
-        d_samples = d_md_list = d_pt_list = d_counts = d_best_slot = nullptr;
+        d_pair = d_err = d_scores = d_score1 = nullptr;
+        d_samples = d_counts = nullptr;
+        d_res = nullptr;
         d_models = nullptr;
         d_recs = d_rec1 = nullptr;
         d_pt_cand = nullptr;
         d_pt_ncand = d_pt_valid = nullptr;
         d_pt_slots = nullptr;
-        h_samples = h_md_list = h_pt_list = h_counts = h_best_slot = nullptr;
-        h_best = h_err = h_score1 = nullptr;
+        h_samples = nullptr;
+        h_res = nullptr;
+        h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
         h_model1 = nullptr;
         for (auto &sl : sweep_slot) sl.release();
@@ -370,12 +376,9 @@ struct DeviceCtx {
         MP_HIP(hipSetDevice(device));
         MP_HIP(hipMalloc(&d_pair, sizeof(double) * 8 * nn));
         MP_HIP(hipMalloc(&d_err, sizeof(double) * 3 * nn));
-        MP_HIP(hipMalloc(&d_samples, sizeof(int) * 8 * bb));
-        MP_HIP(hipMalloc(&d_md_list, sizeof(int) * bb));
-        MP_HIP(hipMalloc(&d_pt_list, sizeof(int) * bb));
+        MP_HIP(hipMalloc(&d_samples, sizeof(int) * 9 * bb));
         MP_HIP(hipMalloc(&d_counts, sizeof(int) * bb));
-        MP_HIP(hipMalloc(&d_best_slot, sizeof(int) * bb));
-        MP_HIP(hipMalloc(&d_best, sizeof(double) * bb));
+        MP_HIP(hipMalloc(&d_res, sizeof(IterResult) * bb));
         MP_HIP(hipMalloc(&d_models, sizeof(Model) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_scores, sizeof(double) * (size_t)bb * mm));
@@ -386,12 +389,8 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb * kPtSlotStride));
         MP_HIP(hipMalloc(&d_score1, sizeof(double) * 64));
         // two slots each: the next batch is generated while the current one is in flight
-        MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 8 * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_md_list, sizeof(int) * 2 * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_pt_list, sizeof(int) * 2 * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_counts, sizeof(int) * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_best_slot, sizeof(int) * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_best, sizeof(double) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 9 * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_res, sizeof(IterResult) * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_err, sizeof(double) * 3 * nn, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
@@ -954,13 +953,10 @@ class Run {
         const double b = batch_s_ / std::max(draw_s_per_it_, 1e-9);
         return std::min<uint32_t>(want, (uint32_t)std::max<double>(min_batch_, std::min<double>(b, 1e9)));
     }
-    int *slot_ptr(int which, int slot) const {
-        const size_t so = (size_t)slot * max_batch_;
-        return which == 0 ? X_.h_samples + 8 * so : which == 1 ? X_.h_md_list + so : X_.h_pt_list + so;
-    }
+    int *slot_ptr(int slot) const { return X_.h_samples + (size_t)slot * 9 * max_batch_; }
     void generate(Batch &g, uint32_t B, int slot) {
         auto t0 = Clock::now();
-        draw_batch(rs_, g, B, slot, slot_ptr(0, slot), slot_ptr(1, slot), slot_ptr(2, slot), nullptr);
+        draw_batch(rs_, g, B, slot, slot_ptr(slot), nullptr);
         sample_s_ += secs(t0);
     }
     // both streams to the end of iteration j of batch g
@@ -983,31 +979,27 @@ class Run {
         hipStream_t s = X_.stream;
         const bool prof = g_prof_on.load(std::memory_order_relaxed);
         batch_prof_ = prof;
-        const size_t so = (size_t)g.slot * max_batch_;
-        MP_HIP(hipMemcpyAsync(X_.d_samples, X_.h_samples + 8 * so, sizeof(int) * 8 * B, hipMemcpyHostToDevice, s));
-        MP_HIP(hipMemcpyAsync(X_.d_md_list, X_.h_md_list + so, sizeof(int) * std::max(nmd, 1), hipMemcpyHostToDevice, s));
-        MP_HIP(hipMemcpyAsync(X_.d_pt_list, X_.h_pt_list + so, sizeof(int) * std::max(npt, 1), hipMemcpyHostToDevice, s));
+        // one upload: samples, then the MD list and the (descending) point list
+        MP_HIP(hipMemcpyAsync(X_.d_samples, slot_ptr(g.slot), sizeof(int) * 9 * (size_t)B, hipMemcpyHostToDevice, s));
+        const int *d_md_list = X_.d_samples + 8 * (size_t)B, *d_pt_list = d_md_list + nmd;
         if (prof) MP_HIP(hipEventRecord(X_.ev[0], s));
         // MD iterations on the side stream, point iterations on the main one (they
         // write disjoint model slots); scoring waits for both
         if (nmd > 0) {
             MP_HIP(hipEventRecord(X_.ev_fork, s));
             MP_HIP(hipStreamWaitEvent(X_.md_stream, X_.ev_fork, 0));
-            MP_HIP(launch_md_solve(X_.md_stream, D_, P_.C, X_.d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs,
+            MP_HIP(launch_md_solve(X_.md_stream, D_, P_.C, d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs,
                                    X_.d_counts, maxm_));
             MP_HIP(hipEventRecord(X_.ev_join, X_.md_stream));
         }
         const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid};
-        MP_HIP(launch_pt_solve(s, D_, P_.C, X_.d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
+        MP_HIP(launch_pt_solve(s, D_, P_.C, d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
                                maxm_));
         if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
         if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
-        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_best,
-                                  X_.d_best_slot));
+        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res));
         if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
-        MP_HIP(hipMemcpyAsync(X_.h_best, X_.d_best, sizeof(double) * B, hipMemcpyDeviceToHost, s));
-        MP_HIP(hipMemcpyAsync(X_.h_best_slot, X_.d_best_slot, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-        MP_HIP(hipMemcpyAsync(X_.h_counts, X_.d_counts, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        MP_HIP(hipMemcpyAsync(X_.h_res, X_.d_res, sizeof(IterResult) * B, hipMemcpyDeviceToHost, s));
     }
 
     Model fetch_model(int b, int slot) {
@@ -1124,8 +1116,7 @@ void Run::run(Model *best, Stats *S) {
                                                           (uint64_t)max_batch_,
                                                           std::max<uint64_t>((uint64_t)min_batch_, 4ull * it_next)))
                                 : 0;
-        if (Bn > 0) X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(0, cur ^ 1), slot_ptr(1, cur ^ 1),
-                                      slot_ptr(2, cur ^ 1));
+        if (Bn > 0) X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(cur ^ 1));
         auto tw = Clock::now();
         MP_HIP(hipStreamSynchronize(X_.stream));
         S->seconds_gpu_wait += secs(tw);
@@ -1136,7 +1127,7 @@ void Run::run(Model *best, Stats *S) {
             MP_HIP(hipEventElapsedTime(&ms_solve, X_.ev[0], X_.ev[1]));
             MP_HIP(hipEventElapsedTime(&ms_score, X_.ev[1], X_.ev[2]));
             uint64_t h = 0;
-            for (uint32_t q = 0; q < B; ++q) h += (uint64_t)X_.h_counts[q];
+            for (uint32_t q = 0; q < B; ++q) h += (uint64_t)X_.h_res[q].count;
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.batches += 1;
             g_prof.iterations += B;
@@ -1154,17 +1145,17 @@ void Run::run(Model *best, Stats *S) {
             const uint32_t iter = it + j;
             const int st = g.types[j];
             S->num_iterations_per_solver[st] += 1;
-            const int nm = X_.h_counts[j];
+            const int nm = X_.h_res[j].count;
             S->num_hypotheses += (uint64_t)nm;
             bool lo_here = false;
             if (nm > 0) {
-                const double bl = X_.h_best[j];
+                const double bl = X_.h_res[j].best;
                 if (bl < best_min_score || iter == lo_start) {
                     const bool new_best = bl < best_min_score;
                     if (new_best) {
                         if (trace_) std::fprintf(stderr, "[engine] it=%u new best %.17g (solver %d, %d models)\n", iter, bl, st, nm);
                         best_min_score = bl;
-                        best_min = fetch_model((int)j, X_.h_best_slot[j]);
+                        best_min = fetch_model((int)j, X_.h_res[j].slot);
                         update_best(best_min_score, best_min, st, &S->best_model_score, best, &S->best_solver_type);
                     }
                     const bool run_lo = iter >= lo_start && best_min_score < kMax;
@@ -1184,8 +1175,8 @@ void Run::run(Model *best, Stats *S) {
                                     (uint64_t)max_batch_, std::max<uint64_t>((uint64_t)min_batch_, 4ull * at));
                                 const int slot = cur ^ 1;
                                 Batch *gs = &gen[slot];
-                                X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(0, slot),
-                                                  slot_ptr(1, slot), slot_ptr(2, slot), [this, gs] { launch_batch(*gs); });
+                                X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(slot),
+                                                  [this, gs] { launch_batch(*gs); });
                                 spec = true;
                                 spec_draws = sel_end.draws();
                             };

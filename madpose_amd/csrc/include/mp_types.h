@@ -69,6 +69,14 @@ struct PairData {
     const double *r0, *r1;                          // 1/|K^-1 x| (CAL bearings), else unused
 };
 
+// Per-iteration outcome of a batch (score_batch): the iteration's best score
+// (GetBestEstimatedModelId), its model slot and the number of models -- one 16-byte
+// record, so a batch's results come back in one copy.
+struct IterResult {
+    double best;
+    int slot, count;
+};
+
 constexpr int kMaxModelsCal = 10; // MD <= 4, 5pt <= 10
 constexpr int kMaxModelsSF = 16;  // MD <= 8, 6pt <= 15
 constexpr int kMaxModelsTF = 4;   // MD <= 4, 7pt <= 3

@@ -28,9 +28,9 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                            const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
                            int maxm);
 // scoring sweep: one workgroup per iteration, every model of the iteration scored
-// over all correspondences; per-iteration argmin (first minimum wins).
+// over all correspondences; per-iteration argmin (first minimum wins) into res[b].
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
-                              const int *counts, int nb, int maxm, double *scores, double *best, int *best_slot);
+                              const int *counts, int nb, int maxm, double *scores, IterResult *res);
 // single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);

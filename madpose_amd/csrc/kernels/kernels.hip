@@ -474,14 +474,11 @@ template <int V, int MAXM>
 __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairConst C,
                                                              const ScoreRec *__restrict__ recs,
                                                              const int *__restrict__ counts, double *scores,
-                                                             double *best, int *best_slot) {
+                                                             IterResult *res) {
     const int b = blockIdx.x;
     const int nm = counts[b];
     if (nm == 0) {
-        if (threadIdx.x == 0) {
-            best[b] = DBL_MAX;
-            best_slot[b] = 0;
-        }
+        if (threadIdx.x == 0) res[b] = IterResult{DBL_MAX, 0, 0};
         return;
     }
     const ScoreRec *R = recs + (size_t)b * MAXM;
@@ -524,8 +521,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                 bi = m;
             }
         }
-        best[b] = bs;
-        best_slot[b] = bi;
+        res[b] = IterResult{bs, bi, nm};
     }
 }
 
@@ -879,15 +875,15 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
 }
 
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
-                              const int *counts, int nb, int maxm, double *scores, double *best, int *best_slot) {
+                              const int *counts, int nb, int maxm, double *scores, IterResult *res) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
     if (C.variant == kCal)
-        score_batch_kernel<kCal, kMaxModelsCal><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, best, best_slot);
+        score_batch_kernel<kCal, kMaxModelsCal><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
     else if (C.variant == kSF)
-        score_batch_kernel<kSF, kMaxModelsSF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, best, best_slot);
+        score_batch_kernel<kSF, kMaxModelsSF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
     else
-        score_batch_kernel<kTF, kMaxModelsTF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, best, best_slot);
+        score_batch_kernel<kTF, kMaxModelsTF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
     return hipGetLastError();
 }
 
