@@ -184,6 +184,15 @@ def test_calibrated_estimator_parity(seed):
     _assert_parity(*_run_both(p, o, c, 0))
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_large_pair_parity(variant):
+    # N = 9000: the LO sweeps span 36 workgroups (one completion flag each) and the
+    # batches carry every kernel at a larger size than the other parity cases
+    p = synthetic.make_pair(11 + variant, n=9000)
+    o, c = synthetic.example_options("calibrated" if variant == 0 else "shared_focal", iterations=150)
+    _assert_parity(*_run_both(p, o, c, variant))
+
+
 @pytest.mark.parametrize("solver,score,lo", [(2, 0, 0), (1, 0, 0), (0, 1, 0), (0, 2, 2), (0, 0, 1)])
 def test_calibrated_estimator_config_modes(solver, score, lo):
     p = synthetic.make_pair(7, n=300)
