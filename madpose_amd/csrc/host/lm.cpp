@@ -102,15 +102,22 @@ struct Acc {
 // way, so the result does not depend on the pool.
 constexpr size_t kChunk = 256;
 constexpr size_t kPoolBlocks = 2048;
+// Workers spin (with pause) for a while after each job before they block on the
+// condition variable: the evaluations of one LM follow each other within
+// microseconds, and a futex wake-up per evaluation would cost about as much as the
+// evaluation's share per thread.  MADPOSE_LO_SPIN=0: block right away.
 class Pool {
   public:
     explicit Pool(int n) {
+        const char *e = std::getenv("MADPOSE_LO_SPIN");
+        spin_ = (e && e[0] == '0') ? 0 : 20000;
         for (int i = 0; i < n - 1; ++i) th_.emplace_back([this] { loop(); });
     }
     ~Pool() {
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto &t : th_) t.join();
@@ -127,32 +134,55 @@ class Pool {
             f_ = &f;
             n_ = n;
             next_.store(0);
-            active_ = (int)th_.size();
-            ++gen_;
+            active_.store((int)th_.size(), std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         work();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return active_ == 0; });
+        // the workers' share: spin, then block
+        for (int k = 0; active_.load(std::memory_order_acquire) != 0; ++k) {
+            if (k < spin_) {
+                pause();
+            } else {
+                std::unique_lock<std::mutex> lk(mu_);
+                done_cv_.wait(lk, [this] { return active_.load(std::memory_order_acquire) == 0; });
+                break;
+            }
+        }
         f_ = nullptr;
     }
 
   private:
+    static void pause() {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
     void work() {
         for (size_t k; (k = next_.fetch_add(1)) < n_;) (*f_)(k);
     }
     void loop() {
         uint64_t seen = 0;
         for (;;) {
-            {
+            bool ready = false;
+            for (int k = 0; k < spin_ && !ready; ++k) {
+                ready = gen_.load(std::memory_order_acquire) != seen;
+                if (!ready) pause();
+            }
+            if (!ready) {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu_); // (pairs with run()'s publication)
                 if (stop_) return;
-                seen = gen_;
+                seen = gen_.load(std::memory_order_relaxed);
             }
             work();
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--active_ == 0) done_cv_.notify_one();
+            if (active_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> lk(mu_);
+                done_cv_.notify_one();
+            }
         }
     }
     std::vector<std::thread> th_;
@@ -161,9 +191,10 @@ class Pool {
     const std::function<void(size_t)> *f_ = nullptr;
     size_t n_ = 0;
     std::atomic<size_t> next_{0};
-    int active_ = 0;
-    uint64_t gen_ = 0;
+    std::atomic<int> active_{0};
+    std::atomic<uint64_t> gen_{0};
     bool stop_ = false;
+    int spin_ = 0;
 };
 
 Pool &lo_pool() {
