@@ -59,8 +59,52 @@ def _estimate(madpose, variant, args, o, c, device):
     return fn(*args, o, c, device=device)
 
 
-def cpu_baseline(wl, pair, budget_s=15.0):
-    """Scalar CPU oracle (kind "port") on a bounded iteration count of the same pair."""
+def host_cpu_info():
+    """nproc, the CPUs this process may run on, physical cores among them, lscpu model."""
+    import platform
+
+    aff = sorted(os.sched_getaffinity(0))
+    model, tpc = platform.processor() or "unknown", 1
+    try:
+        with open("/proc/cpuinfo") as f:
+            info = f.read()
+        for line in info.splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+        sib = [l for l in info.splitlines() if l.startswith("siblings")]
+        cores = [l for l in info.splitlines() if l.startswith("cpu cores")]
+        if sib and cores:
+            tpc = max(1, int(sib[0].split(":")[1]) // max(1, int(cores[0].split(":")[1])))
+    except OSError:
+        pass
+    share = len(aff)
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():  # the GPU box's CPU share per GPU
+        share = min(share, int(os.environ["OMP_NUM_THREADS"]))
+    return {"nproc": os.cpu_count(), "affinity_cpus": len(aff), "threads_per_core": tpc,
+            "physical_cores_used": max(1, share // tpc), "model": model}
+
+
+def _oracle_pair_run(job):
+    """One CPU-baseline process: the scalar oracle on one pair of the workload."""
+    wl_key, seed, it = job
+    import oracle
+    from madpose_amd import synthetic
+    from tests.helpers import oracle_cfg, oracle_opts
+
+    wl = WORKLOADS[wl_key]
+    pair = synthetic.config_pair(wl["config"], seed=seed)
+    o, c = synthetic.throughput_options(wl["kind"], iterations=it)
+    t0 = time.perf_counter()
+    _, st, _ = oracle.estimate(wl["variant"], *_pair_args(pair, wl["variant"]), oracle_opts(o), oracle_cfg(c))
+    return st.num_hypotheses, time.perf_counter() - t0
+
+
+def cpu_baseline(wl, pair, budget_s=15.0, procs=0):
+    """Scalar CPU oracle (kind "port", compiled like the reference: -O3, FMA contraction)
+    on a bounded iteration count of the workload: (1) one thread on the bench's own pair,
+    (2) one process per physical core of this host's CPU share, each on its own pair
+    (independent pairs).  `value` is the all-core aggregate."""
     try:
         import oracle
         from tests.helpers import oracle_cfg, oracle_opts
@@ -77,9 +121,26 @@ def cpu_baseline(wl, pair, budget_s=15.0):
         if dt >= budget_s / 3 or it >= wl["iterations"]:
             break
         it = min(wl["iterations"], int(it * max(2.0, budget_s / max(dt, 1e-3))))
-    return {"value": st.num_hypotheses / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
-            "sample": f"same pair, {it} iterations (min=max=per-solver cap), single thread, {dt:.1f} s, "
-                      f"{st.num_hypotheses} hypotheses, {st.number_lo_iterations} LO runs"}
+    single = {"value": st.num_hypotheses / dt, "cores": 1,
+              "sample": f"same pair, {it} iterations (min=max=per-solver cap), single thread, {dt:.1f} s, "
+                        f"{st.num_hypotheses} hypotheses, {st.number_lo_iterations} LO runs"}
+    host = host_cpu_info()
+    p = procs or host["physical_cores_used"]
+    key = [k for k, v in WORKLOADS.items() if v is wl][0]
+    import multiprocessing as mp
+
+    jobs = [(key, 900000 + j, it) for j in range(p)]
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(p) as pool:
+        got = pool.map(_oracle_pair_run, jobs)
+    wall = time.perf_counter() - t0
+    hyps = sum(h for h, _ in got)
+    inner = max(d for _, d in got)
+    return {"value": hyps / inner, "unit": "hypotheses/s", "cores": p, "kind": "port",
+            "sample": f"{p} processes (one per physical core of the host's CPU share), each the oracle on its own "
+                      f"pair of the workload for {it} iterations; {hyps} hypotheses over the slowest process's "
+                      f"{inner:.1f} s ({wall:.1f} s with process start-up)",
+            "single_thread": single, "host": host}
 
 
 def pmc_traffic_model():
@@ -223,15 +284,17 @@ def summarize_scannet(allv, errs, wl, steps, warmup, world, total):
     }
 
 
-def cpu_baseline_pairs(wl, pairs, budget_s):
-    """The scalar CPU oracle on as many of the rank's pairs as fit in budget_s."""
-    try:
-        import oracle
-        from tests.helpers import oracle_cfg, oracle_opts
-        from madpose_amd import synthetic
-    except Exception as e:
-        return {"value": None, "unit": "pairs/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+def _oracle_pairs_run(job):
+    """One CPU-baseline process of the ScanNet stand-in: the oracle on its pairs until
+    the budget is spent; returns (pairs done, seconds)."""
+    wl_key, seeds, budget_s = job
+    import oracle
+    from madpose_amd import synthetic
+    from tests.helpers import oracle_cfg, oracle_opts
+
+    wl = WORKLOADS[wl_key]
     o, c = synthetic.example_options(wl["kind"], iterations=wl["iterations"])
+    pairs = [synthetic.scannet_pair(s) for s in seeds]
     t0 = time.perf_counter()
     k = 0
     for p in pairs:
@@ -239,126 +302,279 @@ def cpu_baseline_pairs(wl, pairs, budget_s):
         k += 1
         if time.perf_counter() - t0 >= budget_s:
             break
-    dt = time.perf_counter() - t0
-    return {"value": k / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"first {k} pairs of the set, single thread, {dt:.1f} s"}
+    return k, time.perf_counter() - t0
 
 
-def run_scannet(a, wl, world, rank, dev, barrier):
-    import madpose_amd as madpose
+def cpu_baseline_pairs(wl, seeds, budget_s, procs=0):
+    """The scalar CPU oracle on the rank's pairs: one thread on the first pairs that fit
+    in budget_s, and one process per physical core over disjoint pairs for budget_s each."""
+    try:
+        import oracle  # noqa: F401
+    except Exception as e:
+        return {"value": None, "unit": "pairs/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+    k, dt = _oracle_pairs_run(("scannet", seeds, budget_s / 2))
+    single = {"value": k / dt, "cores": 1, "sample": f"first {k} pairs of the set, single thread, {dt:.1f} s"}
+    host = host_cpu_info()
+    p = procs or host["physical_cores_used"]
+    import multiprocessing as mp
+
+    jobs = [("scannet", seeds[j::p][:64], budget_s / 2) for j in range(p)]
+    with mp.get_context("spawn").Pool(p) as pool:
+        got = pool.map(_oracle_pairs_run, jobs)
+    done = sum(g[0] for g in got)
+    rate = sum(g[0] / g[1] for g in got)
+    return {"value": rate, "unit": "pairs/s", "cores": p, "kind": "port",
+            "sample": f"{p} processes (one per physical core of the host's CPU share) over disjoint pairs of the "
+                      f"set, {done} pairs in {budget_s / 2:.1f} s each; value = sum of per-process rates",
+            "single_thread": single, "host": host}
+
+
+RECORD_FIELDS = (["seed"] + [f"R{i}{j}" for i in range(3) for j in range(3)] + ["t0", "t1", "t2", "scale", "offset0",
+                 "offset1", "focal0", "focal1", "num_iterations_total", "best_num_inliers", "best_model_score",
+                 "number_lo_iterations", "err_R_deg", "err_t_deg"])
+
+
+def result_record(seed, model, stats, pair):
+    """One fixed-size result record per pair (pose + stats), the unit
+    the ranks exchange at the end: seed, R, t, scale, offsets, focal(s), iteration and
+    inlier counts, score, LO count, and the pose error against the synthetic ground truth
+    (madpose/utils.py:59-78 compute_pose_error)."""
+    from madpose_amd import utils
+
+    R, t = np.asarray(model.R(), dtype=np.float64), np.asarray(model.t(), dtype=np.float64)
+    f0 = getattr(model, "focal0", getattr(model, "focal", np.nan))
+    f1 = getattr(model, "focal1", getattr(model, "focal", np.nan))
+    et, eR = utils.compute_pose_error(pair["T_0to1"], R, t)
+    rec = ([float(seed)] + list(R.reshape(9)) + list(t.reshape(3)) +
+           [getattr(model, "scale", np.nan), getattr(model, "offset0", np.nan), getattr(model, "offset1", np.nan), f0,
+            f1, stats.num_iterations_total, stats.best_num_inliers, stats.best_model_score,
+            stats.number_lo_iterations, eR, et])
+    assert len(rec) == len(RECORD_FIELDS)
+    return rec
+
+
+def gather_records(recs, per_rank, world):
+    """All ranks' result records (one all_gather over RCCL / gloo). Ranks own different
+    numbers of pairs, so each pads to per_rank rows with NaN; padding is dropped."""
+    w = len(RECORD_FIELDS)
+    local = np.full((per_rank, w), np.nan)
+    if recs:
+        local[: len(recs)] = np.asarray(recs, dtype=np.float64)
+    allr = gather_counters(local.reshape(-1).tolist(), world).reshape(world * per_rank, w)
+    return allr[np.isfinite(allr[:, 0])]
+
+
+def records_summary(recs):
+    """What rank 0 reports about the gathered records."""
+    seeds = recs[:, 0]
+    err = np.maximum(recs[:, RECORD_FIELDS.index("err_R_deg")], recs[:, RECORD_FIELDS.index("err_t_deg")])
+    return {"records": int(len(recs)), "record_doubles": len(RECORD_FIELDS),
+            "pairs_disjoint": bool(len(np.unique(seeds)) == len(seeds)),
+            "median_pose_err_deg": float(np.median(err)) if len(err) else None}
+
+
+def shard_scannet(total, world, rank):
+    """configs[4] pairs of this rank: longest-processing-time-first over the pair sizes
+    (work ~ N x iterations); deterministic, every rank computes the same
+    assignment, and the pair of seed s is the same on whichever rank draws it."""
+    from madpose_amd import synthetic
+
+    sizes = [synthetic.scannet_size(s) for s in range(total)]
+    load = [0] * world
+    owner = [0] * total
+    for s in sorted(range(total), key=lambda s: (-sizes[s], s)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        owner[s] = r
+        load[r] += sizes[s]
+    return [s for s in range(total) if owner[s] == rank]
+
+
+def run_scannet(a, wl, world, rank, dev, barrier, eng):
     from madpose_amd import synthetic
 
     total = a.pairs or wl["pairs"]
-    seeds = list(range(rank, total, world))
+    seeds = shard_scannet(total, world, rank)
     pairs = [synthetic.scannet_pair(s) for s in seeds]
     o, c = synthetic.example_options(wl["kind"], iterations=wl["iterations"])
     for _ in range(a.warmup):
-        madpose.estimate_batch(wl["variant"], pairs[: min(len(pairs), 2 * a.streams)], o, c, device=dev,
-                               num_streams=a.streams)
+        eng.estimate_batch(wl["variant"], pairs[: min(len(pairs), 2 * a.streams)], o, c, device=dev,
+                           num_streams=a.streams)
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        res = madpose.estimate_batch(wl["variant"], pairs, o, c, device=dev, num_streams=a.streams)
+        res = eng.estimate_batch(wl["variant"], pairs, o, c, device=dev, num_streams=a.streams)
     barrier()
     elapsed = time.perf_counter() - t0
-    errs = pair_errors(res, pairs)
+    recs = [result_record(s, m, st, p) for s, (m, st), p in zip(seeds, res, pairs)]
     local = [elapsed, float(len(pairs) * a.steps), float(sum(st.num_hypotheses for _, st in res) * a.steps),
              float(sum(st.num_iterations_total for _, st in res) * a.steps)]
     allv = gather_counters(local, world)
-    per = (total + world - 1) // world
-    errs_all = gather_counters(errs + [np.nan] * (per - len(errs)), world).reshape(-1)
+    per = (total + world - 1) // world + 1
+    allr = gather_records(recs, per, world)
     if rank == 0:
-        out = summarize_scannet(allv, errs_all, wl, a.steps, a.warmup, world, total)
+        errs = np.maximum(allr[:, RECORD_FIELDS.index("err_R_deg")], allr[:, RECORD_FIELDS.index("err_t_deg")])
+        out = summarize_scannet(allv, errs, wl, a.steps, a.warmup, world, total)
+        out["results"] = records_summary(allr)
         if world == 1 and a.cpu_budget > 0:
-            out["cpu_baseline"] = cpu_baseline_pairs(wl, pairs, a.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline_pairs(wl, seeds, a.cpu_budget, a.cpu_procs)
         print(json.dumps(out), flush=True)
 
 
-def main():
+class _Engine:
+    """The product path: madpose_amd through the C ABI on the HIP device."""
+
+    def __init__(self):
+        import madpose_amd
+
+        self.m = madpose_amd
+
+    def estimate(self, variant, args, o, c, device):
+        return _estimate(self.m, variant, args, o, c, device)
+
+    def estimate_batch(self, *args, **kw):
+        return self.m.estimate_batch(*args, **kw)
+
+    def profile_reset(self):
+        self.m.profile_reset()
+
+    def profile_enable(self, on):
+        self.m.profile_enable(on)
+
+    def profile_read(self):
+        return self.m.profile_read()
+
+
+def _engine(a):
+    if a.engine_module:  # tests only: a CPU stand-in that drives the sharding / gather plumbing
+        import importlib
+
+        return importlib.import_module(a.engine_module).Engine()
+    return _Engine()
+
+
+def spawn_ranks(n, argv):
+    """--gpus N without a launcher: start N child processes of this script, one per GPU
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), before anything in
+    this process touches the GPU, and exit with the worst child status."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one process per GPU); default: WORLD_SIZE or 1")
     # defaults: 40 / 4 pairs for the single-pair workloads (about 0.5 s timed, so the
     # host LO's jitter averages out), 10 / 2 passes over the pair set for scannet
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cal")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU oracle work (0 = skip)")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="processes of the all-core CPU baseline leg (0 = one per physical core)")
     ap.add_argument("--pairs", type=int, default=0, help="scannet: total pairs (default 1500)")
     ap.add_argument("--streams", type=int, default=8, help="scannet: pairs in flight per GPU")
-    a = ap.parse_args()
+    ap.add_argument("--engine-module", default=None, help=argparse.SUPPRESS)
+    a = ap.parse_args(argv)
     if a.steps is None:
         a.steps = 10 if a.workload == "scannet" else 40
     if a.warmup is None:
         a.warmup = 2 if a.workload == "scannet" else 4
     wl = WORKLOADS[a.workload]
 
+    if "WORLD_SIZE" not in os.environ and a.gpus is not None and a.gpus > 1:
+        return spawn_ranks(a.gpus, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus is not None and a.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
     import torch.distributed as dist
 
-    import madpose_amd as madpose
     from madpose_amd import synthetic
 
+    eng = _engine(a)
+    gpu = a.engine_module is None and torch.cuda.is_available()
     if world > 1:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = "nccl" if gpu else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend=backend)
-    dev = local_rank if torch.cuda.is_available() else 0
+    dev = local_rank if gpu else 0
 
     def barrier():
         if world > 1:
             dist.barrier()
-        if torch.cuda.is_available():
+        if gpu:
             torch.cuda.synchronize()
 
     if a.workload == "scannet":
-        run_scannet(a, wl, world, rank, dev, barrier)
+        run_scannet(a, wl, world, rank, dev, barrier, eng)
         if world > 1:
             dist.destroy_process_group()
-        return
+        return 0
 
-    # per-rank pairs, generated before timing (weak scaling: one pair per rank per step)
+    # per-rank pairs, generated before timing (weak scaling: one pair per rank per step;
+    # rank r owns seeds r*1000 + k, disjoint across ranks)
     n_pairs = a.warmup + a.steps
-    pairs = [synthetic.config_pair(wl["config"], seed=rank * 1000 + k) for k in range(n_pairs)]
+    seeds = [rank * 1000 + k for k in range(n_pairs)]
+    pairs = [synthetic.config_pair(wl["config"], seed=s) for s in seeds]
     o, c = synthetic.throughput_options(wl["kind"], iterations=wl["iterations"])
 
     for k in range(a.warmup):
-        _estimate(madpose, wl["variant"], _pair_args(pairs[k], wl["variant"]), o, c, dev)
+        eng.estimate(wl["variant"], _pair_args(pairs[k], wl["variant"]), o, c, dev)
 
-    madpose.profile_reset()
-    madpose.profile_enable(True)
+    eng.profile_reset()
+    eng.profile_enable(True)
     hyps = iters = lo = 0
     t_lo = 0.0
+    res = []
     barrier()
     t0 = time.perf_counter()
     for k in range(a.warmup, n_pairs):
-        _, st = _estimate(madpose, wl["variant"], _pair_args(pairs[k], wl["variant"]), o, c, dev)
+        m, st = eng.estimate(wl["variant"], _pair_args(pairs[k], wl["variant"]), o, c, dev)
+        res.append((m, st))
         hyps += st.num_hypotheses
         iters += st.num_iterations_total
         lo += st.number_lo_iterations
         t_lo += st.seconds_lo
     barrier()
     elapsed = time.perf_counter() - t0
-    madpose.profile_enable(False)
-    prof = madpose.profile_read()
+    eng.profile_enable(False)
+    prof = eng.profile_read()
 
+    recs = [result_record(seeds[a.warmup + k], m, st, pairs[a.warmup + k]) for k, (m, st) in enumerate(res)]
     local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
              prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
              prof["sweep_wall_ms"], prof["iterations"], prof["sample_wall_ms"], prof["wait_wall_ms"],
              prof["run_wall_ms"], prof["lm_blocks"], prof["lm_big_calls"], prof["lm_big_wall_ms"]]
     allv = gather_counters(local, world)
+    allr = gather_records(recs, a.steps, world)
     if rank == 0:
-        res = summarize(allv, wl, a.steps, a.warmup, world)
+        out = summarize(allv, wl, a.steps, a.warmup, world)
+        out["results"] = records_summary(allr)
         if world == 1 and a.cpu_budget > 0:
-            res["cpu_baseline"] = cpu_baseline(wl, pairs[a.warmup], a.cpu_budget)
-        print(json.dumps(res), flush=True)
+            out["cpu_baseline"] = cpu_baseline(wl, pairs[a.warmup], a.cpu_budget, a.cpu_procs)
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

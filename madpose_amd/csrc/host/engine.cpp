@@ -1176,7 +1176,12 @@ void Run::run(Model *best, Stats *S) {
                                 const int slot = cur ^ 1;
                                 Batch *gs = &gen[slot];
                                 X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(slot),
-                                                  [this, gs] { launch_batch(*gs); });
+                                                  [this, gs] {
+                                                      // the sampler thread is not bound to the
+                                                      // estimator's device by itself
+                                                      MP_HIP(hipSetDevice(X_.device));
+                                                      launch_batch(*gs);
+                                                  });
                                 spec = true;
                                 spec_draws = sel_end.draws();
                             };

@@ -1,6 +1,7 @@
 // Host LM for LO -- see lm.h.
 #include "lm.h"
 
+#include <chrono>
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -105,12 +106,14 @@ constexpr size_t kPoolBlocks = 2048;
 // Workers spin (with pause) for a while after each job before they block on the
 // condition variable: the evaluations of one LM follow each other within
 // microseconds, and a futex wake-up per evaluation would cost about as much as the
-// evaluation's share per thread.  MADPOSE_LO_SPIN=0: block right away.
+// evaluation's share per thread.  The spin is bounded by time, not by a pause count
+// (pause latency differs ~10x across x86 generations): MADPOSE_LO_SPIN = microseconds
+// (default 100; 0 = block right away).
 class Pool {
   public:
     explicit Pool(int n) {
         const char *e = std::getenv("MADPOSE_LO_SPIN");
-        spin_ = (e && e[0] == '0') ? 0 : 20000;
+        spin_ns_ = (e ? std::max(0, std::atoi(e)) : 100) * 1000ll;
         for (int i = 0; i < n - 1; ++i) th_.emplace_back([this] { loop(); });
     }
     ~Pool() {
@@ -140,14 +143,9 @@ class Pool {
         cv_.notify_all();
         work();
         // the workers' share: spin, then block
-        for (int k = 0; active_.load(std::memory_order_acquire) != 0; ++k) {
-            if (k < spin_) {
-                pause();
-            } else {
-                std::unique_lock<std::mutex> lk(mu_);
-                done_cv_.wait(lk, [this] { return active_.load(std::memory_order_acquire) == 0; });
-                break;
-            }
+        if (!spin_until([this] { return active_.load(std::memory_order_acquire) == 0; })) {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_cv_.wait(lk, [this] { return active_.load(std::memory_order_acquire) == 0; });
         }
         f_ = nullptr;
     }
@@ -158,17 +156,26 @@ class Pool {
         __builtin_ia32_pause();
 #endif
     }
+    // polls ready() with pause for at most spin_ns_; true once it held
+    template <class F> bool spin_until(const F &ready) const {
+        if (spin_ns_ <= 0) return ready();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0;; ++k) {
+            if (ready()) return true;
+            pause();
+            if ((k & 63) == 63 &&
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
+                    spin_ns_)
+                return ready();
+        }
+    }
     void work() {
         for (size_t k; (k = next_.fetch_add(1)) < n_;) (*f_)(k);
     }
     void loop() {
         uint64_t seen = 0;
         for (;;) {
-            bool ready = false;
-            for (int k = 0; k < spin_ && !ready; ++k) {
-                ready = gen_.load(std::memory_order_acquire) != seen;
-                if (!ready) pause();
-            }
+            const bool ready = spin_until([&] { return gen_.load(std::memory_order_acquire) != seen; });
             if (!ready) {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
@@ -194,7 +201,7 @@ class Pool {
     std::atomic<int> active_{0};
     std::atomic<uint64_t> gen_{0};
     bool stop_ = false;
-    int spin_ = 0;
+    long long spin_ns_ = 0;
 };
 
 Pool &lo_pool() {

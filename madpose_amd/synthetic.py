@@ -91,12 +91,16 @@ def config_pair(config, seed=0):
     raise ValueError(config)
 
 
+def scannet_size(seed, n_range=(1500, 2500)):
+    """Correspondence count of the configs[4] pair of this seed (cheap: no pair is built)."""
+    return int(np.random.default_rng([7, seed]).integers(n_range[0], n_range[1] + 1))
+
+
 def scannet_pair(seed, n_range=(1500, 2500)):
     """configs[4] stand-in (ScanNet-1500): a shared-focal pair
     with ScanNet intrinsics (f = 577.87, pp = ((W-1)/2, (H-1)/2)) and N ~ U{1500..2500}
     correspondences; the pair of seed s is the same whatever rank or batch draws it."""
-    n = int(np.random.default_rng([7, seed]).integers(n_range[0], n_range[1] + 1))
-    return make_pair(seed, n=n)
+    return make_pair(seed, n=scannet_size(seed, n_range))
 
 
 def example_options(kind="calibrated", iterations=1000, min_iterations=100):

@@ -80,3 +80,71 @@ def test_scannet_summary_and_gathered_errors():
     assert res["pose_auc"]["pairs"] == 5
     ref = utils.pose_auc(errs[:5], (5, 10, 20))
     assert [res["pose_auc"][k] for k in ("5", "10", "20")] == ref
+
+
+def _run_bench(args, timeout=600):
+    import json
+    import subprocess
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+def test_gpus_flag_spawns_ranks_and_gathers_records():
+    """bench.py --gpus 2 with no launcher starts two ranks (gloo on CPU), each estimating
+    its own pairs through main()'s sharding path; rank 0 reports n_gpus 2 and the
+    gathered per-pair records of both ranks, rank-disjoint."""
+    res = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--cpu-budget", "0", "--engine-module",
+                      "tests.bench_stub_engine"])
+    assert res["n_gpus"] == 2
+    assert res["results"]["records"] == 6 and res["results"]["pairs_disjoint"]
+    assert res["value"] > 0 and res["scaling"] == "weak"
+
+
+def test_gpus_flag_scannet_shards_all_pairs():
+    res = _run_bench(["--gpus", "2", "--workload", "scannet", "--pairs", "9", "--steps", "1", "--warmup", "0",
+                      "--cpu-budget", "0", "--engine-module", "tests.bench_stub_engine"])
+    assert res["n_gpus"] == 2 and res["config"]["pairs"] == 9
+    assert res["results"]["records"] == 9 and res["results"]["pairs_disjoint"]
+    assert res["pose_auc"]["pairs"] == 9
+
+
+def test_gpus_mismatch_fails_loudly():
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--engine-module",
+                        "tests.bench_stub_engine"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_scannet_sharding_is_a_balanced_partition():
+    sys.path.insert(0, ROOT)
+    import bench
+    from madpose_amd import synthetic
+
+    total, world = 1500, 8
+    parts = [bench.shard_scannet(total, world, r) for r in range(world)]
+    allp = sorted(s for p in parts for s in p)
+    assert allp == list(range(total))
+    loads = [sum(synthetic.scannet_size(s) for s in p) for p in parts]
+    assert max(loads) - min(loads) <= 2500  # LPT: within one pair of each other
+
+
+def test_records_summary_and_gather_single_rank():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    w = len(bench.RECORD_FIELDS)
+    recs = [[float(s)] + [0.0] * (w - 3) + [float(s), 2.0 * s] for s in range(4)]
+    allr = bench.gather_records(recs, 6, 1)
+    assert allr.shape == (4, w)
+    s = bench.records_summary(allr)
+    assert s["records"] == 4 and s["pairs_disjoint"] and s["median_pose_err_deg"] == np.median([0, 2, 4, 6])

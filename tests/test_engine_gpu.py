@@ -262,6 +262,41 @@ def test_example_pair_runs():
     _assert_parity(pose, st, om, ost, oinl)
 
 
+def test_two_focal_example_pair_parity():
+    """The reference's two-focal example (examples/two_focal.py:20-100) on its own
+    2_2d3ds pair (782 MASt3R matches, DepthAnything priors looked up by the reference's
+    get_depths): GPU estimator against the oracle, plus the focal lengths."""
+    ex = np.load(os.path.join(GOLDEN, "example_pairs.npz"))
+    o, c = synthetic.example_options("two_focal", iterations=1000)
+    pp0 = (ex["2d3ds_img0_shape"][::-1].astype(np.float64) - 1) / 2
+    pp1 = (ex["2d3ds_img1_shape"][::-1].astype(np.float64) - 1) / 2
+    args = (ex["2d3ds_m0"], ex["2d3ds_m1"], ex["2d3ds_depth0"], ex["2d3ds_depth1"], ex["2d3ds_mindepth"], pp0, pp1)
+    pose, st = madpose.HybridEstimatePoseScaleOffsetTwoFocal(*args, o, c)
+    om, ost, oinl = oracle.estimate(2, *args, oracle_opts(o), oracle_cfg(c))
+    _assert_parity(pose, st, om, ost, oinl)
+    assert abs(pose.focal0 - om["focal0"]) <= 1e-8 * om["focal0"]
+    assert abs(pose.focal1 - om["focal1"]) <= 1e-8 * om["focal1"]
+    K0, K1 = ex["2d3ds_K0"], ex["2d3ds_K1"]
+    err_f = max(abs(pose.focal0 - K0[0, 0]) / K0[0, 0], abs(pose.focal1 - K1[0, 0]) / K1[0, 0])
+    err_t, err_R = madpose.utils.compute_pose_error(ex["2d3ds_T"], pose.R(), pose.t())
+    assert err_R < 10.0 and err_f < 0.5, (err_R, err_t, err_f)
+
+
+def test_nonzero_device_matches_device_zero():
+    """estimate(device=1) gives the same results as device 0 (every HIP call of the
+    engine, including the sampler thread's post-LO launches, runs on the estimator's
+    device).  Needs two visible GPUs."""
+    if madpose.device_count() < 2:
+        pytest.skip("one visible GPU")
+    p = synthetic.make_pair(5, n=800)
+    o, c = synthetic.example_options("calibrated", iterations=2000, min_iterations=2000)
+    outs = [madpose.HybridEstimatePoseScaleOffset(p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"],
+                                                  p["K0"], p["K1"], o, c, device=d) for d in (0, 1)]
+    (p0, s0), (p1, s1) = outs
+    assert np.array_equal(p0.pose, p1.pose) and s0.inlier_indices == s1.inlier_indices
+    assert s0.num_iterations_total == s1.num_iterations_total and s0.best_model_score == s1.best_model_score
+
+
 def test_invalid_inputs_raise():
     with pytest.raises(ValueError):
         madpose.HybridEstimatePoseScaleOffset(np.zeros((5, 2)), np.zeros((4, 2)), np.ones(5), np.ones(5), [0, 0],
