@@ -152,6 +152,12 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
 int mp_get_depths(int dtype, int32_t num_pairs, const void *depth_maps, const int64_t *dims, const int64_t *pt_offsets,
                   const double *keypoints, void *out, int device);
 
+/* bougnoux_focals (src/hybrid_pose_two_focal_estimator.cpp:11-32; numpy twin
+ * madpose/utils.py:25-56 bougnoux_numpy with p1 = p2 = 0): squared focal lengths
+ * (f0^2, f1^2) of k fundamental matrices F (k x 9, row-major) into out (k x 2), on
+ * the device with the same code the two-focal 7-point tail runs. */
+int mp_bougnoux_focals(int64_t k, const double *F, double *out, int device);
+
 /* Point minimal solver (PoseLib relpose_5pt, src/hybrid_pose_estimator.cpp:134) on unit bearings
  * (5 points, point-major 3 doubles each).  Returns count or -code. */
 int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device);

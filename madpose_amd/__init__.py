@@ -23,6 +23,7 @@ from .api import (  # noqa: F401
     device_count,
     estimate_batch,
     estimate_scale_and_pose,
+    bougnoux_focals_batch,
     get_depths_batch,
     profile_enable,
     profile_read,

@@ -120,6 +120,7 @@ EXPORTS = {
                                          ctypes.c_int]),
     "mp_get_depths": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_void_p, c_int64_p, c_int64_p, c_double_p,
                                      ctypes.c_void_p, ctypes.c_int]),
+    "mp_bougnoux_focals": (ctypes.c_int, [ctypes.c_int64, c_double_p, c_double_p, ctypes.c_int]),
     "mp_estimate_scale_and_pose": (ctypes.c_int, [c_double_p, c_double_p, c_double_p, ctypes.c_int64,
                                                   ctypes.POINTER(mp_model), ctypes.c_int]),
     "mp_solve_scale_and_shift": (ctypes.c_int, [ctypes.c_int, c_double_p, c_double_p, c_double_p, c_double_p,

@@ -415,6 +415,16 @@ def estimate_batch(variant, pairs, options, est_config=None, device=None, num_st
     return out
 
 
+def bougnoux_focals_batch(F, device=None):
+    """Squared Bougnoux focal lengths (f0^2, f1^2) of fundamental matrices F (k x 3 x 3,
+    principal points at the origin) on the device: the two-focal 7-point tail's own
+    code (src/hybrid_pose_two_focal_estimator.cpp:11-32; madpose/utils.py:25-56)."""
+    F = np.ascontiguousarray(np.asarray(F, dtype=np.float64).reshape(-1, 9))
+    out = np.zeros((len(F), 2))
+    L.check(L.lib().mp_bougnoux_focals(len(F), _dp(F), _dp(out), _DEFAULT_DEVICE if device is None else int(device)))
+    return out
+
+
 def get_depths_batch(images, depth_maps, mkpts, device=None):
     """madpose.utils.get_depths (madpose/utils.py:4-22) for many pairs in one device
     launch.  images: the images (only their shapes are used) or (h, w) tuples;

@@ -193,6 +193,14 @@ int mp_get_depths(int dtype, int32_t num_pairs, const void *depth_maps, const in
     });
 }
 
+int mp_bougnoux_focals(int64_t k, const double *F, double *out, int device) {
+    return guarded([&]() {
+        if (k < 0 || (k > 0 && (!F || !out))) throw std::invalid_argument("bad bougnoux arguments");
+        mp::bougnoux_batch(k, F, out, device);
+        return MP_OK;
+    });
+}
+
 int mp_estimate_scale_and_pose(const double *X, const double *Y, const double *W, int64_t n, mp_model *out,
                                int device) {
     return guarded([&]() {

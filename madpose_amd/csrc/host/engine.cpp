@@ -1458,6 +1458,21 @@ void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const
     for (void *p : {(void *)d_pair, (void *)d_cand, (void *)d_smp, (void *)d_list, (void *)d_n}) hipFree(p);
 }
 
+void bougnoux_batch(int64_t k, const double *F, double *out, int device) {
+    if (k <= 0) return;
+    CtxLease lease(device);
+    hipStream_t s = lease.c->stream;
+    double *d_F, *d_out;
+    MP_HIP(hipMalloc(&d_F, sizeof(double) * 9 * (size_t)k));
+    MP_HIP(hipMalloc(&d_out, sizeof(double) * 2 * (size_t)k));
+    MP_HIP(hipMemcpyAsync(d_F, F, sizeof(double) * 9 * (size_t)k, hipMemcpyHostToDevice, s));
+    MP_HIP(launch_bougnoux(s, d_F, k, d_out));
+    MP_HIP(hipMemcpyAsync(out, d_out, sizeof(double) * 2 * (size_t)k, hipMemcpyDeviceToHost, s));
+    MP_HIP(hipStreamSynchronize(s));
+    MP_HIP(hipFree(d_F));
+    MP_HIP(hipFree(d_out));
+}
+
 void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *dims, const int64_t *pt_off,
                       const double *pts, void *out, int device) {
     if (dtype != 0 && dtype != 1) throw std::invalid_argument("dtype must be 0 (float32) or 1 (float64)");

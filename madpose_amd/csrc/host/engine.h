@@ -77,6 +77,8 @@ void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device);
 // get_depths of num pairs on the device (see launch_get_depths); dims: num x 4
 // (depth-map h, w, image h, w); host buffers in and out
+// squared Bougnoux focals of k fundamental matrices (device kernel, mp_bougnoux_focals)
+void bougnoux_batch(int64_t k, const double *F, double *out, int device);
 void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *dims, const int64_t *pt_off,
                       const double *pts, void *out, int device);
 

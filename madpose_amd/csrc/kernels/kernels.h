@@ -55,6 +55,9 @@ hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *i
                             double *sols, int *nsols, Model *poses, int *nposes);
 hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes);
 
+// squared Bougnoux focals of k fundamental matrices (9 doubles each) into out (2 each)
+hipError_t launch_bougnoux(hipStream_t s, const double *F, int64_t k, double *out);
+
 // estimate_scale_and_pose over n points (in = X(3n) Y(3n) W(n)), one thread
 hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out);
 

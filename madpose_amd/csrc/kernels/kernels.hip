@@ -979,6 +979,27 @@ hipError_t launch_get_depths(hipStream_t s, int dtype, const void *maps, const i
     return hipGetLastError();
 }
 
+// bougnoux_focals (src/hybrid_pose_two_focal_estimator.cpp:11-32) of k fundamental
+// matrices (row-major, principal points at the origin), one lane each: the squared
+// focals exactly as the 7pt tail computes them (mp_pt67.h bougnoux_sq)
+__global__ void bougnoux_kernel(const double *F, int64_t k, double *out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    double f[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) f[e] = F[9 * i + e];
+    double f0, f1;
+    bougnoux_sq(f, &f0, &f1);
+    out[2 * i] = f0;
+    out[2 * i + 1] = f1;
+}
+
+hipError_t launch_bougnoux(hipStream_t s, const double *F, int64_t k, double *out) {
+    if (k <= 0) return hipSuccess;
+    bougnoux_kernel<<<(int)((k + 255) / 256), 256, 0, s>>>(F, k, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out) {
     scale_and_pose_kernel<<<1, 64, 0, s>>>(in, n, out);
     return hipGetLastError();

@@ -14,6 +14,12 @@ What it produces (all plain data, loadable with allow_pickle=False):
   These prototypes use the same elimination templates as src/solver.cpp:35-480.
   Instances follow the instance generators of the reference's own self-checks
   (solver_py/scale_and_shift.py:131-155 and the shared/two-focal analogues), seeded.
+* md_pose.npz     -- the pose stage of the MD solvers: every solution in md_solvers.npz
+  that passes the positivity filter of src/solver.cpp:503-504 (704-705, 1008-1009)
+  turned into (R, t, scale, offset0, offset1, focals) with the reference's own
+  find_transform (solver_py/scale_and_shift.py:120-129, _shared_focal.py:297,
+  _two_focal.py:356) on the corrected 3D points (image points divided by the focal(s)
+  first, as src/solver.cpp:711-714 does).
 * utils.npz       -- outputs of madpose/utils.py (get_depths, compute_pose_error,
   bougnoux_numpy) on the example pairs shipped in examples/image_pairs/.
 * example_pairs.npz -- the example matches / intrinsics / GT poses (data files of the
@@ -113,6 +119,41 @@ def gen_md(ss, ssf, stf, n_clean=150, n_noisy=50):
         out[f"{name}_gt"] = np.array(GT)
     np.savez_compressed(os.path.join(OUT, "md_solvers.npz"), **out)
     print("md_solvers.npz:", {k: v.shape for k, v in out.items() if k.endswith("_sols")})
+
+
+def gen_md_pose(ss, ssf, stf):
+    md = np.load(os.path.join(OUT, "md_solvers.npz"))
+    out = {}
+    for name, ft in (("cal", ss.find_transform), ("sf", ssf.find_transform), ("tf", stf.find_transform)):
+        X, Y, DX, DY = md[f"{name}_x"], md[f"{name}_y"], md[f"{name}_dx"], md[f"{name}_dy"]
+        SOL, NS = md[f"{name}_sols"], md[f"{name}_nsols"]
+        poses = np.full((len(X), 8, 17), np.nan)
+        count = np.zeros(len(X), dtype=np.int32)
+        for i in range(len(X)):
+            k = 0
+            for j in range(min(int(NS[i]), 8)):
+                s_ = SOL[i, j]
+                b1, a2, b2 = s_[1], s_[2], s_[3]
+                d1 = DX[i] + b1
+                d2 = DY[i] * a2 + b2
+                if d1.min() <= 0 or d2.min() <= 0:  # src/solver.cpp:503-504
+                    continue
+                f0 = f1 = 1.0
+                if name == "sf":
+                    f0 = f1 = s_[4]
+                elif name == "tf":
+                    f0, f1 = s_[4], s_[5]
+                xu, yu = X[i].copy(), Y[i].copy()
+                xu[:2] /= f0
+                yu[:2] /= f1
+                R, t = ft((xu * d1[None, :]).T, (yu * d2[None, :]).T)
+                poses[i, k] = np.r_[R.ravel(), t, a2, b1, b2, f0, f1]
+                k += 1
+            count[i] = k
+        out[f"{name}_pose"] = poses
+        out[f"{name}_npose"] = count
+    np.savez_compressed(os.path.join(OUT, "md_pose.npz"), **out)
+    print("md_pose.npz:", {k: int(v.sum()) for k, v in out.items() if k.endswith("_npose")})
 
 
 def gen_examples(utils):
@@ -229,8 +270,10 @@ def main():
     ssf = _load(os.path.join(REF, "solver_py", "scale_and_shift_shared_focal.py"), "ref_ssf")
     stf = _load(os.path.join(REF, "solver_py", "scale_and_shift_two_focal.py"), "ref_stf")
     utils = _load(os.path.join(REF, "madpose", "utils.py"), "ref_utils")
-    gen_md(ss, ssf, stf)
-    gen_examples(utils)
+    if "--pose-only" not in sys.argv:
+        gen_md(ss, ssf, stf)
+        gen_examples(utils)
+    gen_md_pose(ss, ssf, stf)
 
 
 if __name__ == "__main__":

@@ -61,6 +61,58 @@ def test_md_pose_matches_oracle(variant, name):
             assert abs(p.scale - r["scale"]) <= 1e-7 * (1 + abs(r["scale"]))
 
 
+@pytest.mark.parametrize("variant,name", [(0, "cal"), (1, "sf"), (2, "tf")])
+def test_md_pose_matches_reference_find_transform(variant, name):
+    """Pose stage of the MD solvers pinned by the reference itself: md_pose.npz holds,
+    for every reference solution that passes the positivity filter of
+    src/solver.cpp:503-504, the pose from the reference's find_transform
+    (solver_py/scale_and_shift*.py:120-129 / 297 / 356).  Same count per instance,
+    rotation within 1e-6 deg, the rest within 1e-6 relative."""
+    g = np.load(os.path.join(GOLDEN, "md_solvers.npz"))
+    gp = np.load(os.path.join(GOLDEN, "md_pose.npz"))
+    fn = [madpose.solve_scale_shift_pose, madpose.solve_scale_shift_pose_shared_focal,
+          madpose.solve_scale_shift_pose_two_focal][variant]
+    checked = 0
+    for i in range(len(g[f"{name}_x"])):
+        x, y, dx, dy = g[f"{name}_x"][i], g[f"{name}_y"][i], g[f"{name}_dx"][i], g[f"{name}_dy"][i]
+        mine = fn(x, y, dx, dy)
+        k = int(gp[f"{name}_npose"][i])
+        ref = gp[f"{name}_pose"][i, :k]
+        # noisy instances: the reference's LAPACK roots themselves carry ~1e-7 relative
+        # error on the worst-conditioned two-focal systems, which the pose inherits
+        tol = 1e-4 if g[f"{name}_noise"][i] > 0 else 1e-6
+        assert len(mine) == k, (i, len(mine), k)
+        for p in mine:
+            j = int(np.argmin(np.abs(ref[:, 13] - p.offset0)))
+            r = ref[j]
+            assert rot_angle_deg(p.R(), r[:9].reshape(3, 3)) < tol, i
+            np.testing.assert_allclose(p.t(), r[9:12], rtol=tol, atol=1e-8)
+            assert abs(p.scale - r[12]) <= tol * (1 + abs(r[12]))
+            assert abs(p.offset0 - r[13]) <= tol * (1 + abs(r[13]))
+            assert abs(p.offset1 - r[14]) <= tol * (1 + abs(r[14]))
+            if variant == 1:
+                assert abs(p.focal - r[15]) <= tol * r[15]
+            elif variant == 2:
+                assert abs(p.focal0 - r[15]) <= tol * r[15] and abs(p.focal1 - r[16]) <= tol * r[16]
+            checked += 1
+    assert checked > 200
+
+
+def test_bougnoux_matches_reference_numpy():
+    """Device bougnoux_sq (the two-focal 7pt tail's code) against the reference's
+    bougnoux_numpy outputs in utils.npz (madpose/utils.py:25-56).  The goldens carry
+    principal points p1, p2; the C++ form has them at the origin, so F is moved to
+    centred coordinates first: F' = T1^T F T0 with T = [[1,0,px],[0,1,py],[0,0,1]]."""
+    u = np.load(os.path.join(GOLDEN, "utils.npz"))
+    Fc = []
+    for F, pp in zip(u["bg_F"], u["bg_pp"]):
+        T0 = np.array([[1, 0, pp[0]], [0, 1, pp[1]], [0, 0, 1.0]])
+        T1 = np.array([[1, 0, pp[2]], [0, 1, pp[3]], [0, 0, 1.0]])
+        Fc.append(T1.T @ F @ T0)
+    got = madpose.bougnoux_focals_batch(np.array(Fc))
+    np.testing.assert_allclose(got, u["bg_out"], rtol=1e-8)
+
+
 def _rand_rot(rng):
     R = np.linalg.qr(rng.standard_normal((3, 3)))[0]
     return R * np.linalg.det(R)

@@ -95,3 +95,29 @@ def test_oracle_alt_solvers_recover_ground_truth():
         hits["tf"] += any(abs(m["focal0"] - f0) < 1e-6 and abs(m["focal1"] - f1) < 1e-6 for m in sols)
     # the calibrated solver drops roots that the reference's column bookkeeping loses
     assert hits["cal"] >= 0.9 * n and hits["sf"] == n and hits["tf"] == n, hits
+
+
+@pytest.mark.parametrize("variant,name", [(0, "cal"), (1, "sf"), (2, "tf")])
+def test_oracle_md_pose_matches_reference_find_transform(variant, name):
+    """The oracle's MD pose stage against md_pose.npz (reference find_transform on the
+    reference prototypes' roots, positivity filter of src/solver.cpp:503-504)."""
+    g = np.load(os.path.join(GOLDEN, "md_solvers.npz"))
+    gp = np.load(os.path.join(GOLDEN, "md_pose.npz"))
+    checked = 0
+    for i in range(len(g[f"{name}_x"])):
+        x, y, dx, dy = g[f"{name}_x"][i], g[f"{name}_y"][i], g[f"{name}_dx"][i], g[f"{name}_dy"][i]
+        mine = oracle.md_pose(variant, x.T, y.T, dx, dy)
+        k = int(gp[f"{name}_npose"][i])
+        ref = gp[f"{name}_pose"][i, :k]
+        # noisy instances: the reference's LAPACK roots themselves carry ~1e-7 relative
+        # error on the worst-conditioned two-focal systems, which the pose inherits
+        tol = 1e-4 if g[f"{name}_noise"][i] > 0 else 1e-6
+        assert len(mine) == k, (i, len(mine), k)
+        for p in mine:
+            r = ref[int(np.argmin(np.abs(ref[:, 13] - p["offset0"])))]
+            assert rot_angle_deg(p["R"], r[:9].reshape(3, 3)) < tol, i
+            np.testing.assert_allclose(p["t"], r[9:12], rtol=tol, atol=1e-8)
+            assert abs(p["scale"] - r[12]) <= tol * (1 + abs(r[12]))
+            assert abs(p["offset1"] - r[14]) <= tol * (1 + abs(r[14]))
+            checked += 1
+    assert checked > 200
