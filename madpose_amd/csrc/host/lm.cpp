@@ -108,12 +108,12 @@ constexpr size_t kPoolBlocks = 2048;
 // microseconds, and a futex wake-up per evaluation would cost about as much as the
 // evaluation's share per thread.  The spin is bounded by time, not by a pause count
 // (pause latency differs ~10x across x86 generations): MADPOSE_LO_SPIN = microseconds
-// (default 100; 0 = block right away).
+// (default 300; 0 = block right away).
 class Pool {
   public:
     explicit Pool(int n) {
         const char *e = std::getenv("MADPOSE_LO_SPIN");
-        spin_ns_ = (e ? std::max(0, std::atoi(e)) : 100) * 1000ll;
+        spin_ns_ = (e ? std::max(0, std::atoi(e)) : 300) * 1000ll;
         for (int i = 0; i < n - 1; ++i) th_.emplace_back([this] { loop(); });
     }
     ~Pool() {
