@@ -504,6 +504,9 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
         std::memcpy(H.x1.data(), in.x1, sizeof(double) * 2 * n);
         const double s = 1.0 / (C.K0[0] + C.K0[4]) + 1.0 / (C.K1[0] + C.K1[4]);
         C.loss_scale = 1.0 / (s * s);
+        // upper-triangular intrinsics with unit last row: the score kernels' ray form
+        auto tri = [](const double *K) { return K[3] == 0.0 && K[6] == 0.0 && K[7] == 0.0 && K[8] == 1.0; };
+        C.kstd = (tri(C.K0) && tri(C.K1) && tri(C.K0i) && tri(C.K1i) && !std::getenv("MADPOSE_SCORE_MATRIX_FORM")) ? 1 : 0;
     } else {
         double scale = 0.0;
         for (int i = 0; i < n; ++i) {

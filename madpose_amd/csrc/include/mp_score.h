@@ -51,6 +51,9 @@ MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r) {
     matvec3(Rt, t, rtt);
     double k1[3];
     matvec3(K0, rtt, k1);
+    r.nrt[0] = -rtt[0];
+    r.nrt[1] = -rtt[1];
+    r.nrt[2] = -rtt[2];
     r.k1[0] = -k1[0];
     r.k1[1] = -k1[1];
     r.k1[2] = -k1[2];
@@ -149,6 +152,54 @@ MP_HD double sampson_err(const double *G, double au, double av, double bu, doubl
     const double f1 = G[1] * bu + G[4] * bv + G[7];
     const double c = bu * e0 + bv * e1 + e2;
     return div_nonneg(c * c, e0 * e0 + e1 * e1 + f0 * f0 + f1 * f1);
+}
+
+// Calibrated residuals in ray form (C.kstd: K = [k00 k01 k02; 0 k11 k12; 0 0 1] for
+// both views): with a = K0^-1 x0 and b = K1^-1 x1 (third components 1),
+//   t=0: q = R a (d0 + o0) + t,       x1 - proj(K1 q) = K1[0:2,0:2] (q_xy / q_z - b_xy)
+//   t=1: q = R^T b (d1 s + o1 s) - R^T t, likewise against a through K0,
+// the same quantities as EvaluateModelOnPoint (src/hybrid_pose_estimator.cpp:223-246)
+// with K1 q / (K1 q)_z rewritten, and R a shared with the cheirality test (R n0 =
+// (R a) r0) -- fewer FP64 instructions per (correspondence, model) than the matrix
+// form M0 = K1 R K0^-1 of reproj_err.
+MP_HD double reproj_ray(const double *q, const double *K, double bu, double bv) {
+    if (q[2] < 1e-2) return DBL_MAX;
+    const double iz = rcp_depth(q[2]);
+    const double dx = fma(q[0], iz, -bu), dy = fma(q[1], iz, -bv);
+    const double ex = fma(K[1], dy, K[0] * dx), ey = K[4] * dy;
+    return fma(ex, ex, ey * ey);
+}
+MP_HD void eval_corr_cal_ray(const PairConst &C, const ScoreRec &r, const Corr &p, double &e0, double &e1, double &e2) {
+    const double *R = r.R, *t = r.t;
+    // R a and R^T b (a_2 = b_2 = 1)
+    const double ra0 = fma(R[0], p.a0, fma(R[1], p.a1, R[2]));
+    const double ra1 = fma(R[3], p.a0, fma(R[4], p.a1, R[5]));
+    const double ra2 = fma(R[6], p.a0, fma(R[7], p.a1, R[8]));
+    const double rb0 = fma(R[0], p.b0, fma(R[3], p.b1, R[6]));
+    const double rb1 = fma(R[1], p.b0, fma(R[4], p.b1, R[7]));
+    const double rb2 = fma(R[2], p.b0, fma(R[5], p.b1, R[8]));
+    {
+        const double s0 = p.d0 + r.o0;
+        const double q[3] = {fma(ra0, s0, t[0]), fma(ra1, s0, t[1]), fma(ra2, s0, t[2])};
+        e0 = reproj_ray(q, C.K1, p.b0, p.b1);
+    }
+    {
+        const double s1 = fma(p.d1, r.s, r.o1s);
+        const double q[3] = {fma(rb0, s1, r.nrt[0]), fma(rb1, s1, r.nrt[1]), fma(rb2, s1, r.nrt[2])};
+        e1 = reproj_ray(q, C.K0, p.a0, p.a1);
+    }
+    // check_cheirality(R, t, n0, n1, 1e-2) with R n0 = (R a) r0
+    const double rn0 = ra0 * p.r0, rn1 = ra1 * p.r0, rn2 = ra2 * p.r0;
+    const double a = -(rn0 * p.n1[0] + rn1 * p.n1[1] + rn2 * p.n1[2]);
+    const double b1 = -(rn0 * t[0] + rn1 * t[1] + rn2 * t[2]);
+    const double b2 = p.n1[0] * t[0] + p.n1[1] * t[1] + p.n1[2] * t[2];
+    const double l1 = b1 - a * b2, l2 = -a * b1 + b2;
+    const double md = 1e-2 * (1 - a * a);
+    if (!(l1 > md && l2 > md)) {
+        e2 = DBL_MAX;
+        return;
+    }
+    e2 = sampson_err(r.G, p.a0, p.a1, p.b0, p.b1) * C.loss_scale;
 }
 
 // Squared errors of the three data types for one correspondence.

@@ -42,8 +42,9 @@ struct Model {
 //   t=1:  p = M1 (x1,y1,1) * (d1*s + o1s) + k1   (M1 = K0 R^T K1^-1, k1 = -K0 R^T t)
 //   t=2:  Sampson with G (E for calibrated rays, F for normalized pixels),
 //         cheirality with R, t on unit bearings (calibrated variant only).
+//   nrt = -R^T t (the ray form of t=1, calibrated intrinsics of the kstd shape)
 struct ScoreRec {
-    double M0[9], k0[3], M1[9], k1[3], G[9], R[9], t[3];
+    double M0[9], k0[3], M1[9], k1[3], G[9], R[9], t[3], nrt[3];
     double o0, s, o1s, pad;
 };
 
@@ -56,7 +57,7 @@ struct PairConst {
     int use_shift;
     int md_alt; // 0 default MD solvers, 1 use_ours, 2 use_4p4d (two-focal)
     int scale_only; // HybridEstimatePoseAndScale (calibrated geometry, no offsets)
-    int pad1;
+    int kstd;       // calibrated K0, K1 (and inverses) of the form [a b c; 0 d e; 0 0 1] (score ray form)
     double K0[9], K1[9], K0i[9], K1i[9]; // identity for SF/TF (focal lives in the model)
     double thr[3], w[3];                 // squared thresholds / weights after the option transform
     double loss_scale;                   // calibrated Sampson scale (src/hybrid_pose_estimator.h:35-36)

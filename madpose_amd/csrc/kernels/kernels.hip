@@ -52,6 +52,9 @@ __device__ inline Corr load_corr(const PairConst &C, const PairData &D, int i, b
 }
 
 __device__ inline double msac(double e, double thr, double w) { return ((thr < e) ? thr : e) * w; }
+// the same term with thr * w precomputed (tw): the uniform value is selected directly
+// instead of being moved into a vector register first; bit-identical to msac
+__device__ inline double msac_tw(double e, double thr, double tw, double w) { return (thr < e) ? tw : e * w; }
 
 __global__ void prep_pair_kernel(PairConst C, PairData D, double *r0, double *r1) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -470,7 +473,10 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
     counts[b] = n;
 }
 
-template <int V, int MAXM>
+// FAST: score_type 0 (hybrid, no gating) and not scale-only, and for the calibrated
+// variant intrinsics of the kstd shape (ray form, mp_score.h eval_corr_cal_ray);
+// everything else takes the general path (runtime gating, matrix form).
+template <int V, int MAXM, bool FAST>
 __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairConst C,
                                                              const ScoreRec *__restrict__ recs,
                                                              const int *__restrict__ counts, double *scores,
@@ -487,14 +493,18 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     for (int m = 0; m < MAXM; ++m) acc[m] = 0.0;
     const double t0 = C.thr[0], t1 = C.thr[1], t2 = C.thr[2];
     const double w0 = C.w[0], w1 = C.w[1], w2 = C.w[2];
+    const double tw0 = t0 * w0, tw1 = t1 * w1, tw2 = t2 * w2;
     for (int i = threadIdx.x; i < C.n; i += kBlock) {
         const Corr p = load_corr(C, D, i, V == kCal);
 #pragma unroll
         for (int m = 0; m < MAXM; ++m) {
             if (m < nm) {
                 double e0, e1, e2;
-                eval_corr<V>(C, R[m], p, true, e0, e1, e2);
-                acc[m] += msac(e0, t0, w0) + msac(e1, t1, w1) + msac(e2, t2, w2);
+                if (FAST && V == kCal)
+                    eval_corr_cal_ray(C, R[m], p, e0, e1, e2);
+                else
+                    eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2);
+                acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
             }
         }
     }
@@ -878,12 +888,23 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
                               const int *counts, int nb, int maxm, double *scores, IterResult *res) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
-    if (C.variant == kCal)
-        score_batch_kernel<kCal, kMaxModelsCal><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
-    else if (C.variant == kSF)
-        score_batch_kernel<kSF, kMaxModelsSF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
-    else
-        score_batch_kernel<kTF, kMaxModelsTF><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+    const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
+    if (C.variant == kCal) {
+        if (fast)
+            score_batch_kernel<kCal, kMaxModelsCal, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+        else
+            score_batch_kernel<kCal, kMaxModelsCal, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+    } else if (C.variant == kSF) {
+        if (fast)
+            score_batch_kernel<kSF, kMaxModelsSF, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+        else
+            score_batch_kernel<kSF, kMaxModelsSF, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+    } else {
+        if (fast)
+            score_batch_kernel<kTF, kMaxModelsTF, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+        else
+            score_batch_kernel<kTF, kMaxModelsTF, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+    }
     return hipGetLastError();
 }
 
