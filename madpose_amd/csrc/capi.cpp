@@ -55,6 +55,7 @@ mp::EstimatorConfig to_cfg(const mp_estimator_config *c) {
     r.gtol = c->ceres_gradient_tolerance;
     r.ptol = c->ceres_parameter_tolerance;
     r.max_iter = c->ceres_max_num_iterations;
+    r.nonmonotonic = c->ceres_use_nonmonotonic_steps != 0;
     return r;
 }
 

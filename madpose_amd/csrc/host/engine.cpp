@@ -755,6 +755,7 @@ class Run {
         S.gtol = cfg_.gtol;
         S.ptol = cfg_.ptol;
         S.max_iter = (int)cfg_.max_iter;
+        S.nonmonotonic = cfg_.nonmonotonic;
         auto t_lm = Clock::now();
         lm_refine(P_.H, sample, S, m);
         if (g_prof_on.load(std::memory_order_relaxed)) {

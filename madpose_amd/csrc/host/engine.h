@@ -26,6 +26,7 @@ struct EstimatorConfig {
     int solver_type = 0, score_type = 0, lo_type = 0;
     bool min_depth_constraint = true, use_shift = true;
     double ftol = 1e-6, gtol = 1e-8, ptol = 1e-6, max_iter = 25;
+    bool nonmonotonic = true; // ceres_use_nonmonotonic_steps
 };
 
 struct Stats {

@@ -1006,6 +1006,16 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
         return v;
     };
     double radius = 1e4, decrease = 2.0;
+    // Ceres TrustRegionStepEvaluator: step quality against the current cost and
+    // against a reference cost that may lag behind it for up to 5 consecutive
+    // non-monotonic steps (0 when use_nonmonotonic_steps is off, which makes the
+    // reference the current cost and the quality the plain relative decrease); the
+    // parameters returned are those of the lowest cost reached (Ceres writes the
+    // user's parameter blocks only on a new minimum).
+    const int max_nonmono = S.nonmonotonic ? 5 : 0;
+    double ref_cost = cost, min_cost = cost, cand_cost_ref = cost, acc_ref = 0.0, acc_cand = 0.0;
+    int n_nonmono = 0;
+    Params best = x;
     if (!(gmax() <= S.gtol)) {
         for (int iter = 0; iter < S.max_iter; ++iter) {
             double sc[kNFull], A[kNFull * kNFull], y[kNFull];
@@ -1072,12 +1082,34 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
                 for (int b = 0; b < n; ++b) jd2 += d[a] * H[a * n + b] * d[b];
             }
             const double mcc = -(gd + 0.5 * jd2);
-            const double rho = (mcc > 0 && std::isfinite(cand_cost)) ? (cost - cand_cost) / mcc : -1.0;
+            const double rho = (mcc > 0 && std::isfinite(cand_cost))
+                                   ? std::max((cost - cand_cost) / mcc, (ref_cost - cand_cost) / (acc_ref + mcc))
+                                   : -1.0;
             if (rho > 1e-3) {
                 x = c;
                 cost = cand_cost;
                 std::swap(H, Hc);
                 std::swap(g, gc);
+                // TrustRegionStepEvaluator::StepAccepted
+                acc_cand += mcc;
+                acc_ref += mcc;
+                if (cost < min_cost) {
+                    min_cost = cost;
+                    n_nonmono = 0;
+                    cand_cost_ref = cost;
+                    acc_cand = 0.0;
+                    best = x;
+                } else {
+                    ++n_nonmono;
+                    if (cost > cand_cost_ref) {
+                        cand_cost_ref = cost;
+                        acc_cand = 0.0;
+                    }
+                }
+                if (n_nonmono == max_nonmono) {
+                    ref_cost = cand_cost_ref;
+                    acc_ref = acc_cand;
+                }
                 radius = std::min(1e16, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3)));
                 decrease = 2.0;
                 if (gmax() <= S.gtol) break;
@@ -1088,13 +1120,13 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
             }
         }
     }
-    quat_to_rot(x.q, m->R);
-    std::memcpy(m->t, x.t, sizeof(x.t));
-    m->scale = x.s;
-    m->offset0 = x.o0;
-    m->offset1 = x.o1;
-    m->focal0 = x.f0;
-    m->focal1 = (P.variant == kSF) ? x.f0 : x.f1;
+    quat_to_rot(best.q, m->R);
+    std::memcpy(m->t, best.t, sizeof(best.t));
+    m->scale = best.s;
+    m->offset0 = best.o0;
+    m->offset1 = best.o1;
+    m->focal0 = best.f0;
+    m->focal1 = (P.variant == kSF) ? best.f0 : best.f1;
     return true;
 }
 

@@ -30,6 +30,9 @@ struct LMSettings {
     double w_sampson = 1.0;
     double ftol = 1e-6, gtol = 1e-8, ptol = 1e-6;
     int max_iter = 25;
+    // Ceres use_nonmonotonic_steps (EstimatorConfig default true, src/estimator_config.h:31)
+    // with Ceres' default max_consecutive_nonmonotonic_steps = 5
+    bool nonmonotonic = true;
 };
 
 // Refines m over the residual blocks sample[0] (reproj 0->1), sample[1] (reproj 1->0),

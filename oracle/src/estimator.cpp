@@ -778,6 +778,14 @@ bool run_lm(const LMProblem &L, const EstConfig &cfg, Model *m) {
         return v;
     };
     double radius = 1e4, decrease = 2.0;
+    // Ceres TrustRegionStepEvaluator (use_nonmonotonic_steps, at most 5 consecutive
+    // non-monotonic steps; 0 when off) and TrustRegionMinimizer's rule that the user's
+    // parameters are written only on a new minimum cost
+    const int max_nonmono = cfg.ceres_use_nonmonotonic_steps ? 5 : 0;
+    double ref_cost = cost, min_cost = cost, cand_ref = cost, acc_ref = 0.0, acc_cand = 0.0;
+    int n_nonmono = 0;
+    double best[kJetN];
+    for (int k = 0; k < kJetN; ++k) best[k] = x[k];
     if (gmax() <= gtol) goto done;
     for (int iter = 0; iter < max_iter; ++iter) {
         // Jacobi scaling + LM step
@@ -826,12 +834,36 @@ bool run_lm(const LMProblem &L, const EstConfig &cfg, Model *m) {
             jd2 += s * s;
         }
         double mcc = -(gd + 0.5 * jd2);
-        double rho = (mcc > 0 && std::isfinite(cand_cost)) ? (cost - cand_cost) / mcc : -1.0;
+        double rho = -1.0;
+        if (mcc > 0 && std::isfinite(cand_cost)) {
+            const double relative = (cost - cand_cost) / mcc;
+            const double historical = (ref_cost - cand_cost) / (acc_ref + mcc);
+            rho = std::max(relative, historical);
+        }
         if (rho > 1e-3) {
             for (int k = 0; k < kJetN; ++k) x[k] = cand[k];
             evaluate(L, x, T, &r, &J, &m_res);
             cost = cand_cost;
             gradient(&g);
+            acc_cand += mcc;
+            acc_ref += mcc;
+            if (cost < min_cost) {
+                min_cost = cost;
+                n_nonmono = 0;
+                cand_ref = cost;
+                acc_cand = 0.0;
+                for (int k = 0; k < kJetN; ++k) best[k] = x[k];
+            } else {
+                ++n_nonmono;
+                if (cost > cand_ref) {
+                    cand_ref = cost;
+                    acc_cand = 0.0;
+                }
+            }
+            if (n_nonmono == max_nonmono) {
+                ref_cost = cand_ref;
+                acc_ref = acc_cand;
+            }
             radius = std::min(1e16, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rho - 1.0, 3)));
             decrease = 2.0;
             if (gmax() <= gtol) break;
@@ -842,15 +874,15 @@ bool run_lm(const LMProblem &L, const EstConfig &cfg, Model *m) {
         }
     }
 done:
-    double qn[4] = {x[QW], x[QX], x[QY], x[QZ]};
+    double qn[4] = {best[QW], best[QX], best[QY], best[QZ]};
     quat_to_R<double>(qn, m->R);
-    for (int c = 0; c < 3; ++c) m->t[c] = x[TX + c];
-    m->scale = x[SC];
-    m->offset0 = x[O0];
-    m->offset1 = x[O1];
-    m->focal0 = x[F0];
-    m->focal1 = x[F1];
-    if (P.variant == SF) m->focal1 = x[F0];
+    for (int c = 0; c < 3; ++c) m->t[c] = best[TX + c];
+    m->scale = best[SC];
+    m->offset0 = best[O0];
+    m->offset1 = best[O1];
+    m->focal0 = best[F0];
+    m->focal1 = best[F1];
+    if (P.variant == SF) m->focal1 = best[F0];
     return true;
 }
 
