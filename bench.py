@@ -30,6 +30,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (HBM3E spec peak)
+# FP64 vector peak: 256 CUs x 4 SIMD-32 x 16 FP64 FMA lanes per cycle x 2 x 2.4 GHz (public
+# MI355X spec figure; the guide has no FP64 row)
+FP64_PEAK_TFLOPS = 78.6
 BYTES_PER_CORR = 48    # x0u, x0v, x1u, x1v, d0, d1 in FP64
 
 WORKLOADS = {
@@ -191,6 +194,8 @@ def summarize(allv, wl, steps, warmup, world):
     launches = int(c["prof_batches"].sum())
     traffic, traffic_note = None, None
     tm = pmc_traffic_model()
+    if tm is not None and not tm.get("kernel", "").startswith(f"score_batch_kernel<{wl['variant']},"):
+        tm = None  # the committed PMC fit is of another variant's kernel
     if tm is not None and launches > 0:
         it_per_launch = float(c["prof_iterations"].sum()) / launches
         traffic = tm["fetch_bytes_fixed_per_launch"] + tm["fetch_bytes_per_iteration"] * it_per_launch
@@ -198,6 +203,17 @@ def summarize(allv, wl, steps, warmup, world):
                         f"{it_per_launch:.0f} iterations per launch; algorithmic bytes per launch "
                         f"{float(c['prof_correspondences'].sum()) * BYTES_PER_CORR / launches:.3g}: the pair's "
                         f"arrays stay L2-resident across the workgroups of a launch")
+    fp64 = None
+    if tm is not None and launches > 0 and "f64_flops_per_iteration" in tm and score_ms > 0:
+        it_per_launch = float(c["prof_iterations"].sum()) / launches
+        flops = tm["f64_flops_fixed_per_launch"] + tm["f64_flops_per_iteration"] * it_per_launch
+        tflops = flops / (score_ms * 1e-3 / launches) / 1e12
+        fp64 = {"bound": "fp64_valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tflops / FP64_PEAK_TFLOPS, "valu_issue_frac": tm.get("valu_issue_frac_median"),
+                "f64_share_of_valu": tm.get("f64_share_of_valu"),
+                "note": f"FP64 flops per launch from the SQ_INSTS_VALU_*_F64 fit in {tm['file']} at "
+                        f"{it_per_launch:.0f} iterations per launch over the HIP-event launch time; "
+                        f"valu_issue_frac = VALU issue cycles / SIMD cycles of the profiled dispatches"}
     return {
         "metric": "RANSAC hypotheses/sec + image-pairs/sec on 1xMI355X",
         "value": float(c["hypotheses"].sum()) / t_max,
@@ -238,6 +254,7 @@ def summarize(allv, wl, steps, warmup, world):
             "avg_launch_us": score_ms * 1e3 / max(launches, 1),
             "bytes_per_hypothesis": BYTES_PER_CORR * wl["n"],
             "solve_ms_per_launch": float(c["solve_ms"].sum()) / max(launches, 1),
+            "fp64_valu": fp64,
         },
         "cpu_baseline": None,
     }
