@@ -425,13 +425,37 @@ def run_scannet(a, wl, world, rank, dev, barrier, eng):
     recs = [result_record(s, m, st, p) for s, (m, st), p in zip(seeds, res, pairs)]
     local = [elapsed, float(len(pairs) * a.steps), float(sum(st.num_hypotheses for _, st in res) * a.steps),
              float(sum(st.num_iterations_total for _, st in res) * a.steps)]
+    # point-only baseline (untimed): the examples compare against PoseLib's point-based
+    # estimate_relative_pose (examples/calibrated.py:92-122, shared_focal.py:111-130);
+    # PoseLib is not vendored, so the reference's own point-only mode stands in:
+    # EstimatorConfig(solver=EPI_ONLY, score=EPI_ONLY, LO=EPI_ONLY) on the same pairs
+    prec = []
+    if a.point_only:
+        from madpose_amd.api import EstimatorConfig
+
+        cp = EstimatorConfig(1, 1, 1)
+        cp.min_depth_constraint, cp.use_shift = c.min_depth_constraint, c.use_shift
+        pres = eng.estimate_batch(wl["variant"], pairs, o, cp, device=dev, num_streams=a.streams)
+        prec = [result_record(s, m, st, p) for s, (m, st), p in zip(seeds, pres, pairs)]
     allv = gather_counters(local, world)
     per = (total + world - 1) // world + 1
     allr = gather_records(recs, per, world)
+    allp = gather_records(prec, per, world) if a.point_only else None
     if rank == 0:
         errs = np.maximum(allr[:, RECORD_FIELDS.index("err_R_deg")], allr[:, RECORD_FIELDS.index("err_t_deg")])
         out = summarize_scannet(allv, errs, wl, a.steps, a.warmup, world, total)
         out["results"] = records_summary(allr)
+        if allp is not None:
+            from madpose_amd import utils
+
+            pe = np.maximum(allp[:, RECORD_FIELDS.index("err_R_deg")], allp[:, RECORD_FIELDS.index("err_t_deg")])
+            pe = pe[np.isfinite(pe)]
+            auc = utils.pose_auc(pe, (5, 10, 20)) if len(pe) else [None] * 3
+            out["point_only_baseline"] = {
+                "pose_auc": {"5": auc[0], "10": auc[1], "20": auc[2], "pairs": int(len(pe))},
+                "config": "EstimatorConfig(solver=EPI_ONLY, score=EPI_ONLY, LO=EPI_ONLY): the reference's own "
+                          "point-only mode (6pt shared-focal solver, Sampson error only), standing in for the "
+                          "examples' poselib estimate_*_relative_pose (PoseLib is not vendored); untimed"}
         if world == 1 and a.cpu_budget > 0:
             out["cpu_baseline"] = cpu_baseline_pairs(wl, seeds, a.cpu_budget, a.cpu_procs)
         print(json.dumps(out), flush=True)
@@ -504,6 +528,8 @@ def main(argv=None):
                     help="processes of the all-core CPU baseline leg (0 = one per physical core)")
     ap.add_argument("--pairs", type=int, default=0, help="scannet: total pairs (default 1500)")
     ap.add_argument("--streams", type=int, default=8, help="scannet: pairs in flight per GPU")
+    ap.add_argument("--no-point-only", dest="point_only", action="store_false",
+                    help="scannet: skip the untimed point-only baseline pass")
     ap.add_argument("--engine-module", default=None, help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     if a.steps is None:

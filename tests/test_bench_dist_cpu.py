@@ -114,6 +114,7 @@ def test_gpus_flag_scannet_shards_all_pairs():
     assert res["n_gpus"] == 2 and res["config"]["pairs"] == 9
     assert res["results"]["records"] == 9 and res["results"]["pairs_disjoint"]
     assert res["pose_auc"]["pairs"] == 9
+    assert res["point_only_baseline"]["pose_auc"]["pairs"] == 9
 
 
 def test_gpus_mismatch_fails_loudly():

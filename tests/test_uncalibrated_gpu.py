@@ -70,11 +70,16 @@ def test_6pt_shared_focal_matches_oracle_and_ground_truth():
             err = min(rot_angle_deg(m.R(), R) + abs(m.focal - f0) + np.abs(m.t() / np.linalg.norm(m.t()) - tn).max()
                       for m in dev) if dev else np.inf
             gt_found += err < 1e-5
-    # two independent root finders (DFT-interpolated determinant + Sturm on the
-    # device, companion eigenvalues in the oracle) may disagree on clusters of
-    # nearly coincident roots; everything else must match
-    assert set_mismatch <= 0.03 * n_trials, set_mismatch
-    assert gt_found >= 0.97 * (n_trials // 2), gt_found
+    # Two independent root finders: the device interpolates q(u) = det(pencil) / u^5
+    # by a 16-point DFT and isolates its real roots by Sturm sequences, the oracle
+    # takes the eigenvalues of the 20x20 companion matrix.  Measured over 2000 trials
+    # (tools/diag_pt67.py, round 2): 10 pose-set mismatches (0.5 %), all on trials
+    # whose exact root set (rational arithmetic, sympy) shows the DFT coefficients,
+    # not the eigenvalues, at fault -- roots below ~0.1 of the mean root modulus or
+    # within 1e-3 of a neighbour, where the small coefficients of q lose their digits
+    # (DESIGN.md §6).  The bounds below are that rate with sampling margin.
+    assert set_mismatch <= 2, set_mismatch
+    assert gt_found >= n_trials // 2 - 1, gt_found
 
 
 def test_7pt_two_focal_matches_oracle_and_ground_truth():
@@ -101,9 +106,9 @@ def test_7pt_two_focal_matches_oracle_and_ground_truth():
         if clean:
             err = min(abs(m.focal0 - f0) + abs(m.focal1 - f1) for m in dev)
             gt_found += err < 1e-6
-    # recoverPose candidate ties resolve by label order, which depends on the SVD
-    # sign convention when E has two equal singular values (noise-free data)
-    assert mismatch <= 0.02 * n_trials, mismatch
+    # 0 of 2000 trials disagree (tools/diag_pt67.py, round 2): the candidate labels of
+    # recoverPose follow the canonical SVD signs on both sides
+    assert mismatch == 0, mismatch
     assert gt_found == n_trials // 2
 
 
