@@ -152,6 +152,32 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
 int mp_get_depths(int dtype, int32_t num_pairs, const void *depth_maps, const int64_t *dims, const int64_t *pt_offsets,
                   const double *keypoints, void *out, int device);
 
+/* Batched device Levenberg-Marquardt: the Ceres solves of the local
+ * optimisation -- HybridPoseOptimizer* (src/optimizer.h:48-125, SF :265-369, TF
+ * :383-499) over the cost functors of src/cost_functions.h:16-387, as called by
+ * LeastSquares (kinds[j] = 0; src/hybrid_pose_estimator.cpp:263-295) or
+ * NonMinimalSolver (1; :188-214) -- for num_problems problems on one pair, one device
+ * workgroup each.  Problem j refines models[j] (in/out, problem units: SF/TF focals
+ * divided by the pair's normalize_points scale) over the residual blocks
+ * sample_idx[sample_offsets[3j] ..) (reprojection 0->1), [sample_offsets[3j+1] ..)
+ * (1->0), [sample_offsets[3j+2] .. sample_offsets[3j+3]) (Sampson).  status[j]: 1
+ * refined, 0 no residuals, 2 infeasible constant bounded block, 3 too few data for
+ * the solver (model unchanged in cases 0, 2, 3).  Options and config as mp_estimate
+ * (thresholds / weights / Ceres settings); min_depth may be NULL (zeros). */
+int mp_lm_refine_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                       const double *d1, const double *min_depth, const double *cam0, const double *cam1,
+                       const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
+                       const int32_t *kinds, const int64_t *sample_offsets, const int32_t *sample_idx,
+                       mp_model *models, int32_t *status, int device);
+
+/* mp_debug_lm_refine_host: the same problems through the engine's host LM (the
+ * default LO path) -- test hook, no device needed. */
+int mp_debug_lm_refine_host(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                            const double *d1, const double *min_depth, const double *cam0, const double *cam1,
+                            const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
+                            const int32_t *kinds, const int64_t *sample_offsets, const int32_t *sample_idx,
+                            mp_model *models, int32_t *status);
+
 /* bougnoux_focals (src/hybrid_pose_two_focal_estimator.cpp:11-32; numpy twin
  * madpose/utils.py:25-56 bougnoux_numpy with p1 = p2 = 0): squared focal lengths
  * (f0^2, f1^2) of k fundamental matrices F (k x 9, row-major) into out (k x 2), on

@@ -24,6 +24,7 @@ from .api import (  # noqa: F401
     estimate_batch,
     estimate_scale_and_pose,
     bougnoux_focals_batch,
+    lm_refine_batch,
     get_depths_batch,
     profile_enable,
     profile_read,

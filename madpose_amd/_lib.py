@@ -120,6 +120,15 @@ EXPORTS = {
                                          ctypes.c_int]),
     "mp_get_depths": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_void_p, c_int64_p, c_int64_p, c_double_p,
                                      ctypes.c_void_p, ctypes.c_int]),
+    "mp_lm_refine_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p, c_double_p,
+                                          c_double_p, c_double_p, c_double_p, ctypes.POINTER(mp_ransac_options),
+                                          ctypes.POINTER(mp_estimator_config), ctypes.c_int32, c_int32_p, c_int64_p,
+                                          c_int32_p, ctypes.POINTER(mp_model), c_int32_p, ctypes.c_int]),
+    "mp_debug_lm_refine_host": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p,
+                                               c_double_p, c_double_p, c_double_p, c_double_p,
+                                               ctypes.POINTER(mp_ransac_options), ctypes.POINTER(mp_estimator_config),
+                                               ctypes.c_int32, c_int32_p, c_int64_p, c_int32_p,
+                                               ctypes.POINTER(mp_model), c_int32_p]),
     "mp_bougnoux_focals": (ctypes.c_int, [ctypes.c_int64, c_double_p, c_double_p, ctypes.c_int]),
     "mp_estimate_scale_and_pose": (ctypes.c_int, [c_double_p, c_double_p, c_double_p, ctypes.c_int64,
                                                   ctypes.POINTER(mp_model), ctypes.c_int]),

@@ -415,6 +415,51 @@ def estimate_batch(variant, pairs, options, est_config=None, device=None, num_st
     return out
 
 
+def lm_refine_batch(variant, x0, x1, depth0, depth1, min_depth, cam0, cam1, options, est_config, problems,
+                    device=None, on_host=False):
+    """Batched device LM (the LO's Ceres solves, src/optimizer.h:48-125 over
+    src/cost_functions.h): problems is a list of (kind, (idx0, idx1, idx2), model) with
+    kind 0 = LeastSquares, 1 = NonMinimalSolver, idx* the residual blocks of the three
+    data types and model a PoseScaleOffset* in problem units (SF/TF focals divided by
+    the pair's normalize_points scale).  One device workgroup per problem.  Returns a
+    list of (model, status): 1 refined, 0 no residuals, 2 infeasible constant block,
+    3 too few data (unchanged)."""
+    if est_config is None:
+        est_config = EstimatorConfig()
+    x0 = _pts(x0, "x0")
+    n = x0.shape[0]
+    x1 = _pts(x1, "x1")
+    d0, d1 = _vec(depth0, n, "depth0"), _vec(depth1, n, "depth1")
+    md = np.asarray(min_depth, dtype=np.float64).reshape(2)
+    k = 9 if variant == L.CALIBRATED else 2
+    c0 = np.ascontiguousarray(np.asarray(cam0, dtype=np.float64).reshape(k))
+    c1 = np.ascontiguousarray(np.asarray(cam1, dtype=np.float64).reshape(k))
+    P = len(problems)
+    kinds = np.array([int(p[0]) for p in problems] or [0], dtype=np.int32)
+    offs, idx = [0], []
+    for _, lists, _m in problems:
+        for t in range(3):
+            a = np.asarray(lists[t], dtype=np.int32).reshape(-1)
+            idx.append(a)
+            offs.append(offs[-1] + len(a))
+    offs = np.asarray(offs, dtype=np.int64)
+    idx = np.ascontiguousarray(np.concatenate(idx) if idx and offs[-1] > 0 else np.zeros(1, dtype=np.int32))
+    models = (L.mp_model * max(P, 1))()
+    for j, (_, _, m) in enumerate(problems):
+        models[j] = _model_to_c(m, variant)
+    status = np.zeros(max(P, 1), dtype=np.int32)
+    o = options._to_c()
+    c = est_config._to_c()
+    common = (variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(md), _dp(c0), _dp(c1), ctypes.byref(o),
+              ctypes.byref(c), P, kinds.ctypes.data_as(L.c_int32_p), offs.ctypes.data_as(L.c_int64_p),
+              idx.ctypes.data_as(L.c_int32_p), models, status.ctypes.data_as(L.c_int32_p))
+    if on_host:  # test hook: the engine's host LM (the default LO path) on the same problems
+        L.check(L.lib().mp_debug_lm_refine_host(*common))
+    else:
+        L.check(L.lib().mp_lm_refine_batch(*common, _DEFAULT_DEVICE if device is None else int(device)))
+    return [(_model_from_c(models[j], variant), int(status[j])) for j in range(P)]
+
+
 def bougnoux_focals_batch(F, device=None):
     """Squared Bougnoux focal lengths (f0^2, f1^2) of fundamental matrices F (k x 3 x 3,
     principal points at the origin) on the device: the two-focal 7-point tail's own

@@ -270,6 +270,40 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
     });
 }
 
+int mp_lm_refine_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                       const double *d1, const double *min_depth, const double *cam0, const double *cam1,
+                       const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
+                       const int32_t *kinds, const int64_t *sample_offsets, const int32_t *sample_idx,
+                       mp_model *models, int32_t *status, int device) {
+    return guarded([&]() {
+        if (!options || num_problems < 0 || (num_problems > 0 && (!sample_offsets || !models || !status)))
+            throw std::invalid_argument("bad arguments");
+        if (num_problems > 0 && sample_offsets[3 * num_problems] > 0 && !sample_idx)
+            throw std::invalid_argument("null sample indices");
+        const double md0[2] = {0.0, 0.0};
+        mp::PairInput in = make_input(variant, n, x0, x1, d0, d1, min_depth ? min_depth : md0, cam0, cam1);
+        std::vector<mp::Model> ms(num_problems);
+        std::memcpy(ms.data(), models, sizeof(mp_model) * num_problems);
+        if (device == -1000) // mp_debug_lm_refine_host
+            mp::lm_refine_batch_host(in, to_opts(options), to_cfg(config), num_problems, kinds, sample_offsets,
+                                     sample_idx, ms.data(), status);
+        else
+            mp::lm_refine_batch_device(in, to_opts(options), to_cfg(config), num_problems, kinds, sample_offsets,
+                                       sample_idx, ms.data(), status, device);
+        for (int j = 0; j < num_problems; ++j) to_model(ms[j], &models[j]);
+        return MP_OK;
+    });
+}
+
+int mp_debug_lm_refine_host(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                            const double *d1, const double *min_depth, const double *cam0, const double *cam1,
+                            const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
+                            const int32_t *kinds, const int64_t *sample_offsets, const int32_t *sample_idx,
+                            mp_model *models, int32_t *status) {
+    return mp_lm_refine_batch(variant, n, x0, x1, d0, d1, min_depth, cam0, cam1, options, config, num_problems, kinds,
+                              sample_offsets, sample_idx, models, status, -1000);
+}
+
 static int point_direct(int kind, const double *x1, const double *x2, mp_model *out, int max_out, int device) {
     if (!x1 || !x2 || (max_out > 0 && !out)) return -fail(MP_EINVAL, "null argument");
     int r = guarded([&]() {

@@ -219,9 +219,9 @@ struct SweepSlot {
         }
         if (nn <= cap) return;
         release();
-        const int nb = sweep_blocks(nn);
-        MP_HIP(hipHostMalloc(&h_out, sizeof(double) * (3 * nn + nb), hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostMalloc(&h_out2, sizeof(double) * (3 * nn + nb), hipHostMallocMapped | hipHostMallocCoherent));
+        const int nb = sweep_blocks(nn), np = nb * sweep_waves_per_block();
+        MP_HIP(hipHostMalloc(&h_out, sizeof(double) * (3 * nn + np), hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostMalloc(&h_out2, sizeof(double) * (3 * nn + np), hipHostMallocMapped | hipHostMallocCoherent));
         MP_HIP(hipHostMalloc(&h_flag, sizeof(int) * nb, hipHostMallocMapped | hipHostMallocCoherent));
         MP_HIP(hipHostGetDevicePointer((void **)&d_out, h_out, 0));
         MP_HIP(hipHostGetDevicePointer((void **)&d_out2, h_out2, 0));
@@ -663,8 +663,13 @@ class Run {
                 }
             }
         }
-        double total = 0.0; // partial scores in workgroup order
-        for (int b = 0; b < nb; ++b) total += h_out[3 * n_ + b];
+        double total = 0.0; // partial scores: waves in order within a workgroup, workgroups in order
+        const int W = sweep_waves_per_block();
+        for (int b = 0; b < nb; ++b) {
+            double sb = 0.0;
+            for (int w = 0; w < W; ++w) sb += h_out[3 * n_ + W * b + w];
+            total += sb;
+        }
         const double t_done = secs(t_sw);
         L.err = h_out;
         L.t[0] += t_launched;
@@ -1344,6 +1349,129 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
     MP_HIP(hipStreamSynchronize(X.stream));
     hipFree(d_recs);
     hipFree(d_sc);
+}
+
+// Ceres settings of one LeastSquares / NonMinimalSolver call (the flags of
+// Run::least_squares; src/hybrid_pose_estimator.cpp:203, 281 and the SF/TF analogues)
+LmJob make_lm_job(const Problem &P, const EstimatorConfig &cfg, const int *sizes, int off, bool nonminimal,
+                  const Model &m) {
+    LmJob J;
+    std::memset(&J, 0, sizeof(J));
+    const bool use_reproj = cfg.lo_type != 1, use_sampson = cfg.lo_type != 2;
+    const int v = P.C.variant;
+    J.off0 = off;
+    J.n0 = use_reproj ? sizes[0] : 0;
+    J.off1 = off + sizes[0];
+    J.n1 = use_reproj ? sizes[1] : 0;
+    J.off2 = off + sizes[0] + sizes[1];
+    J.n2 = use_sampson ? sizes[2] : 0;
+    J.use_shift = (v == kCal || (v == kSF && nonminimal)) ? cfg.use_shift : 1;
+    J.min_depth_constraint = cfg.min_depth_constraint;
+    if (P.C.scale_only) { // HybridPoseOptimizerScaleOnly: offsets constant, unbounded
+        J.use_shift = 0;
+        J.min_depth_constraint = 0;
+    }
+    J.w_sampson = v == kCal ? std::sqrt(P.H.sampson_squared_weight) /
+                                  (1.0 / (P.C.K0[0] + P.C.K0[4]) + 1.0 / (P.C.K1[0] + P.C.K1[4]))
+                            : std::sqrt(P.H.sampson_squared_weight);
+    J.ftol = cfg.ftol;
+    J.gtol = cfg.gtol;
+    J.ptol = cfg.ptol;
+    J.max_iter = (int)cfg.max_iter;
+    J.nonmonotonic = cfg.nonmonotonic ? 1 : 0;
+    J.m = m;
+    return J;
+}
+
+// the same problems through the host LM (host/lm.cpp) -- test hook (mp_debug_lm_refine_host)
+void lm_refine_batch_host(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nprob,
+                          const int32_t *kinds, const int64_t *offsets, const int32_t *idx, Model *models,
+                          int32_t *status) {
+    validate(in, opts);
+    Problem P = make_problem(in, opts, cfg);
+    const int v = P.C.variant;
+    const int kmd = v == kCal ? 3 : 4, kpt = v == kCal ? 5 : (v == kSF ? 6 : 7);
+    for (int j = 0; j < nprob; ++j) {
+        std::vector<int> smp[3];
+        int sz[3];
+        for (int t = 0; t < 3; ++t) {
+            smp[t].assign(idx + offsets[3 * j + t], idx + offsets[3 * j + t + 1]);
+            sz[t] = (int)smp[t].size();
+        }
+        if ((sz[0] < kmd && sz[1] < kmd) || sz[2] < kpt) {
+            status[j] = 3;
+            continue;
+        }
+        const LmJob J = make_lm_job(P, cfg, sz, 0, kinds && kinds[j] == 1, models[j]);
+        LMSettings S;
+        S.use_reproj = cfg.lo_type != 1;
+        S.use_sampson = cfg.lo_type != 2;
+        S.use_shift = J.use_shift != 0;
+        S.min_depth_constraint = J.min_depth_constraint != 0;
+        S.w_sampson = J.w_sampson;
+        S.ftol = J.ftol;
+        S.gtol = J.gtol;
+        S.ptol = J.ptol;
+        S.max_iter = J.max_iter;
+        S.nonmonotonic = J.nonmonotonic != 0;
+        status[j] = lm_refine(P.H, smp, S, &models[j]) ? 1 : 0;
+    }
+}
+
+void lm_refine_batch_device(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nprob,
+                            const int32_t *kinds, const int64_t *offsets, const int32_t *idx, Model *models,
+                            int32_t *status, int device) {
+    validate(in, opts);
+    if (nprob <= 0) return;
+    CtxLease lease(device);
+    DeviceCtx &X = *lease.c;
+    Problem P = make_problem(in, opts, cfg);
+    X.ensure(in.n, 64, max_models(in.variant == kScaleOnly ? kCal : in.variant));
+    PairData D;
+    upload_pair(X, P, &D);
+    const int v = P.C.variant;
+    const int kmd = v == kCal ? 3 : 4, kpt = v == kCal ? 5 : (v == kSF ? 6 : 7);
+    std::vector<LmJob> jobs;
+    std::vector<int> which;
+    for (int j = 0; j < nprob; ++j) {
+        int sz[3];
+        for (int t = 0; t < 3; ++t) {
+            const int64_t a = offsets[3 * j + t], b = offsets[3 * j + t + 1];
+            if (b < a) throw std::invalid_argument("sample offsets must not decrease");
+            sz[t] = (int)(b - a);
+            for (int64_t k = a; k < b; ++k)
+                if (idx[k] < 0 || idx[k] >= in.n) throw std::invalid_argument("sample index out of range");
+        }
+        // too few data for the solver (the size test of least_squares)
+        if ((sz[0] < kmd && sz[1] < kmd) || sz[2] < kpt) {
+            status[j] = 3;
+            continue;
+        }
+        jobs.push_back(make_lm_job(P, cfg, sz, (int)offsets[3 * j], kinds && kinds[j] == 1, models[j]));
+        which.push_back(j);
+    }
+    if (jobs.empty()) return;
+    const int64_t nidx = offsets[3 * nprob];
+    LmJob *d_jobs;
+    int *d_idx, *d_status;
+    Model *d_out;
+    MP_HIP(hipMalloc(&d_jobs, sizeof(LmJob) * jobs.size()));
+    MP_HIP(hipMalloc(&d_idx, sizeof(int) * (size_t)std::max<int64_t>(nidx, 1)));
+    MP_HIP(hipMalloc(&d_status, sizeof(int) * jobs.size()));
+    MP_HIP(hipMalloc(&d_out, sizeof(Model) * jobs.size()));
+    MP_HIP(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(LmJob) * jobs.size(), hipMemcpyHostToDevice, X.stream));
+    if (nidx > 0) MP_HIP(hipMemcpyAsync(d_idx, idx, sizeof(int) * nidx, hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_lm_batch(X.stream, D, P.C, d_jobs, (int)jobs.size(), d_idx, d_out, d_status));
+    std::vector<Model> out(jobs.size());
+    std::vector<int> st(jobs.size());
+    MP_HIP(hipMemcpyAsync(out.data(), d_out, sizeof(Model) * out.size(), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(st.data(), d_status, sizeof(int) * st.size(), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipStreamSynchronize(X.stream));
+    for (size_t k = 0; k < which.size(); ++k) {
+        models[which[k]] = out[k];
+        status[which[k]] = st[k];
+    }
+    for (void *q : {(void *)d_jobs, (void *)d_idx, (void *)d_status, (void *)d_out}) hipFree(q);
 }
 
 int solve_md_direct(int variant, const double *x, const double *y, const double *dx, const double *dy, double *sols,

@@ -61,6 +61,19 @@ void estimate_pair(const PairInput &in, const RansacOptions &opts, const Estimat
 void score_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
                   int nm, double *scores, double *errors, int device, double *norm_scale);
 
+// Batched device LM (mp_lm_refine_batch): problem j refines models[j] (problem units)
+// over the residual blocks idx[offsets[3j] .. offsets[3j+1]) (reproj 0->1),
+// [offsets[3j+1] .. offsets[3j+2]) (1->0), [offsets[3j+2] .. offsets[3j+3]) (Sampson),
+// with the settings of LeastSquares (kinds[j] 0) or NonMinimalSolver (1).  status[j]:
+// 1 refined, 0 no residuals, 2 infeasible constant block, 3 too few data (unchanged).
+void lm_refine_batch_device(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nprob,
+                            const int32_t *kinds, const int64_t *offsets, const int32_t *idx, Model *models,
+                            int32_t *status, int device);
+
+void lm_refine_batch_host(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nprob,
+                          const int32_t *kinds, const int64_t *offsets, const int32_t *idx, Model *models,
+                          int32_t *status);
+
 // Standalone solvers on the device (mp_solve_* / mp_relpose_5pt).
 // alt: 0 default MD solver, 1 use_ours, 2 use_4p4d (two-focal)
 int solve_md_direct(int variant, const double *x, const double *y, const double *dx, const double *dy, double *sols,

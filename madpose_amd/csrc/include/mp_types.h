@@ -78,6 +78,16 @@ struct IterResult {
     int slot, count;
 };
 
+// One least-squares problem of the batched device LM (kernels/lm_device.h): residual
+// blocks idx[off0 .. off0+n0) (reprojection 0->1), idx[off1 ..) (1->0), idx[off2 ..)
+// (Sampson) of the pair, the Ceres settings of the call and the start model.
+struct LmJob {
+    int off0, n0, off1, n1, off2, n2;
+    int use_shift, min_depth_constraint, nonmonotonic, max_iter;
+    double w_sampson, ftol, gtol, ptol;
+    Model m;
+};
+
 constexpr int kMaxModelsCal = 10; // MD <= 4, 5pt <= 10
 constexpr int kMaxModelsSF = 16;  // MD <= 8, 6pt <= 15
 constexpr int kMaxModelsTF = 4;   // MD <= 4, 7pt <= 3

@@ -40,10 +40,12 @@ hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, co
 hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, double *cand, int *ncand, int impl);
 // the single-model sweep writing straight to host-mapped memory: out[0, 3n) the errors,
-// out[3n + b] workgroup b's partial score, flags[b] = seq (system scope) once
-// workgroup b is done, for b < sweep_blocks(n); the score is the sum of the partials
-// in workgroup order
+// out[3n + W b + w] the partial score of wave w of workgroup b (W =
+// sweep_waves_per_block()), flags[b] = seq (system scope) once workgroup b is done,
+// for b < sweep_blocks(n); the score is the sum over workgroups in order of each
+// workgroup's wave partials summed in wave order
 int sweep_blocks(int64_t n);
+int sweep_waves_per_block();
 hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
                             int *flags, int seq);
 // scores of many explicit models (one workgroup per model) -- used by mp_score_models
@@ -54,6 +56,11 @@ hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst
 hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *in /* x(3K) y(3K) dx(K) dy(K) */,
                             double *sols, int *nsols, Model *poses, int *nposes);
 hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes);
+
+// batched device LM: one workgroup per job; out[j] the refined model, status[j] 1
+// refined, 0 no residuals, 2 infeasible constant block (unchanged)
+hipError_t launch_lm_batch(hipStream_t s, const PairData &D, const PairConst &C, const LmJob *jobs, int njobs,
+                           const int *idx, Model *out, int *status);
 
 // squared Bougnoux focals of k fundamental matrices (9 doubles each) into out (2 each)
 hipError_t launch_bougnoux(hipStream_t s, const double *F, int64_t k, double *out);

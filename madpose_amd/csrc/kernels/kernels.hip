@@ -23,6 +23,7 @@
 #include "group_5pt.h"
 #include "group_6pt.h"
 #include "group_tail.h"
+#include "lm_device.h"
 #include "kernels.h"
 
 namespace mp {
@@ -587,18 +588,14 @@ __global__ void __launch_bounds__(kSweepBlock) sweep_host_kernel(PairData D, Pai
         acc += gate_md ? C.thr[0] * C.w[0] + C.thr[1] * C.w[1] : msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]);
         acc += gate_epi ? C.thr[2] * C.w[2] : msac(e2, C.thr[2], C.w[2]);
     }
-    __shared__ double wpart[kSweepBlock / 64];
+    // each wave's partial score goes to host memory beside the error rows, so one
+    // system-scope fence per thread covers both before the workgroup's flag
     const double v = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = v;
-    __threadfence_system(); // this workgroup's error rows reach host memory
+    if ((threadIdx.x & 63) == 0) out[3 * C.n + (kSweepBlock / 64) * blockIdx.x + (threadIdx.x >> 6)] = v;
+    __threadfence_system(); // this thread's error rows and partial reach host memory
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double sc = 0.0;
-        for (int w = 0; w < kSweepBlock / 64; ++w) sc += wpart[w];
-        out[3 * C.n + blockIdx.x] = sc;
-        __threadfence_system();
+    if (threadIdx.x == 0)
         __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
 }
 
 template <int V>
@@ -929,6 +926,7 @@ hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C,
 }
 
 int sweep_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kSweepBlock - 1) / kSweepBlock); }
+int sweep_waves_per_block() { return kSweepBlock / 64; }
 
 hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
                             int *flags, int seq) {
@@ -1013,6 +1011,15 @@ __global__ void bougnoux_kernel(const double *F, int64_t k, double *out) {
     bougnoux_sq(f, &f0, &f1);
     out[2 * i] = f0;
     out[2 * i + 1] = f1;
+}
+
+hipError_t launch_lm_batch(hipStream_t s, const PairData &D, const PairConst &C, const LmJob *jobs, int njobs,
+                           const int *idx, Model *out, int *status) {
+    if (njobs <= 0) return hipSuccess;
+    return by_variant(C.variant, [&](auto V) {
+        lm_batch_kernel<decltype(V)::value><<<njobs, kLmBlock, 0, s>>>(D, C, jobs, idx, out, status);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_bougnoux(hipStream_t s, const double *F, int64_t k, double *out) {

@@ -194,6 +194,25 @@ def score_models(variant, x0, x1, d0, d1, cam0, cam1, opts, cfg, models):
     return scores[:nm], errors[:nm], ns.value
 
 
+def least_squares(variant, x0, x1, d0, d1, min_depth, cam0, cam1, opts, cfg, kind, samples, model):
+    """LeastSquares (kind 0) / NonMinimalSolver (kind 1) on one sample (three index
+    lists) from `model` (dict with R, t, scale, offset0, offset1, focal0, focal1;
+    problem units).  Returns (refined model dict, ran)."""
+    n = len(d0)
+    m = OrModel()
+    m.R[:] = list(np.asarray(model["R"], dtype=np.float64).reshape(9))
+    m.t[:] = list(np.asarray(model["t"], dtype=np.float64).reshape(3))
+    for k in ("scale", "offset0", "offset1", "focal0", "focal1"):
+        setattr(m, k, float(model[k]))
+    ss = [np.ascontiguousarray(np.asarray(s, dtype=np.int32).reshape(-1)) for s in samples]
+    ip = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    ran = lib().oracle_least_squares(
+        variant, ctypes.c_int64(n), _dp(_c(x0)), _dp(_c(x1)), _dp(_c(d0)), _dp(_c(d1)), _dp(_c(min_depth)),
+        _dp(_c(cam0)), _dp(_c(cam1)), ctypes.byref(opts), ctypes.byref(cfg), int(kind), ip(ss[0]), len(ss[0]),
+        ip(ss[1]), len(ss[1]), ip(ss[2]), len(ss[2]), ctypes.byref(m))
+    return model_to_dict(m), bool(ran)
+
+
 def estimate(variant, x0, x1, d0, d1, min_depth, cam0, cam1, opts, cfg):
     """Returns (model dict, stats struct, [inlier index arrays x3])."""
     n = len(d0)

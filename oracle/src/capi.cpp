@@ -188,6 +188,32 @@ int oracle_score_models(int variant, int64_t n, const double *x0, const double *
     return 0;
 }
 
+// LeastSquares (kind 0) / NonMinimalSolver (kind 1) of the estimators on one sample
+// (three index lists); model in/out in problem units.  Returns 1 when the solver ran,
+// 0 when the sample is too small (model unchanged).
+int oracle_least_squares(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                         const double *d1, const double *min_depth, const double *cam0, const double *cam1,
+                         const or_ransac_options *o, const or_estimator_config *c, int32_t kind, const int32_t *s0,
+                         int32_t n0, const int32_t *s1, int32_t n1, const int32_t *s2, int32_t n2, or_model *model) {
+    oracle::Options opts = to_opts(o);
+    const double md0[2] = {0, 0};
+    oracle::Problem P = oracle::make_problem((oracle::Variant)variant, (int)n, x0, x1, d0, d1,
+                                             min_depth ? min_depth : md0, cam0, cam1, to_cfg(c), &opts);
+    std::vector<std::vector<int>> sample(3);
+    sample[0].assign(s0, s0 + n0);
+    sample[1].assign(s1, s1 + n1);
+    sample[2].assign(s2, s2 + n2);
+    oracle::Model m = get_model(model);
+    const int kmd = (variant == 0) ? 3 : 4, kpt = (variant == 0) ? 5 : (variant == 1 ? 6 : 7);
+    const bool small = (n0 < kmd && n1 < kmd) || n2 < kpt;
+    if (kind == 1)
+        oracle::non_minimal_solver(P, sample, 0, &m);
+    else
+        oracle::least_squares(P, sample, 0, &m);
+    put_model(m, model);
+    return small ? 0 : 1;
+}
+
 int oracle_estimate(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
                     const double *min_depth, const double *cam0, const double *cam1, const or_ransac_options *o,
                     const or_estimator_config *c, or_model *out, or_stats *st, int32_t *inlier_idx) {

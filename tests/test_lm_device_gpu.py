@@ -1,0 +1,108 @@
+"""Batched device LM (kernels/lm_device.h) against the oracle's
+LeastSquares / NonMinimalSolver (the Ceres restatement of src/optimizer.h:48-125 over
+src/cost_functions.h:16-387, parity unpinned: Ceres is not vendored).  Many problems of
+one pair in one launch: subsets of the three data types as the LO draws them, start
+models perturbed from the ground truth, all three variants, both solver kinds, the
+non-monotonic step evaluator on and off, and the EPI_ONLY / MD_ONLY LO modes."""
+import numpy as np
+import pytest
+
+import madpose
+import oracle
+from madpose_amd import synthetic
+from tests.helpers import oracle_cfg, oracle_opts, rot_angle_deg
+
+pytestmark = pytest.mark.gpu
+
+KIND = {0: "calibrated", 1: "shared_focal", 2: "two_focal"}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def require_gpu():
+    if madpose.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X")
+
+
+def _small_rot(rng, deg):
+    a = rng.standard_normal(3)
+    a *= np.deg2rad(deg) / np.linalg.norm(a)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    th = np.linalg.norm(a)
+    K /= th
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def _problems(rng, p, variant, norm_scale, count, est):
+    """LO-like problems: start models near the estimator's own result `est` (problem
+    units), residual blocks drawn as the LO draws them (subsets of the inliers, some
+    with outliers, and all-inlier fits)."""
+    inl = np.flatnonzero(p["inlier_mask"])
+    out = []
+    for j in range(count):
+        sizes = [int(rng.integers(0, 150)), int(rng.integers(0, 150)), int(rng.integers(5, 300))]
+        if j % 5 == 0:
+            sizes = [len(inl), len(inl), len(inl)]  # an all-inlier fit (the big LO problems)
+        lists = [rng.choice(inl, min(s, len(inl)), replace=False) for s in sizes]
+        if j % 3 == 0:  # a few outliers, as a relaxed-threshold inlier set holds them
+            out_idx = np.flatnonzero(~p["inlier_mask"])
+            lists = [np.r_[l, rng.choice(out_idx, len(l) // 30, replace=False)] for l in lists]
+        lists = [np.sort(l) for l in lists]
+        R = est.R() @ _small_rot(rng, 0.5)
+        t = est.t() * (1 + 0.02 * rng.standard_normal(3))
+        sc, o0, o1 = est.scale * (1 + 0.01 * rng.standard_normal()), est.offset0, est.offset1
+        if variant == 0:
+            m = madpose.PoseScaleOffset(R, t, sc, o0, o1)
+        elif variant == 1:
+            m = madpose.PoseScaleOffsetSharedFocal(R, t, sc, o0, o1, est.focal / norm_scale * 1.02)
+        else:
+            m = madpose.PoseScaleOffsetTwoFocal(R, t, sc, o0, o1, est.focal0 / norm_scale * 1.02,
+                                                est.focal1 / norm_scale * 0.98)
+        out.append((j % 2, lists, m))
+    return out
+
+
+def _oracle_model(m, variant):
+    d = dict(R=m.R(), t=m.t(), scale=m.scale, offset0=m.offset0, offset1=m.offset1, focal0=1.0, focal1=1.0)
+    if variant == 1:
+        d["focal0"] = d["focal1"] = m.focal
+    elif variant == 2:
+        d["focal0"], d["focal1"] = m.focal0, m.focal1
+    return d
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("nonmono,lo_type", [(True, 0), (False, 0), (True, 1), (True, 2)])
+def test_device_lm_matches_oracle(variant, nonmono, lo_type):
+    rng = np.random.default_rng(100 + variant)
+    p = synthetic.make_pair(40 + variant, n=800) if variant < 2 else synthetic.config_pair(4, seed=40)
+    o, c = synthetic.example_options(KIND[variant], iterations=100)
+    c.ceres_use_nonmonotonic_steps = nonmono
+    c.LO_type = lo_type
+    cam0, cam1 = (p["K0"], p["K1"]) if variant == 0 else (p["pp0"], p["pp1"])
+    args = (p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], cam0, cam1)
+    _, _, norm_scale = oracle.score_models(variant, *args[:4], cam0, cam1, oracle_opts(o), oracle_cfg(c), [])
+    fn = [madpose.HybridEstimatePoseScaleOffset, madpose.HybridEstimatePoseScaleOffsetSharedFocal,
+          madpose.HybridEstimatePoseScaleOffsetTwoFocal][variant]
+    est, _ = fn(*args, o, synthetic.example_options(KIND[variant], iterations=100)[1])
+    probs = _problems(rng, p, variant, norm_scale, 24, est)
+    got = madpose.lm_refine_batch(variant, *args, o, c, probs)
+    checked = 0
+    for (kind, lists, m0), (m, st) in zip(probs, got):
+        ref, ran = oracle.least_squares(variant, *args, oracle_opts(o), oracle_cfg(c), kind, lists,
+                                        _oracle_model(m0, variant))
+        if not ran:
+            assert st == 3
+            assert np.array_equal(m.pose, m0.pose)
+            continue
+        assert st in (0, 1, 2)
+        assert rot_angle_deg(m.R(), ref["R"]) < 1e-6
+        np.testing.assert_allclose(m.t(), ref["t"], rtol=1e-7, atol=1e-9)
+        for k in ("scale", "offset0", "offset1"):
+            assert abs(getattr(m, k) - ref[k]) <= 1e-7 * (1 + abs(ref[k])), k
+        if variant == 1:
+            assert abs(m.focal - ref["focal0"]) <= 1e-7 * ref["focal0"]
+        elif variant == 2:
+            assert abs(m.focal0 - ref["focal0"]) <= 1e-7 * ref["focal0"]
+            assert abs(m.focal1 - ref["focal1"]) <= 1e-7 * ref["focal1"]
+        checked += 1
+    assert checked >= 12
