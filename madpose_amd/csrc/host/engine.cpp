@@ -197,6 +197,23 @@ struct SweepSlot {
     int flip = 0;
     int *h_flag = nullptr, *d_flag = nullptr; // one completion flag per workgroup
     int seq = 0;
+    // device-LM staging (MADPOSE_DEVICE_LM): job + index lists up, model + status down
+    int64_t lm_cap = 0;
+    char *h_lm = nullptr, *d_lm = nullptr;
+    hipEvent_t lm_done = nullptr; // blocking-sync event: the waiting thread sleeps
+
+    void ensure_lm(int64_t nidx) {
+        if (!lm_done) MP_HIP(hipEventCreateWithFlags(&lm_done, hipEventBlockingSync | hipEventDisableTiming));
+        if (nidx <= lm_cap) return;
+        if (h_lm) hipHostFree(h_lm);
+        if (d_lm) hipFree(d_lm);
+        const size_t bytes = lm_bytes(nidx);
+        MP_HIP(hipHostMalloc(&h_lm, bytes, hipHostMallocDefault));
+        MP_HIP(hipMalloc(&d_lm, bytes));
+        lm_cap = nidx;
+    }
+    // layout: LmJob | Model out | int status | pad | int idx[nidx]
+    static size_t lm_bytes(int64_t nidx) { return 512 + sizeof(int) * (size_t)nidx; }
 
     void release() {
         if (h_out) hipHostFree(h_out);
@@ -468,6 +485,38 @@ struct Problem {
     double norm_scale = 1.0;
 };
 
+// Ceres settings of one LeastSquares / NonMinimalSolver call (the flags of
+// Run::least_squares; src/hybrid_pose_estimator.cpp:203, 281 and the SF/TF analogues)
+LmJob make_lm_job(const Problem &P, const EstimatorConfig &cfg, const int *sizes, int off, bool nonminimal,
+                  const Model &m) {
+    LmJob J;
+    std::memset(&J, 0, sizeof(J));
+    const bool use_reproj = cfg.lo_type != 1, use_sampson = cfg.lo_type != 2;
+    const int v = P.C.variant;
+    J.off0 = off;
+    J.n0 = use_reproj ? sizes[0] : 0;
+    J.off1 = off + sizes[0];
+    J.n1 = use_reproj ? sizes[1] : 0;
+    J.off2 = off + sizes[0] + sizes[1];
+    J.n2 = use_sampson ? sizes[2] : 0;
+    J.use_shift = (v == kCal || (v == kSF && nonminimal)) ? cfg.use_shift : 1;
+    J.min_depth_constraint = cfg.min_depth_constraint;
+    if (P.C.scale_only) { // HybridPoseOptimizerScaleOnly: offsets constant, unbounded
+        J.use_shift = 0;
+        J.min_depth_constraint = 0;
+    }
+    J.w_sampson = v == kCal ? std::sqrt(P.H.sampson_squared_weight) /
+                                  (1.0 / (P.C.K0[0] + P.C.K0[4]) + 1.0 / (P.C.K1[0] + P.C.K1[4]))
+                            : std::sqrt(P.H.sampson_squared_weight);
+    J.ftol = cfg.ftol;
+    J.gtol = cfg.gtol;
+    J.ptol = cfg.ptol;
+    J.max_iter = (int)cfg.max_iter;
+    J.nonmonotonic = cfg.nonmonotonic ? 1 : 0;
+    J.m = m;
+    return J;
+}
+
 Problem make_problem(const PairInput &in, const RansacOptions &o, const EstimatorConfig &cfg) {
     Problem P;
     const int n = (int)in.n;
@@ -738,10 +787,47 @@ class Run {
     }
 
     // --- LO (src/hybrid_ransac.h:383-538) ---
-    void least_squares(const std::vector<int> sample[3], Model *m, bool nonminimal) {
+    // The batched device LM (kernels/lm_device.h) on the lane's stream instead of the
+    // host LM (MADPOSE_DEVICE_LM=1).  The issuing thread sleeps on a blocking-sync event
+    // meanwhile, which frees its core for other pairs in flight (estimate_batch).
+    bool device_lm_ = false;
+    void least_squares_device(Lane &L, const std::vector<int> sample[3], Model *m, bool nonminimal) {
+        SweepSlot &sl = *L.slot;
+        const int sz[3] = {(int)sample[0].size(), (int)sample[1].size(), (int)sample[2].size()};
+        const int64_t nidx = (int64_t)sz[0] + sz[1] + sz[2];
+        sl.ensure_lm(nidx);
+        constexpr size_t kJob = 0, kOut = 256, kSt = 448, kIdx = 512;
+        static_assert(sizeof(LmJob) <= kOut && kOut + sizeof(Model) <= kSt, "LM staging layout");
+        const LmJob J = make_lm_job(P_, cfg_, sz, 0, nonminimal, *m);
+        std::memcpy(sl.h_lm + kJob, &J, sizeof(J));
+        int *hi = (int *)(sl.h_lm + kIdx);
+        for (int t = 0, o = 0; t < 3; ++t) {
+            std::memcpy(hi + o, sample[t].data(), sizeof(int) * sz[t]);
+            o += sz[t];
+        }
+        MP_HIP(hipMemcpyAsync(sl.d_lm, sl.h_lm, kIdx + sizeof(int) * (size_t)nidx, hipMemcpyHostToDevice, sl.stream));
+        MP_HIP(launch_lm_batch(sl.stream, D_, P_.C, (const LmJob *)(sl.d_lm + kJob), 1, (const int *)(sl.d_lm + kIdx),
+                               (Model *)(sl.d_lm + kOut), (int *)(sl.d_lm + kSt)));
+        MP_HIP(hipMemcpyAsync(sl.h_lm + kOut, sl.d_lm + kOut, kIdx - kOut, hipMemcpyDeviceToHost, sl.stream));
+        MP_HIP(hipEventRecord(sl.lm_done, sl.stream));
+        MP_HIP(hipEventSynchronize(sl.lm_done));
+        std::memcpy(m, sl.h_lm + kOut, sizeof(Model));
+    }
+
+    void least_squares(Lane &L, const std::vector<int> sample[3], Model *m, bool nonminimal) {
         const int kmd = variant_ == kCal ? 3 : 4;
         if (((int)sample[0].size() < kmd && (int)sample[1].size() < kmd) || (int)sample[2].size() < min_sample_size_)
             return;
+        if (device_lm_) {
+            auto t_lm = Clock::now();
+            least_squares_device(L, sample, m, nonminimal);
+            if (g_prof_on.load(std::memory_order_relaxed)) {
+                std::lock_guard<std::mutex> lk(g_prof_mu);
+                g_prof.lm_calls += 1;
+                g_prof.lm_wall_ms += 1e3 * secs(t_lm);
+            }
+            return;
+        }
         LMSettings S;
         S.use_reproj = cfg_.lo_type != 1;
         S.use_sampson = cfg_.lo_type != 2;
@@ -814,7 +900,7 @@ class Run {
             k[t] = std::min(ss_[st][t] * o_.min_sample_multiplicator, (int)inl[t].size());
         }
         if (use_all) {
-            least_squares(inl, m, false);
+            least_squares(L, inl, m, false);
             return;
         }
         const int total = (k[0] + k[1] + k[2]) * o_.min_sample_multiplicator;
@@ -825,7 +911,7 @@ class Run {
         shuffle_resize(*L.sel, total, &all);
         std::vector<int> smp[3];
         split(all, n_, smp);
-        least_squares(smp, m, false);
+        least_squares(L, smp, m, false);
     }
 
     // The non-minimal sample of an LO step is unusable (NonMinimalSolver returns 0,
@@ -853,7 +939,7 @@ class Run {
         Model m = m_init;
         std::vector<int> smp[3];
         split(sample_all, n_, smp);
-        least_squares(smp, &m, true);
+        least_squares(L, smp, &m, true);
         out.updates.emplace_back(score(L, m), m);
         lsq_fit(L, thr_, st, &m, false);
         double cur[3] = {thr[0], thr[1], thr[2]};
@@ -1046,6 +1132,8 @@ void Run::run(Model *best, Stats *S) {
     {
         const char *e = std::getenv("MADPOSE_LO_PARALLEL");
         lo_parallel_ = !(e && e[0] == '0') && o_.num_lo_steps > 1;
+        const char *d = std::getenv("MADPOSE_DEVICE_LM");
+        device_lm_ = d && d[0] == '1';
     }
     if (lo_parallel_) {
         if (!X_.lo_workers) X_.lo_workers.reset(new LoWorkers(kLoLanes));
@@ -1255,7 +1343,7 @@ void Run::run(Model *best, Stats *S) {
     if (o_.final_least_squares) {
         auto t0 = Clock::now();
         Model refined = *best;
-        least_squares(S->inlier_indices, &refined, false);
+        least_squares(lanes_[0], S->inlier_indices, &refined, false);
         const double sc = score(lanes_[0], refined);
         if (sc < S->best_model_score) {
             S->best_model_score = sc;
@@ -1349,38 +1437,6 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
     MP_HIP(hipStreamSynchronize(X.stream));
     hipFree(d_recs);
     hipFree(d_sc);
-}
-
-// Ceres settings of one LeastSquares / NonMinimalSolver call (the flags of
-// Run::least_squares; src/hybrid_pose_estimator.cpp:203, 281 and the SF/TF analogues)
-LmJob make_lm_job(const Problem &P, const EstimatorConfig &cfg, const int *sizes, int off, bool nonminimal,
-                  const Model &m) {
-    LmJob J;
-    std::memset(&J, 0, sizeof(J));
-    const bool use_reproj = cfg.lo_type != 1, use_sampson = cfg.lo_type != 2;
-    const int v = P.C.variant;
-    J.off0 = off;
-    J.n0 = use_reproj ? sizes[0] : 0;
-    J.off1 = off + sizes[0];
-    J.n1 = use_reproj ? sizes[1] : 0;
-    J.off2 = off + sizes[0] + sizes[1];
-    J.n2 = use_sampson ? sizes[2] : 0;
-    J.use_shift = (v == kCal || (v == kSF && nonminimal)) ? cfg.use_shift : 1;
-    J.min_depth_constraint = cfg.min_depth_constraint;
-    if (P.C.scale_only) { // HybridPoseOptimizerScaleOnly: offsets constant, unbounded
-        J.use_shift = 0;
-        J.min_depth_constraint = 0;
-    }
-    J.w_sampson = v == kCal ? std::sqrt(P.H.sampson_squared_weight) /
-                                  (1.0 / (P.C.K0[0] + P.C.K0[4]) + 1.0 / (P.C.K1[0] + P.C.K1[4]))
-                            : std::sqrt(P.H.sampson_squared_weight);
-    J.ftol = cfg.ftol;
-    J.gtol = cfg.gtol;
-    J.ptol = cfg.ptol;
-    J.max_iter = (int)cfg.max_iter;
-    J.nonmonotonic = cfg.nonmonotonic ? 1 : 0;
-    J.m = m;
-    return J;
 }
 
 // the same problems through the host LM (host/lm.cpp) -- test hook (mp_debug_lm_refine_host)
