@@ -415,27 +415,31 @@ __device__ inline void lm_block_sampson(const PairData &D, const PairConst &C, c
 
 constexpr int kLmBlock = 256;
 
-// Shared state of one problem (LDS).
+// Shared state of one problem (LDS).  The reduced normal equations stay in the full
+// NA-parameter layout (packed upper triangle, then g, then the cost); parameters that
+// are inactive for the call are masked to an identity row with zero gradient, which
+// leaves every operation on the active ones exactly as in the compacted system of
+// host/lm.cpp (the extra terms are exact zeros).
 template <int NA> struct LmShared {
     static constexpr int kPack = NA * (NA + 1) / 2, kRed = kPack + NA + 1;
     LmParams x, c, best;
     double part[kLmBlock / 64][kRed]; // per-wave reduced accumulators
-    double H[kLNFull * kLNFull], g[kLNFull], Hc[kLNFull * kLNFull], gc[kLNFull], A[kLNFull * kLNFull];
-    double sc[kLNFull], y[kLNFull], d[kLNFull]; // lane 0's step vectors (LDS: runtime-indexed)
+    double red[2][kRed];              // the systems of x (red[cur]) and of the candidate
+    double d[NA];                     // the step (lane 0)
+    LmSampsonConst K;                 // Sampson constants of the parameter set being evaluated
     double lo[kLNFull];
     int has_lo[kLNFull];
-    double cost, cand_cost;
-    LmSampsonConst K; // Sampson constants of the parameter set being evaluated
     int col[kLNFull];
-    int n;
-    int action; // 0 stop, 1 evaluate the candidate sh.c, 2 retry the step (no evaluation)
+    int cur;
+    int action; // 0 stop, 1 evaluate the candidate sh.c, 2 propose a step
 };
 
-// reduce every lane's accumulator over the workgroup into (H, g, cost) in the active
-// layout (lane 0 holds the result; waves summed in order)
-template <int NA>
-__device__ inline void lm_reduce(LmAcc<NA> &acc, LmShared<NA> &sh, double *H, double *g, double *cost) {
-    constexpr int kPack = LmShared<NA>::kPack;
+__device__ inline int lm_up(int a, int b, int na) { return a * na - a * (a - 1) / 2 + (b - a); } // a <= b
+
+// reduce every lane's accumulator over the workgroup into out[kRed] (LDS): the four
+// waves' butterflies, then one entry per thread summed over the waves in order
+template <int NA> __device__ inline void lm_reduce(LmAcc<NA> &acc, LmShared<NA> &sh, double *out) {
+    constexpr int kPack = LmShared<NA>::kPack, kRed = LmShared<NA>::kRed;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int q = 0; q < kPack; ++q) {
@@ -452,35 +456,19 @@ __device__ inline void lm_reduce(LmAcc<NA> &acc, LmShared<NA> &sh, double *H, do
         if (lane == 0) sh.part[wave][kPack + NA] = v;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int n = sh.n;
-        for (int k = 0; k < n * n; ++k) H[k] = 0.0;
-        for (int k = 0; k < n; ++k) g[k] = 0.0;
-        int q = 0;
-        for (int a = 0; a < NA; ++a) {
-            const int ca = sh.col[a];
-            double ga = 0.0;
-            for (int w = 0; w < kLmBlock / 64; ++w) ga += sh.part[w][kPack + a];
-            if (ca >= 0) g[ca] = ga;
-            for (int b = a; b < NA; ++b, ++q) {
-                const int cb = sh.col[b];
-                if (ca >= 0 && cb >= 0) {
-                    double h = 0.0;
-                    for (int w = 0; w < kLmBlock / 64; ++w) h += sh.part[w][q];
-                    H[ca * n + cb] = H[cb * n + ca] = h;
-                }
-            }
-        }
-        double c = 0.0;
-        for (int w = 0; w < kLmBlock / 64; ++w) c += sh.part[w][kPack + NA];
-        *cost = c;
+    if (threadIdx.x < kRed) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < kLmBlock / 64; ++w) v += sh.part[w][threadIdx.x];
+        out[threadIdx.x] = v;
     }
+    __syncthreads();
 }
 
-// cost and normal equations of parameter set p over the job's blocks
+// cost and normal equations of parameter set p over the job's blocks into out
 template <int V, int NA>
 __device__ inline void lm_evaluate(const PairData &D, const PairConst &C, const LmJob &J, const int *idx,
-                                   const LmParams &p, LmShared<NA> &sh, double *H, double *g, double *cost) {
+                                   const LmParams &p, LmShared<NA> &sh, double *out) {
     LmAcc<NA> acc;
     acc.clear();
     const int nb = J.n0 + J.n1 + J.n2;
@@ -494,33 +482,78 @@ __device__ inline void lm_evaluate(const PairData &D, const PairConst &C, const 
     for (; b < J.n0 + J.n1; b += kLmBlock) lm_block_reproj1<V, NA>(D, C, p, idx[J.off1 + b - J.n0], true, acc);
     for (; b < nb; b += kLmBlock)
         lm_block_sampson<V, NA>(D, C, p, sh.K, J.w_sampson, idx[J.off2 + b - J.n0 - J.n1], true, acc);
-    lm_reduce<NA>(acc, sh, H, g, cost);
+    lm_reduce<NA>(acc, sh, out);
 }
 
-// Cholesky solve of the n x n SPD system A x = b in place (host/lm.cpp chol_solve)
-__device__ inline bool lm_chol_solve(double *A, int n, double *b) {
-    for (int j = 0; j < n; ++j) {
-        double d = A[j * n + j];
-        for (int k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
-        if (!(d > 0)) return false;
-        d = sqrt(d);
-        A[j * n + j] = d;
-        for (int i = j + 1; i < n; ++i) {
-            double s = A[i * n + j];
-            for (int k = 0; k < j; ++k) s -= A[i * n + k] * A[j * n + k];
-            A[i * n + j] = s / d;
+// gradient max-norm over the active parameters
+template <int NA> __device__ inline double lm_gmax(const double *red, const bool (&act)[NA]) {
+    double v = 0.0;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+        if (act[a]) v = fmax(v, fabs(red[LmShared<NA>::kPack + a]));
+    return v;
+}
+
+// The LM step of host/lm.cpp (Jacobi scaling, clamped diagonal / radius, Cholesky) in
+// registers with compile-time indices; d = 0 on inactive parameters.  False when the
+// damped system is not positive definite.
+template <int NA>
+__device__ inline bool lm_step(const double *red, const bool (&act)[NA], double radius, double (&d)[NA]) {
+    constexpr int kP = NA * (NA + 1) / 2;
+    double L[kP]; // lower triangle, row-major packed: (i, j) at i (i + 1) / 2 + j
+    double sc[NA], y[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        const double h = act[a] ? red[lm_up(a, a, NA)] : 1.0;
+        sc[a] = 1.0 / (1.0 + sqrt(h));
+        y[a] = act[a] ? -red[kP + a] * sc[a] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) {
+            const double h = (act[i] && act[j]) ? red[lm_up(j, i, NA)] : (i == j ? 1.0 : 0.0);
+            L[i * (i + 1) / 2 + j] = h * sc[i] * sc[j];
+        }
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        double &a = L[j * (j + 1) / 2 + j];
+        a += fmin(fmax(a, 1e-6), 1e32) / radius;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        double dj = L[j * (j + 1) / 2 + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) dj -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+        ok = ok && (dj > 0);
+        dj = sqrt(dj);
+        L[j * (j + 1) / 2 + j] = dj;
+#pragma unroll
+        for (int i = j + 1; i < NA; ++i) {
+            double s2 = L[i * (i + 1) / 2 + j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) s2 -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+            L[i * (i + 1) / 2 + j] = s2 / dj;
         }
     }
-    for (int i = 0; i < n; ++i) {
-        double s = b[i];
-        for (int k = 0; k < i; ++k) s -= A[i * n + k] * b[k];
-        b[i] = s / A[i * n + i];
+    if (!ok) return false;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        double s2 = y[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) s2 -= L[i * (i + 1) / 2 + k] * y[k];
+        y[i] = s2 / L[i * (i + 1) / 2 + i];
     }
-    for (int i = n - 1; i >= 0; --i) {
-        double s = b[i];
-        for (int k = i + 1; k < n; ++k) s -= A[k * n + i] * b[k];
-        b[i] = s / A[i * n + i];
+#pragma unroll
+    for (int i = NA - 1; i >= 0; --i) {
+        double s2 = y[i];
+#pragma unroll
+        for (int k = i + 1; k < NA; ++k) s2 -= L[k * (k + 1) / 2 + i] * y[k];
+        y[i] = s2 / L[i * (i + 1) / 2 + i];
     }
+#pragma unroll
+    for (int a = 0; a < NA; ++a) d[a] = act[a] ? y[a] * sc[a] : 0.0;
     return true;
 }
 
@@ -535,9 +568,8 @@ template <int V>
 __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairConst C, const LmJob *jobs,
                                                            const int *idx, Model *out, int *status) {
     constexpr int NA = V == kCal ? kLF0 : (V == kSF ? kLF0 + 1 : kLNFull);
+    constexpr int kPack = LmShared<NA>::kPack;
     __shared__ LmShared<NA> sh;
-    double *lo_s = sh.lo;
-    int *has_lo_s = sh.has_lo;
     const LmJob &J = jobs[blockIdx.x]; // (read in place: uniform, kept out of registers)
     const bool t0 = threadIdx.x == 0;
     // ---- setup (lm_refine in host/lm.cpp) ----
@@ -545,31 +577,29 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
         const bool has_o0 = J.n0 > 0, has_s_o1 = J.n1 > 0;
         for (int k = 0; k < kLNFull; ++k) {
             sh.col[k] = -1;
-            has_lo_s[k] = 0;
-            lo_s[k] = 0.0;
+            sh.has_lo[k] = 0;
+            sh.lo[k] = 0.0;
         }
-        int n = 0;
-        for (int k = 0; k < 6; ++k) sh.col[k] = n++;
+        for (int k = 0; k < 6; ++k) sh.col[k] = k;
         if (has_s_o1) {
-            sh.col[kLS] = n++;
-            has_lo_s[kLS] = 1;
-            lo_s[kLS] = 1e-2;
+            sh.col[kLS] = kLS;
+            sh.has_lo[kLS] = 1;
+            sh.lo[kLS] = 1e-2;
         }
-        if (has_o0 && J.use_shift) sh.col[kLO0] = n++;
-        if (has_s_o1 && J.use_shift) sh.col[kLO1] = n++;
+        if (has_o0 && J.use_shift) sh.col[kLO0] = kLO0;
+        if (has_s_o1 && J.use_shift) sh.col[kLO1] = kLO1;
         if (J.min_depth_constraint) {
-            has_lo_s[kLO0] = has_lo_s[kLO1] = 1;
-            lo_s[kLO0] = -C.min_depth[0] + 1e-2;
-            lo_s[kLO1] = -C.min_depth[1] + 1e-2;
+            sh.has_lo[kLO0] = sh.has_lo[kLO1] = 1;
+            sh.lo[kLO0] = -C.min_depth[0] + 1e-2;
+            sh.lo[kLO1] = -C.min_depth[1] + 1e-2;
         }
-        if (V == kSF) sh.col[kLF0] = n++;
+        if (V == kSF) sh.col[kLF0] = kLF0;
         if (V == kTF) {
-            sh.col[kLF0] = n++;
-            sh.col[kLF1] = n++;
-            has_lo_s[kLF0] = has_lo_s[kLF1] = 1;
-            lo_s[kLF0] = lo_s[kLF1] = 1e-6;
+            sh.col[kLF0] = kLF0;
+            sh.col[kLF1] = kLF1;
+            sh.has_lo[kLF0] = sh.has_lo[kLF1] = 1;
+            sh.lo[kLF0] = sh.lo[kLF1] = 1e-6;
         }
-        sh.n = n;
         LmParams &x = sh.x;
         lm_rot_to_quat(J.m.R, x.q);
         lm_quat_to_rot(x.q, x.R);
@@ -580,12 +610,13 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
         x.f0 = J.m.focal0;
         x.f1 = J.m.focal1;
         sh.best = x;
+        sh.cur = 0;
         sh.action = 1;
         if (J.n0 + J.n1 + J.n2 == 0) sh.action = 0;
         // constant bounded blocks must start feasible (Ceres Program::IsFeasible)
         if (!J.use_shift && J.min_depth_constraint) {
-            if (has_o0 && x.o0 < lo_s[kLO0]) sh.action = 0;
-            if (has_s_o1 && x.o1 < lo_s[kLO1]) sh.action = 0;
+            if (has_o0 && x.o0 < sh.lo[kLO0]) sh.action = 0;
+            if (has_s_o1 && x.o1 < sh.lo[kLO1]) sh.action = 0;
         }
         if (J.n0 + J.n1 + J.n2 == 0)
             status[blockIdx.x] = 0;
@@ -597,45 +628,36 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
         if (t0) out[blockIdx.x] = J.m;
         return;
     }
-    lm_evaluate<V, NA>(D, C, J, idx, sh.x, sh, sh.H, sh.g, &sh.cost);
+    bool act[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) act[a] = sh.col[a] >= 0;
+    lm_evaluate<V, NA>(D, C, J, idx, sh.x, sh, sh.red[0]);
     // ---- trust-region loop (lane 0 decides, every lane evaluates) ----
     double radius = 1e4, decrease = 2.0;
     const int max_nonmono = J.nonmonotonic ? 5 : 0;
     double ref_cost = 0, min_cost = 0, cand_ref = 0, acc_ref = 0.0, acc_cand = 0.0;
     int n_nonmono = 0, iter = 0;
-    double *d = sh.d;
     if (t0) {
-        ref_cost = min_cost = cand_ref = sh.cost;
-        double gm = 0;
-        for (int a = 0; a < sh.n; ++a) gm = fmax(gm, fabs(sh.g[a]));
-        sh.action = (gm <= J.gtol) ? 0 : 2;
+        ref_cost = min_cost = cand_ref = sh.red[0][kPack + NA];
+        sh.action = (lm_gmax<NA>(sh.red[0], act) <= J.gtol) ? 0 : 2;
     }
     __syncthreads();
     while (sh.action != 0) {
         if (t0) {
-            // propose a step from x (repeated while the system is not positive definite)
+            // propose a step from x (repeated while the damped system is not positive definite)
+            const double *R = sh.red[sh.cur];
             sh.action = 0;
             while (iter < J.max_iter) {
                 ++iter;
-                const int n = sh.n;
-                double *sc = sh.sc, *y = sh.y;
-                double *A = sh.A;
-                for (int j = 0; j < n; ++j) sc[j] = 1.0 / (1.0 + sqrt(sh.H[j * n + j]));
-                for (int a = 0; a < n; ++a) {
-                    y[a] = -sh.g[a] * sc[a];
-                    for (int b = 0; b < n; ++b) A[a * n + b] = sh.H[a * n + b] * sc[a] * sc[b];
-                }
-                for (int j = 0; j < n; ++j) {
-                    const double dg = fmin(fmax(A[j * n + j], 1e-6), 1e32);
-                    A[j * n + j] += dg / radius;
-                }
-                if (!lm_chol_solve(A, n, y)) {
+                double d[NA];
+                if (!lm_step<NA>(R, act, radius, d)) {
                     radius /= decrease;
                     decrease *= 2.0;
                     if (radius < 1e-32) break;
                     continue;
                 }
-                for (int j = 0; j < n; ++j) d[j] = y[j] * sc[j];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) sh.d[a] = d[a];
                 // candidate = Plus(x, d), projected onto the bounds
                 const LmParams &x = sh.x;
                 LmParams c = x;
@@ -650,17 +672,18 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
                         c.q[2] = qd[0] * q[2] - qd[1] * q[3] + qd[2] * q[0] + qd[3] * q[1];
                         c.q[3] = qd[0] * q[3] + qd[1] * q[2] - qd[2] * q[1] + qd[3] * q[0];
                     }
+#pragma unroll
                     for (int k = 0; k < 3; ++k) c.t[k] = x.t[k] + d[3 + k];
-                    auto upd = [&](int slot, double v) {
+                    auto upd = [&](int slot, double v, double dv) {
                         if (sh.col[slot] < 0) return v;
-                        v += d[sh.col[slot]];
-                        return (has_lo_s[slot] && v < lo_s[slot]) ? lo_s[slot] : v;
+                        v += dv;
+                        return (sh.has_lo[slot] && v < sh.lo[slot]) ? sh.lo[slot] : v;
                     };
-                    c.s = upd(kLS, c.s);
-                    c.o0 = upd(kLO0, c.o0);
-                    c.o1 = upd(kLO1, c.o1);
-                    c.f0 = upd(kLF0, c.f0);
-                    c.f1 = upd(kLF1, c.f1);
+                    c.s = upd(kLS, c.s, d[kLS]);
+                    c.o0 = upd(kLO0, c.o0, d[kLO0]);
+                    c.o1 = upd(kLO1, c.o1, d[kLO1]);
+                    if (NA > kLF0) c.f0 = upd(kLF0, c.f0, d[NA > kLF0 ? kLF0 : 0]);
+                    if (NA > kLF1) c.f1 = upd(kLF1, c.f1, d[NA > kLF1 ? kLF1 : 0]);
                     lm_quat_to_rot(c.q, c.R);
                 }
                 double step2 = 0;
@@ -668,6 +691,7 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
                     const double dd[12] = {c.q[0] - x.q[0], c.q[1] - x.q[1], c.q[2] - x.q[2], c.q[3] - x.q[3],
                                            c.t[0] - x.t[0], c.t[1] - x.t[1], c.t[2] - x.t[2], c.s - x.s,
                                            c.o0 - x.o0,     c.o1 - x.o1,     c.f0 - x.f0,     c.f1 - x.f1};
+#pragma unroll
                     for (int k = 0; k < 12; ++k) step2 += dd[k] * dd[k];
                 }
                 if (sqrt(step2) <= J.ptol * (sqrt(lm_amb_norm2(x)) + J.ptol)) break; // parameter tolerance
@@ -678,18 +702,26 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
         }
         __syncthreads();
         if (sh.action == 0) break;
-        lm_evaluate<V, NA>(D, C, J, idx, sh.c, sh, sh.Hc, sh.gc, &sh.cand_cost);
+        lm_evaluate<V, NA>(D, C, J, idx, sh.c, sh, sh.red[sh.cur ^ 1]);
         if (t0) {
-            const int n = sh.n;
-            const double cost = sh.cost, cand_cost = sh.cand_cost;
+            const double *R = sh.red[sh.cur], *Rc = sh.red[sh.cur ^ 1];
+            const double cost = R[kPack + NA], cand_cost = Rc[kPack + NA];
             sh.action = 2;
             if (fabs(cost - cand_cost) <= J.ftol * cost) {
                 sh.action = 0; // function tolerance
             } else {
+                double d[NA];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) d[a] = sh.d[a];
                 double gd = 0, jd2 = 0;
-                for (int a = 0; a < n; ++a) {
-                    gd += sh.g[a] * d[a];
-                    for (int b = 0; b < n; ++b) jd2 += d[a] * sh.H[a * n + b] * d[b];
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    gd += (act[a] ? R[kPack + a] : 0.0) * d[a];
+#pragma unroll
+                    for (int b2 = 0; b2 < NA; ++b2) {
+                        const double h = (act[a] && act[b2]) ? R[a <= b2 ? lm_up(a, b2, NA) : lm_up(b2, a, NA)] : 0.0;
+                        jd2 += d[a] * h * d[b2];
+                    }
                 }
                 const double mcc = -(gd + 0.5 * jd2);
                 const double rho = (mcc > 0 && isfinite(cand_cost))
@@ -697,9 +729,7 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
                                        : -1.0;
                 if (rho > 1e-3) {
                     sh.x = sh.c;
-                    sh.cost = cand_cost;
-                    for (int k = 0; k < n * n; ++k) sh.H[k] = sh.Hc[k];
-                    for (int k = 0; k < n; ++k) sh.g[k] = sh.gc[k];
+                    sh.cur ^= 1;
                     // Ceres TrustRegionStepEvaluator::StepAccepted
                     acc_cand += mcc;
                     acc_ref += mcc;
@@ -722,9 +752,7 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
                     }
                     radius = fmin(1e16, radius / fmax(1.0 / 3.0, 1.0 - pow(2.0 * rho - 1.0, 3.0)));
                     decrease = 2.0;
-                    double gm = 0;
-                    for (int a = 0; a < n; ++a) gm = fmax(gm, fabs(sh.g[a]));
-                    if (gm <= J.gtol) sh.action = 0;
+                    if (lm_gmax<NA>(Rc, act) <= J.gtol) sh.action = 0;
                 } else {
                     radius /= decrease;
                     decrease *= 2.0;
