@@ -11,7 +11,7 @@
 //   3. finds its real roots with Sturm-sequence bisection,
 //   4. polishes every root with Newton steps on the original equations,
 //   5. recovers (R, t) with Horn's quaternion method.
-// The solution sets equal the reference's (tests/test_md_solvers.py pins this
+// The solution sets equal the reference's (tests/test_engine_gpu.py::test_md_solver_matches_reference_goldens pins this
 // against tests/golden/md_solvers.npz).
 #pragma once
 #include "mp_math.h"

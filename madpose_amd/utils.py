@@ -1,6 +1,6 @@
 """Pre/post-processing helpers of the reference's Python package (madpose/utils.py).
 
-Same names and semantics (pinned by tests/test_utils.py against outputs of the
+Same names and semantics (pinned by tests/test_utils_cpu.py and tests/test_get_depths_gpu.py against outputs of the
 reference recorded in tests/golden/utils.npz), plus the SuperGlue-style pose AUC used
 for the ScanNet-1500-style evaluation (not in the reference).
 """

@@ -22,7 +22,7 @@
 // whose real roots (companion matrix + Francis QR, wi == 0 exactly, the same
 // real-Schur convention as Eigen::EigenSolver) are polished with Newton steps on the
 // original distance equations.  The solution sets agree with the reference
-// prototypes to ~1e-12 (tests/test_oracle_md.py pins this against
+// prototypes to ~1e-12 (tests/test_oracle_cpu.py::test_oracle_md_matches_reference_goldens pins this against
 // tests/golden/md_solvers.npz).  Root filters follow the reference:
 // tf/sf skip negative focal terms (:283, :470); roots with a2^2 <= 0 would give
 // NaN scales in the reference and are dropped here (they never survive the
