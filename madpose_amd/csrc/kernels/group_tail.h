@@ -34,13 +34,21 @@ __device__ inline int gsum8(int v) {
     return v + dpp_i<dpp::kHalfMirror>(v);
 }
 
-// group g of the launch = root k of sample idx, root-major as pt_tail_kernel
+// group g of the launch = root k of sample idx, root-major as pt_tail_kernel.
+// G = 8: one 8-lane group per (root, sample), every lane tests its point under the
+// four recoverPose candidates in turn.  G = 32: four 8-lane subgroups per (root,
+// sample), subgroup c tests candidate c (one DLT triangulation per lane instead of
+// four), the four good-point counts are exchanged across the subgroups, and the
+// subgroups then run the depth fit redundantly (subgroup 0 writes).
+template <int G>
 __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                             const double *cand, const int *ncand, const int *samples,
                                                             Model *slots, int *valid) {
+    static_assert(G == 8 || G == 32, "8 or 32 lanes per (root, sample)");
     constexpr int K = 7;
     const int lane = threadIdx.x % kTail;
-    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kTail);
+    const int sub = (threadIdx.x % G) / kTail; // candidate of this subgroup (G = 32)
+    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
     const int k = gid / nlist, idx = gid - k * nlist;
     if (k >= 3 || k >= ncand[idx]) return; // the whole group leaves together
     const int *s = samples + (size_t)list[idx] * kSampleStride;
@@ -63,8 +71,15 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
     RecoverCands rc;
     recover_pose_candidates(E, rc);
     int good[4];
+    if (G == 8) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) good[c] = gsum8((has && recover_pose_good(rc, c, p0[0], p1[0], 1e9)) ? 1 : 0);
+        for (int c = 0; c < 4; ++c) good[c] = gsum8((has && recover_pose_good(rc, c, p0[0], p1[0], 1e9)) ? 1 : 0);
+    } else {
+        const int mine = gsum8((has && recover_pose_good(rc, sub, p0[0], p1[0], 1e9)) ? 1 : 0);
+        const int base = (threadIdx.x & 63) & ~(G - 1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) good[c] = __shfl(mine, base + kTail * c, 64);
+    }
     Model m;
     recover_pose_select(rc, good, m.R, m.t);
     m.scale = 1.0;
@@ -77,7 +92,7 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
     const bool shift = C.use_shift != 0 && !C.scale_only, mdc = C.min_depth_constraint != 0;
     const bool ok = point_model_tail_r<1>(p0, p1, dd0, dd1, use, (double)K, m.focal0, m.focal1, shift, mdc,
                                           C.min_depth, m, [](double v) { return gsum8(v); });
-    if (lane == 0) {
+    if (lane == 0 && sub == 0) {
         const size_t q = (size_t)idx * kPtSlotStride + k; // PtTraits<kTF>::kPosesPerRoot == 1
         if (ok) slots[q] = m;
         valid[q] = ok ? 1 : 0;

@@ -865,8 +865,18 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
         static const bool lane_tail = std::getenv("MADPOSE_TAIL_LANE") != nullptr;
         const long lanes = (long)nlist * PtTraits<v>::kRoots;
         const int tgrid = (int)((lanes * kTail + 63) / 64);
-        if (v == kTF && !lane_tail)
-            pt_tail7_group_kernel<<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots, W.valid);
+        // two-focal: 8 lanes per (root, sample); MADPOSE_TAIL7_LANES=32 runs the four
+        // recoverPose candidates on four subgroups (measured slower: DESIGN.md §8)
+        static const int tail7 = [] {
+            const char *e = std::getenv("MADPOSE_TAIL7_LANES");
+            return (e && e[0] == '3') ? 32 : 8;
+        }();
+        if (v == kTF && !lane_tail && tail7 == 32)
+            pt_tail7_group_kernel<32><<<(int)((lanes * 32 + 63) / 64), 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand,
+                                                                                   samples, W.slots, W.valid);
+        else if (v == kTF && !lane_tail)
+            pt_tail7_group_kernel<8><<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots,
+                                                          W.valid);
         else if (v == kCal && !lane_tail)
             pt_tail5_group_kernel<<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots, W.valid);
         else if (v == kSF && !lane_tail)
