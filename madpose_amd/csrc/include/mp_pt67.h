@@ -760,6 +760,24 @@ MP_HD int sixpt_poses_for_root(const double (&M)[3][10][10], const double (&N)[3
         y -= Jtr[1][0];
         w -= Jtr[2][0];
     }
+    // a root of the interpolated q(u) that is not a root of the system leaves a
+    // residual after the polish: the ten equations must vanish to 1e-8 of their scale
+    {
+        double mv[10], dxv[10], dyv[10];
+        mono2(x, y, mv, dxv, dyv);
+        double rr = 0, ss = 0;
+        for (int r = 0; r < 10; ++r) {
+            double res = 0, mag = 0;
+            for (int cc = 0; cc < 10; ++cc) {
+                const double t = (M[0][r][cc] + w * (M[1][r][cc] + w * M[2][r][cc])) * mv[cc];
+                res += t;
+                mag += fabs(t);
+            }
+            rr += res * res;
+            ss += mag * mag;
+        }
+        if (!(rr <= 1e-16 * ss)) return 0;
+    }
     if (!(w > 0.0)) return 0;
     const double foc = 1.0 / sqrt(w);
     double Fm[9], nn = 0.0;
@@ -805,7 +823,20 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
     if (kStop <= 2) return nr;
     int nout = 0;
     for (int k = 0; k < nr; ++k) nout += sixpt_poses_for_root(M, N, roots[k], x1, x2, out, nout, kmax);
-    return nout;
+    // two roots that the polish took to the same solution give the same pose twice:
+    // keep the first (as pt_compact_kernel does for the estimator's batches)
+    int n = 0;
+    for (int q = 0; q < nout; ++q) {
+        bool dup = false;
+        for (int p = 0; p < n && !dup; ++p) {
+            bool same = fabs(out[p].focal0 - out[q].focal0) <= 1e-10 * fabs(out[q].focal0);
+            for (int e = 0; e < 9 && same; ++e) same = fabs(out[p].R[e] - out[q].R[e]) <= 1e-10;
+            for (int e = 0; e < 3 && same; ++e) same = fabs(out[p].t[e] - out[q].t[e]) <= 1e-10 * (1.0 + fabs(out[q].t[e]));
+            dup = same;
+        }
+        if (!dup) out[n++] = out[q];
+    }
+    return n;
 }
 
 // Two-focal candidate of one fundamental matrix: Bougnoux focals, E = K1^T F K0,

@@ -189,6 +189,12 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
     const double *cd = cand + (size_t)idx * kPtCandStride;
     const bool row_lane = r < 10;
     double w = 1.0 / cd[27 + k];
+    // a root that yields no pose clears its slots (they hold an earlier batch's models)
+    auto no_pose = [&]() {
+        if (r == 0)
+#pragma unroll
+            for (int j = 0; j < kPoses; ++j) valid[(size_t)idx * kPtSlotStride + kPoses * k + j] = 0;
+    };
 
     // ---- row r of the pencil and of A(w) ----
     double m0[10], m1[10], m2[10], a[10];
@@ -237,7 +243,10 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
         cols |= 1u << pcol;
         __syncthreads();
     }
-    if (!ok) return; // (uniform)
+    if (!ok) { // (uniform)
+        no_pose();
+        return;
+    }
     // back substitution (lane 0): free column = the one never pivoted, z = 1 there
     if (r == 0) {
         const int fc = __ffs(~cols & 0x3ffu) - 1;
@@ -252,7 +261,10 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
     }
     __syncthreads();
     const double v9 = sh.z[g][9];
-    if (v9 == 0.0) return; // (uniform)
+    if (v9 == 0.0) { // (uniform)
+        no_pose();
+        return;
+    }
     double x = sh.z[g][7] / v9, y = sh.z[g][8] / v9;
 
     // ---- Gauss-Newton polish of (x, y, w), rows summed over the group ----
@@ -281,7 +293,26 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
         y -= Jtr[1][0];
         w -= Jtr[2][0];
     }
-    if (!(w > 0.0)) return;
+    // a root of the interpolated q(u) that is not a root of the system (its small
+    // coefficients carry rounding) leaves a residual after the polish:
+    // keep the root only if the ten equations vanish to 1e-8 of their term scale
+    {
+        double mv[10], dxv[10], dyv[10];
+        mono2(x, y, mv, dxv, dyv);
+        double res = 0, mag = 0;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            const double t = (m0[c] + w * (m1[c] + w * m2[c])) * mv[c];
+            res += t;
+            mag += fabs(t);
+        }
+        const double rr = gsum16(res * res), ss = gsum16(mag * mag);
+        if (!(rr <= 1e-16 * ss)) w = -1.0; // (uniform)
+    }
+    if (!(w > 0.0)) {
+        no_pose();
+        return;
+    }
     const double foc = 1.0 / sqrt(w);
     double Fm[9], nn = 0.0;
 #pragma unroll

@@ -469,7 +469,22 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
     int n = 0;
     for (int q = 0; q < total; ++q) {
         if (!valid[(size_t)idx * kSlotStride + q] || n >= maxm) continue;
-        put_model(C, slots[(size_t)idx * kSlotStride + q], b, n++, maxm, models, recs);
+        const Model &m = slots[(size_t)idx * kSlotStride + q];
+        // shared focal: two roots of the interpolated q(u) that the polish took to the
+        // same solution of the system give the same pose twice; keep the first
+        if (V == kSF) {
+            bool dup = false;
+            for (int p = 0; p < q && !dup; ++p) {
+                if (!valid[(size_t)idx * kSlotStride + p]) continue;
+                const Model &o = slots[(size_t)idx * kSlotStride + p];
+                bool same = fabs(o.focal0 - m.focal0) <= 1e-10 * fabs(m.focal0);
+                for (int e = 0; e < 9 && same; ++e) same = fabs(o.R[e] - m.R[e]) <= 1e-10;
+                for (int e = 0; e < 3 && same; ++e) same = fabs(o.t[e] - m.t[e]) <= 1e-10 * (1.0 + fabs(m.t[e]));
+                dup = same;
+            }
+            if (dup) continue;
+        }
+        put_model(C, m, b, n++, maxm, models, recs);
     }
     counts[b] = n;
 }
