@@ -722,6 +722,29 @@ MP_HD int sixpt_roots(const double (&M)[3][10][10], double (&roots)[15]) {
     return n;
 }
 
+// (x, y) from a null vector v of M(w), v ~ (x^3, x^2 y, x y^2, y^3, x^2, x y, y^2, x,
+// y, 1): each coordinate from the ratio of monomials with the largest denominator
+// (x = v7/v9 = v4/v7 = v0/v4 = v5/v8 = v2/v6, y = v8/v9 = v6/v8 = v3/v6 = v5/v7 =
+// v1/v4).  v7/v9 alone loses the digits of a solution far from the origin (|x| ~ 1e2
+// puts v9 ~ 1e-6 of |v|, below the elimination's absolute accuracy) and the polish
+// then starts from a wrong point; the largest denominators are accurate relative to
+// |v|.  For solutions near the origin the choice is v7/v9, v8/v9 as before.
+MP_HD bool sixpt_xy_from_monomials(const double (&v)[10], double *x, double *y) {
+    double nx = v[7], dx = v[9], ny = v[8], dy = v[9];
+    if (fabs(v[7]) > fabs(dx)) { nx = v[4]; dx = v[7]; }
+    if (fabs(v[4]) > fabs(dx)) { nx = v[0]; dx = v[4]; }
+    if (fabs(v[8]) > fabs(dx)) { nx = v[5]; dx = v[8]; }
+    if (fabs(v[6]) > fabs(dx)) { nx = v[2]; dx = v[6]; }
+    if (fabs(v[8]) > fabs(dy)) { ny = v[6]; dy = v[8]; }
+    if (fabs(v[6]) > fabs(dy)) { ny = v[3]; dy = v[6]; }
+    if (fabs(v[7]) > fabs(dy)) { ny = v[5]; dy = v[7]; }
+    if (fabs(v[4]) > fabs(dy)) { ny = v[1]; dy = v[4]; }
+    if (dx == 0.0 || dy == 0.0) return false;
+    *x = nx / dx;
+    *y = ny / dy;
+    return true;
+}
+
 // Poses of one root u: (x, y) from the null vector of M(w), Gauss-Newton polish of
 // (x, y, w), E = K F K, motion_from_essential on the f-calibrated bearings.
 MP_HD int sixpt_poses_for_root(const double (&M)[3][10][10], const double (&N)[3][9], double u,
@@ -731,8 +754,9 @@ MP_HD int sixpt_poses_for_root(const double (&M)[3][10][10], const double (&N)[3
     for (int r = 0; r < 10; ++r)
         for (int cc = 0; cc < 10; ++cc) A[r][cc] = M[0][r][cc] + w * (M[1][r][cc] + w * M[2][r][cc]);
     double v[10];
-    if (!null_vector10(A, v) || v[9] == 0.0) return 0;
-    double x = v[7] / v[9], y = v[8] / v[9];
+    if (!null_vector10(A, v)) return 0;
+    double x, y;
+    if (!sixpt_xy_from_monomials(v, &x, &y)) return 0;
     // Gauss-Newton polish of (x, y, w) on the ten equations
     for (int it = 0; it < 5; ++it) {
         double mv[10], dxv[10], dyv[10];
@@ -829,9 +853,9 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
     for (int q = 0; q < nout; ++q) {
         bool dup = false;
         for (int p = 0; p < n && !dup; ++p) {
-            bool same = fabs(out[p].focal0 - out[q].focal0) <= 1e-10 * fabs(out[q].focal0);
-            for (int e = 0; e < 9 && same; ++e) same = fabs(out[p].R[e] - out[q].R[e]) <= 1e-10;
-            for (int e = 0; e < 3 && same; ++e) same = fabs(out[p].t[e] - out[q].t[e]) <= 1e-10 * (1.0 + fabs(out[q].t[e]));
+            bool same = fabs(out[p].focal0 - out[q].focal0) <= 1e-8 * fabs(out[q].focal0);
+            for (int e = 0; e < 9 && same; ++e) same = fabs(out[p].R[e] - out[q].R[e]) <= 1e-6;
+            for (int e = 0; e < 3 && same; ++e) same = fabs(out[p].t[e] - out[q].t[e]) <= 1e-6 * (1.0 + fabs(out[q].t[e]));
             dup = same;
         }
         if (!dup) out[n++] = out[q];

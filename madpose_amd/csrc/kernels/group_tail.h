@@ -260,12 +260,16 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
         }
     }
     __syncthreads();
-    const double v9 = sh.z[g][9];
-    if (v9 == 0.0) { // (uniform)
-        no_pose();
-        return;
+    double x, y;
+    {
+        double zv[10];
+#pragma unroll
+        for (int c = 0; c < 10; ++c) zv[c] = sh.z[g][c];
+        if (!sixpt_xy_from_monomials(zv, &x, &y)) { // (uniform)
+            no_pose();
+            return;
+        }
     }
-    double x = sh.z[g][7] / v9, y = sh.z[g][8] / v9;
 
     // ---- Gauss-Newton polish of (x, y, w), rows summed over the group ----
     for (int it = 0; it < 5; ++it) {

@@ -477,9 +477,9 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
             for (int p = 0; p < q && !dup; ++p) {
                 if (!valid[(size_t)idx * kSlotStride + p]) continue;
                 const Model &o = slots[(size_t)idx * kSlotStride + p];
-                bool same = fabs(o.focal0 - m.focal0) <= 1e-10 * fabs(m.focal0);
-                for (int e = 0; e < 9 && same; ++e) same = fabs(o.R[e] - m.R[e]) <= 1e-10;
-                for (int e = 0; e < 3 && same; ++e) same = fabs(o.t[e] - m.t[e]) <= 1e-10 * (1.0 + fabs(m.t[e]));
+                bool same = fabs(o.focal0 - m.focal0) <= 1e-8 * fabs(m.focal0);
+                for (int e = 0; e < 9 && same; ++e) same = fabs(o.R[e] - m.R[e]) <= 1e-6;
+                for (int e = 0; e < 3 && same; ++e) same = fabs(o.t[e] - m.t[e]) <= 1e-6 * (1.0 + fabs(m.t[e]));
                 dup = same;
             }
             if (dup) continue;
