@@ -268,17 +268,19 @@ def pair_errors(results, pairs):
     return [max(utils.compute_pose_error(p["T_0to1"], m.R(), m.t())) for (m, _), p in zip(results, pairs)]
 
 
-def summarize_scannet(allv, errs, wl, steps, warmup, world, total):
+def summarize_scannet(allv, errs, wl, steps, warmup, world, total, auc_fn=None):
     """Whole-job record of the ScanNet-1500 stand-in: value = pairs per second of all
     ranks over the slowest rank's time (total work fixed: strong scaling); AUC@5/10/20
-    over the per-pair errors of every rank."""
+    over the per-pair errors of every rank (auc_fn: the engine's evaluator, the device
+    one for the product engine; default the host pose_auc)."""
     from madpose_amd import utils
 
+    auc_fn = auc_fn or utils.pose_auc
     t_max = float(allv[:, 0].max())
     done = float(allv[:, 1].sum())
     e = np.asarray(errs, dtype=np.float64)
     e = e[np.isfinite(e)]
-    auc = utils.pose_auc(e, (5, 10, 20)) if len(e) else [None] * 3
+    auc = auc_fn(e, (5, 10, 20)) if len(e) else [None] * 3
     return {
         "metric": "image-pairs/sec on 1xMI355X (ScanNet-1500 stand-in) + pose AUC@5/10/20",
         "value": done / t_max,
@@ -351,17 +353,18 @@ RECORD_FIELDS = (["seed"] + [f"R{i}{j}" for i in range(3) for j in range(3)] + [
                  "number_lo_iterations", "err_R_deg", "err_t_deg"])
 
 
-def result_record(seed, model, stats, pair):
+def result_record(seed, model, stats, pair, err=None):
     """One fixed-size result record per pair (pose + stats), the unit
     the ranks exchange at the end: seed, R, t, scale, offsets, focal(s), iteration and
     inlier counts, score, LO count, and the pose error against the synthetic ground truth
-    (madpose/utils.py:59-78 compute_pose_error)."""
+    (madpose/utils.py:59-78 compute_pose_error; err: (err_t, err_R) computed already, e.g.
+    by the device evaluator)."""
     from madpose_amd import utils
 
     R, t = np.asarray(model.R(), dtype=np.float64), np.asarray(model.t(), dtype=np.float64)
     f0 = getattr(model, "focal0", getattr(model, "focal", np.nan))
     f1 = getattr(model, "focal1", getattr(model, "focal", np.nan))
-    et, eR = utils.compute_pose_error(pair["T_0to1"], R, t)
+    et, eR = utils.compute_pose_error(pair["T_0to1"], R, t) if err is None else err
     rec = ([float(seed)] + list(R.reshape(9)) + list(t.reshape(3)) +
            [getattr(model, "scale", np.nan), getattr(model, "offset0", np.nan), getattr(model, "offset1", np.nan), f0,
             f1, stats.num_iterations_total, stats.best_num_inliers, stats.best_model_score,
@@ -388,6 +391,18 @@ def records_summary(recs):
     return {"records": int(len(recs)), "record_doubles": len(RECORD_FIELDS),
             "pairs_disjoint": bool(len(np.unique(seeds)) == len(seeds)),
             "median_pose_err_deg": float(np.median(err)) if len(err) else None}
+
+
+def records_of(eng, seeds, res, pairs):
+    """Result records of a rank's pairs, their pose errors from the engine's evaluator
+    in one call (the device evaluator mp_pose_eval for the product engine)."""
+    if not res:
+        return []
+    T = np.stack([p["T_0to1"] for p in pairs])
+    R = np.stack([np.asarray(m.R(), dtype=np.float64) for m, _ in res])
+    t = np.stack([np.asarray(m.t(), dtype=np.float64).reshape(3) for m, _ in res])
+    et, eR = eng.pose_errors(T, R, t)
+    return [result_record(s, m, st, p, (et[k], eR[k])) for k, (s, (m, st), p) in enumerate(zip(seeds, res, pairs))]
 
 
 def shard_scannet(total, world, rank):
@@ -422,7 +437,7 @@ def run_scannet(a, wl, world, rank, dev, barrier, eng):
         res = eng.estimate_batch(wl["variant"], pairs, o, c, device=dev, num_streams=a.streams)
     barrier()
     elapsed = time.perf_counter() - t0
-    recs = [result_record(s, m, st, p) for s, (m, st), p in zip(seeds, res, pairs)]
+    recs = records_of(eng, seeds, res, pairs)
     local = [elapsed, float(len(pairs) * a.steps), float(sum(st.num_hypotheses for _, st in res) * a.steps),
              float(sum(st.num_iterations_total for _, st in res) * a.steps)]
     # point-only baseline (untimed): the examples compare against PoseLib's point-based
@@ -436,21 +451,19 @@ def run_scannet(a, wl, world, rank, dev, barrier, eng):
         cp = EstimatorConfig(1, 1, 1)
         cp.min_depth_constraint, cp.use_shift = c.min_depth_constraint, c.use_shift
         pres = eng.estimate_batch(wl["variant"], pairs, o, cp, device=dev, num_streams=a.streams)
-        prec = [result_record(s, m, st, p) for s, (m, st), p in zip(seeds, pres, pairs)]
+        prec = records_of(eng, seeds, pres, pairs)
     allv = gather_counters(local, world)
     per = (total + world - 1) // world + 1
     allr = gather_records(recs, per, world)
     allp = gather_records(prec, per, world) if a.point_only else None
     if rank == 0:
         errs = np.maximum(allr[:, RECORD_FIELDS.index("err_R_deg")], allr[:, RECORD_FIELDS.index("err_t_deg")])
-        out = summarize_scannet(allv, errs, wl, a.steps, a.warmup, world, total)
+        out = summarize_scannet(allv, errs, wl, a.steps, a.warmup, world, total, eng.pose_auc)
         out["results"] = records_summary(allr)
         if allp is not None:
-            from madpose_amd import utils
-
             pe = np.maximum(allp[:, RECORD_FIELDS.index("err_R_deg")], allp[:, RECORD_FIELDS.index("err_t_deg")])
             pe = pe[np.isfinite(pe)]
-            auc = utils.pose_auc(pe, (5, 10, 20)) if len(pe) else [None] * 3
+            auc = eng.pose_auc(pe, (5, 10, 20)) if len(pe) else [None] * 3
             out["point_only_baseline"] = {
                 "pose_auc": {"5": auc[0], "10": auc[1], "20": auc[2], "pairs": int(len(pe))},
                 "config": "EstimatorConfig(solver=EPI_ONLY, score=EPI_ONLY, LO=EPI_ONLY): the reference's own "
@@ -474,6 +487,12 @@ class _Engine:
 
     def estimate_batch(self, *args, **kw):
         return self.m.estimate_batch(*args, **kw)
+
+    def pose_errors(self, T, R, t):
+        return self.m.pose_eval_batch(T, R, t, thresholds=())[:2]
+
+    def pose_auc(self, errors, thresholds):
+        return self.m.pose_auc_batch(errors, thresholds)
 
     def profile_reset(self):
         self.m.profile_reset()
@@ -601,7 +620,7 @@ def main(argv=None):
     eng.profile_enable(False)
     prof = eng.profile_read()
 
-    recs = [result_record(seeds[a.warmup + k], m, st, pairs[a.warmup + k]) for k, (m, st) in enumerate(res)]
+    recs = records_of(eng, seeds[a.warmup:a.warmup + len(res)], res, pairs[a.warmup:a.warmup + len(res)])
     local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
              prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
              prof["sweep_wall_ms"], prof["iterations"], prof["sample_wall_ms"], prof["wait_wall_ms"],

@@ -184,6 +184,20 @@ int mp_debug_lm_refine_host(int variant, int64_t n, const double *x0, const doub
  * the device with the same code the two-focal 7-point tail runs. */
 int mp_bougnoux_focals(int64_t k, const double *F, double *out, int device);
 
+/* compute_pose_error (madpose/utils.py:59-78) of k estimated poses against their
+ * ground truth on the device, and the pose AUC of the evaluation the reference's
+ * README reports (ScanNet-1500 AUC@5/10/20, README.md:18-181):
+ * R: k x 9 row-major, t: k x 3, T_0to1: k x 16 (row-major 4x4); t_thres < 0 means
+ * none (else err_t = 0 where |t_gt| < t_thres).  err_t, err_R: k degrees each.  When
+ * nthr > 0, aucs[b] = area under the recall curve of max(err_R, err_t) up to
+ * thresholds[b], divided by it (trapezoid rule, NaN errors sorted last; the
+ * SuperGlue-style pose_auc of madpose_amd/utils.py); k = 0 gives NaN. */
+int mp_pose_eval(int64_t k, const double *R, const double *t, const double *T_0to1, double t_thres, double *err_t,
+                 double *err_R, int32_t nthr, const double *thresholds, double *aucs, int device);
+/* The same pose AUC over k given errors (degrees; e.g. max(err_R, err_t) gathered
+ * from many ranks): aucs[b] for thresholds[b], b < nthr. */
+int mp_pose_auc(int64_t k, const double *errors, int32_t nthr, const double *thresholds, double *aucs, int device);
+
 /* Point minimal solver (PoseLib relpose_5pt, src/hybrid_pose_estimator.cpp:134) on unit bearings
  * (5 points, point-major 3 doubles each).  Returns count or -code. */
 int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_out, int device);

@@ -26,6 +26,8 @@ from .api import (  # noqa: F401
     bougnoux_focals_batch,
     lm_refine_batch,
     get_depths_batch,
+    pose_auc_batch,
+    pose_eval_batch,
     profile_enable,
     profile_read,
     profile_reset,

@@ -130,6 +130,9 @@ EXPORTS = {
                                                ctypes.c_int32, c_int32_p, c_int64_p, c_int32_p,
                                                ctypes.POINTER(mp_model), c_int32_p]),
     "mp_bougnoux_focals": (ctypes.c_int, [ctypes.c_int64, c_double_p, c_double_p, ctypes.c_int]),
+    "mp_pose_eval": (ctypes.c_int, [ctypes.c_int64, c_double_p, c_double_p, c_double_p, ctypes.c_double, c_double_p,
+                                    c_double_p, ctypes.c_int32, c_double_p, c_double_p, ctypes.c_int]),
+    "mp_pose_auc": (ctypes.c_int, [ctypes.c_int64, c_double_p, ctypes.c_int32, c_double_p, c_double_p, ctypes.c_int]),
     "mp_estimate_scale_and_pose": (ctypes.c_int, [c_double_p, c_double_p, c_double_p, ctypes.c_int64,
                                                   ctypes.POINTER(mp_model), ctypes.c_int]),
     "mp_solve_scale_and_shift": (ctypes.c_int, [ctypes.c_int, c_double_p, c_double_p, c_double_p, c_double_p,

@@ -470,6 +470,41 @@ def bougnoux_focals_batch(F, device=None):
     return out
 
 
+def pose_eval_batch(T_0to1, R, t, thresholds=(5, 10, 20), t_thres=None, device=None):
+    """compute_pose_error (madpose/utils.py:59-78) of k estimated poses and the pose
+    AUC of max(err_R, err_t) at each threshold (degrees), in two device launches
+    (SURVEY.md §8(f)4).  T_0to1: k x 4 x 4 ground truths; R: k x 3 x 3; t: k x 3.
+    Returns (err_t, err_R, aucs): the per-pair errors as madpose.utils computes them
+    and the AUCs of madpose_amd.utils.pose_auc (NaN errors count as misses)."""
+    T = np.ascontiguousarray(np.asarray(T_0to1, dtype=np.float64).reshape(-1, 16))
+    Rm = np.ascontiguousarray(np.asarray(R, dtype=np.float64).reshape(-1, 9))
+    tv = np.ascontiguousarray(np.asarray(t, dtype=np.float64).reshape(-1, 3))
+    if not (len(T) == len(Rm) == len(tv)):
+        raise ValueError("T_0to1, R and t must hold the same number of poses")
+    thr = np.ascontiguousarray(np.asarray(thresholds, dtype=np.float64).reshape(-1))
+    if np.any(~(thr > 0)):
+        raise ValueError("AUC thresholds must be positive")
+    k = len(T)
+    et, eR, aucs = np.zeros(max(k, 1)), np.zeros(max(k, 1)), np.zeros(max(len(thr), 1))
+    L.check(L.lib().mp_pose_eval(k, _dp(Rm), _dp(tv), _dp(T), -1.0 if t_thres is None else float(t_thres), _dp(et),
+                                 _dp(eR), len(thr), _dp(thr), _dp(aucs),
+                                 _DEFAULT_DEVICE if device is None else int(device)))
+    return et[:k].copy(), eR[:k].copy(), [float(a) for a in aucs[:len(thr)]]
+
+
+def pose_auc_batch(errors, thresholds=(5, 10, 20), device=None):
+    """Pose AUC of given per-pair errors (degrees) at each threshold on the device: the
+    evaluator of pose_eval_batch for errors gathered elsewhere (e.g. from all ranks)."""
+    e = np.ascontiguousarray(np.asarray(errors, dtype=np.float64).reshape(-1))
+    thr = np.ascontiguousarray(np.asarray(thresholds, dtype=np.float64).reshape(-1))
+    if np.any(~(thr > 0)):
+        raise ValueError("AUC thresholds must be positive")
+    aucs = np.zeros(max(len(thr), 1))
+    L.check(L.lib().mp_pose_auc(len(e), _dp(e if len(e) else np.zeros(1)), len(thr), _dp(thr), _dp(aucs),
+                                _DEFAULT_DEVICE if device is None else int(device)))
+    return [float(a) for a in aucs[:len(thr)]]
+
+
 def get_depths_batch(images, depth_maps, mkpts, device=None):
     """madpose.utils.get_depths (madpose/utils.py:4-22) for many pairs in one device
     launch.  images: the images (only their shapes are used) or (h, w) tuples;

@@ -202,6 +202,30 @@ int mp_bougnoux_focals(int64_t k, const double *F, double *out, int device) {
     });
 }
 
+int mp_pose_eval(int64_t k, const double *R, const double *t, const double *T_0to1, double t_thres, double *err_t,
+                 double *err_R, int32_t nthr, const double *thresholds, double *aucs, int device) {
+    return guarded([&]() {
+        if (k < 0 || nthr < 0 || (k > 0 && (!R || !t || !T_0to1 || !err_t || !err_R)) ||
+            (nthr > 0 && (!thresholds || !aucs)))
+            throw std::invalid_argument("bad pose_eval arguments");
+        for (int b = 0; b < nthr; ++b)
+            if (!(thresholds[b] > 0.0)) throw std::invalid_argument("AUC thresholds must be positive");
+        mp::pose_eval_batch(k, R, t, T_0to1, t_thres, err_t, err_R, nthr, thresholds, aucs, device);
+        return MP_OK;
+    });
+}
+
+int mp_pose_auc(int64_t k, const double *errors, int32_t nthr, const double *thresholds, double *aucs, int device) {
+    return guarded([&]() {
+        if (k < 0 || nthr < 0 || (k > 0 && !errors) || (nthr > 0 && (!thresholds || !aucs)))
+            throw std::invalid_argument("bad pose_auc arguments");
+        for (int b = 0; b < nthr; ++b)
+            if (!(thresholds[b] > 0.0)) throw std::invalid_argument("AUC thresholds must be positive");
+        mp::pose_auc_batch(k, errors, nthr, thresholds, aucs, device);
+        return MP_OK;
+    });
+}
+
 int mp_estimate_scale_and_pose(const double *X, const double *Y, const double *W, int64_t n, mp_model *out,
                                int device) {
     return guarded([&]() {

@@ -1661,6 +1661,54 @@ void bougnoux_batch(int64_t k, const double *F, double *out, int device) {
     MP_HIP(hipFree(d_out));
 }
 
+void pose_eval_batch(int64_t k, const double *R, const double *t, const double *T, double t_thres, double *err_t,
+                     double *err_R, int nthr, const double *thr, double *aucs, int device) {
+    if (k <= 0) {
+        for (int b = 0; b < nthr; ++b) aucs[b] = NAN;
+        return;
+    }
+    CtxLease lease(device);
+    hipStream_t s = lease.c->stream;
+    // one block: R (9k) t (3k) T (16k) | err_t err_R max(err_t, err_R) sorted (4k) | thr, aucs (2 nthr)
+    const size_t in = 28 * (size_t)k, tot = in + 4 * (size_t)k + 2 * (size_t)std::max(nthr, 0);
+    std::vector<double> host(in);
+    std::memcpy(host.data(), R, sizeof(double) * 9 * k);
+    std::memcpy(host.data() + 9 * k, t, sizeof(double) * 3 * k);
+    std::memcpy(host.data() + 12 * k, T, sizeof(double) * 16 * k);
+    double *d;
+    MP_HIP(hipMalloc(&d, sizeof(double) * tot));
+    double *d_et = d + in, *d_eR = d_et + k, *d_max = d_eR + k, *d_sorted = d_max + k, *d_thr = d_sorted + k,
+           *d_auc = d_thr + nthr;
+    MP_HIP(hipMemcpyAsync(d, host.data(), sizeof(double) * in, hipMemcpyHostToDevice, s));
+    if (nthr > 0) MP_HIP(hipMemcpyAsync(d_thr, thr, sizeof(double) * nthr, hipMemcpyHostToDevice, s));
+    MP_HIP(launch_pose_errors(s, k, d, d + 9 * k, d + 12 * k, t_thres, d_et, d_eR, nthr > 0 ? d_max : nullptr));
+    MP_HIP(launch_pose_auc(s, k, d_max, d_sorted, nthr, d_thr, d_auc));
+    MP_HIP(hipMemcpyAsync(err_t, d_et, sizeof(double) * k, hipMemcpyDeviceToHost, s));
+    MP_HIP(hipMemcpyAsync(err_R, d_eR, sizeof(double) * k, hipMemcpyDeviceToHost, s));
+    if (nthr > 0) MP_HIP(hipMemcpyAsync(aucs, d_auc, sizeof(double) * nthr, hipMemcpyDeviceToHost, s));
+    MP_HIP(hipStreamSynchronize(s));
+    MP_HIP(hipFree(d));
+}
+
+void pose_auc_batch(int64_t k, const double *errors, int nthr, const double *thr, double *aucs, int device) {
+    if (nthr <= 0) return;
+    if (k <= 0) {
+        for (int b = 0; b < nthr; ++b) aucs[b] = NAN;
+        return;
+    }
+    CtxLease lease(device);
+    hipStream_t s = lease.c->stream;
+    double *d; // errors (k) | sorted (k) | thresholds, aucs (2 nthr)
+    MP_HIP(hipMalloc(&d, sizeof(double) * (2 * (size_t)k + 2 * (size_t)nthr)));
+    double *d_sorted = d + k, *d_thr = d_sorted + k, *d_auc = d_thr + nthr;
+    MP_HIP(hipMemcpyAsync(d, errors, sizeof(double) * k, hipMemcpyHostToDevice, s));
+    MP_HIP(hipMemcpyAsync(d_thr, thr, sizeof(double) * nthr, hipMemcpyHostToDevice, s));
+    MP_HIP(launch_pose_auc(s, k, d, d_sorted, nthr, d_thr, d_auc));
+    MP_HIP(hipMemcpyAsync(aucs, d_auc, sizeof(double) * nthr, hipMemcpyDeviceToHost, s));
+    MP_HIP(hipStreamSynchronize(s));
+    MP_HIP(hipFree(d));
+}
+
 void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *dims, const int64_t *pt_off,
                       const double *pts, void *out, int device) {
     if (dtype != 0 && dtype != 1) throw std::invalid_argument("dtype must be 0 (float32) or 1 (float64)");

@@ -93,6 +93,12 @@ void scale_and_pose_direct(const double *X, const double *Y, const double *W, in
 // (depth-map h, w, image h, w); host buffers in and out
 // squared Bougnoux focals of k fundamental matrices (device kernel, mp_bougnoux_focals)
 void bougnoux_batch(int64_t k, const double *F, double *out, int device);
+// compute_pose_error of k pairs and the pose AUC of max(err_R, err_t) at nthr
+// thresholds on the device (mp_pose_eval); host buffers in and out
+void pose_eval_batch(int64_t k, const double *R, const double *t, const double *T, double t_thres, double *err_t,
+                     double *err_R, int nthr, const double *thr, double *aucs, int device);
+// the pose AUC of k given errors at nthr thresholds (mp_pose_auc)
+void pose_auc_batch(int64_t k, const double *errors, int nthr, const double *thr, double *aucs, int device);
 void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *dims, const int64_t *pt_off,
                       const double *pts, void *out, int device);
 

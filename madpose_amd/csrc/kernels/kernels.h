@@ -65,6 +65,16 @@ hipError_t launch_lm_batch(hipStream_t s, const PairData &D, const PairConst &C,
 // squared Bougnoux focals of k fundamental matrices (9 doubles each) into out (2 each)
 hipError_t launch_bougnoux(hipStream_t s, const double *F, int64_t k, double *out);
 
+// compute_pose_error of k pairs (R k x 9, t k x 3, T k x 16 row-major T_0to1; t_thres
+// < 0: none) into err_t, err_R (degrees) and, when err_max is given, max(err_t, err_R)
+hipError_t launch_pose_errors(hipStream_t s, int64_t k, const double *R, const double *t, const double *T,
+                              double t_thres, double *err_t, double *err_R, double *err_max);
+
+// pose AUC of k errors at nthr thresholds: rank sort into sorted (k doubles of
+// scratch), then one workgroup per threshold
+hipError_t launch_pose_auc(hipStream_t s, int64_t k, const double *e, double *sorted, int nthr, const double *thr,
+                           double *aucs);
+
 // estimate_scale_and_pose over n points (in = X(3n) Y(3n) W(n)), one thread
 hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out);
 

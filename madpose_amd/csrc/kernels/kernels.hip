@@ -1053,6 +1053,119 @@ hipError_t launch_bougnoux(hipStream_t s, const double *F, int64_t k, double *ou
     return hipGetLastError();
 }
 
+// compute_pose_error (madpose/utils.py:59-78) of k pairs, one lane each: the
+// translation angle folded to [0, 90] (E fixes t up to sign) and the rotation angle
+// between R_est and R_gt, in degrees, with numpy's formulas (norm product as the
+// divisor, cosine clipped to [-1, 1], err_t = 0 when |t_gt| < t_thres if t_thres >= 0).
+// R: k x 9 row-major, t: k x 3, T: k x 16 (row-major 4x4 T_0to1).
+__global__ void pose_error_kernel(int64_t k, const double *R, const double *t, const double *T, double t_thres,
+                                  double *err_t, double *err_R, double *err_max) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const double *Ri = R + 9 * i, *ti = t + 3 * i, *Ti = T + 16 * i;
+    const double kDeg = 180.0 / M_PI;
+    const double tg0 = Ti[3], tg1 = Ti[7], tg2 = Ti[11];
+    const double ng = sqrt(tg0 * tg0 + tg1 * tg1 + tg2 * tg2);
+    const double n = sqrt(ti[0] * ti[0] + ti[1] * ti[1] + ti[2] * ti[2]) * ng;
+    const double ct = (ti[0] * tg0 + ti[1] * tg1 + ti[2] * tg2) / n;
+    // np.clip and np.minimum propagate NaN (a zero translation); fmin / fmax do not
+    double et = isnan(ct) ? NAN : acos(fmin(fmax(ct, -1.0), 1.0)) * kDeg;
+    if (!isnan(et)) et = fmin(et, 180.0 - et);
+    if (t_thres >= 0.0 && ng < t_thres) et = 0.0;
+    // trace(R_est^T R_gt) = sum over all entries of R_est .* R_gt
+    double tr = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) tr += Ri[c] * Ti[c] + Ri[3 + c] * Ti[4 + c] + Ri[6 + c] * Ti[8 + c];
+    double cr = (tr - 1.0) / 2.0;
+    const bool nan_r = isnan(cr);
+    cr = fmin(fmax(cr, -1.0), 1.0);
+    const double er = nan_r ? NAN : fabs(acos(cr)) * kDeg;
+    err_t[i] = et;
+    err_R[i] = er;
+    if (err_max) err_max[i] = isnan(et) || isnan(er) ? NAN : fmax(et, er); // np.maximum propagates NaN
+}
+
+// Total order of the pose-AUC sort: ascending error, NaN last (np.sort), equal keys
+// by index, so the ranks below are a permutation.
+__device__ inline bool auc_before(double a, int64_t ia, double b, int64_t ib) {
+    const bool an = isnan(a), bn = isnan(b);
+    if (an != bn) return bn;
+    if (an) return ia < ib;
+    return a < b || (a == b && ia < ib);
+}
+
+constexpr int kAucBlock = 256, kAucChunk = 2048;
+
+// Rank sort of the pose errors: lane i counts the elements ordered before e[i]
+// (the array streamed through LDS in chunks) and stores e[i] at that rank.
+__global__ __launch_bounds__(kAucBlock) void auc_rank_kernel(int64_t k, const double *e, double *sorted) {
+    __shared__ double chunk[kAucChunk];
+    const int64_t i = blockIdx.x * (int64_t)kAucBlock + threadIdx.x;
+    const double ei = i < k ? e[i] : 0.0;
+    int64_t rank = 0;
+    for (int64_t base = 0; base < k; base += kAucChunk) {
+        const int len = (int)(k - base < kAucChunk ? k - base : kAucChunk);
+        __syncthreads();
+        for (int j = threadIdx.x; j < len; j += kAucBlock) chunk[j] = e[base + j];
+        __syncthreads();
+        if (i < k)
+            for (int j = 0; j < len; ++j) rank += auc_before(chunk[j], base + j, ei, i) ? 1 : 0;
+    }
+    if (i < k) sorted[rank] = ei;
+}
+
+// AUC of the cumulative error curve up to thr[b] (one workgroup per threshold): the
+// trapezoid rule over (0, 0), (s_j, j / k) for the m sorted errors s_j < thr, closed
+// at (thr, m / k), divided by thr -- the SuperGlue-style pose_auc of madpose_amd/utils.py.
+// Lane-strided partial sums in ascending j, then a fixed-order tree: deterministic.
+__global__ __launch_bounds__(kAucBlock) void auc_sum_kernel(int64_t k, const double *s, const double *thr,
+                                                            double *aucs) {
+    __shared__ double part[kAucBlock];
+    __shared__ int64_t cnt[kAucBlock];
+    const double t = thr[blockIdx.x];
+    const double inv = 1.0 / (double)k;
+    double acc = 0.0;
+    int64_t m = 0;
+    for (int64_t j = threadIdx.x; j < k; j += kAucBlock) {
+        const double sj = s[j];
+        if (!(sj < t)) continue; // sorted: the tail (and NaN) is past the threshold
+        ++m;
+        const double prev = j == 0 ? 0.0 : s[j - 1];
+        const double r0 = j == 0 ? 0.0 : (double)j * inv, r1 = (double)(j + 1) * inv;
+        acc += (sj - prev) * (r0 + r1) / 2.0;
+    }
+    part[threadIdx.x] = acc;
+    cnt[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = kAucBlock / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            part[threadIdx.x] += part[threadIdx.x + w];
+            cnt[threadIdx.x] += cnt[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int64_t mm = cnt[0];
+        const double last = mm == 0 ? 0.0 : s[mm - 1], rl = mm == 0 ? 0.0 : (double)mm * inv;
+        aucs[blockIdx.x] = (part[0] + (t - last) * rl) / t;
+    }
+}
+
+hipError_t launch_pose_errors(hipStream_t s, int64_t k, const double *R, const double *t, const double *T,
+                              double t_thres, double *err_t, double *err_R, double *err_max) {
+    if (k <= 0) return hipSuccess;
+    pose_error_kernel<<<(int)((k + 255) / 256), 256, 0, s>>>(k, R, t, T, t_thres, err_t, err_R, err_max);
+    return hipGetLastError();
+}
+
+hipError_t launch_pose_auc(hipStream_t s, int64_t k, const double *e, double *sorted, int nthr, const double *thr,
+                           double *aucs) {
+    if (k <= 0 || nthr <= 0) return hipSuccess;
+    auc_rank_kernel<<<(int)((k + kAucBlock - 1) / kAucBlock), kAucBlock, 0, s>>>(k, e, sorted);
+    auc_sum_kernel<<<nthr, kAucBlock, 0, s>>>(k, sorted, thr, aucs);
+    return hipGetLastError();
+}
+
 hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out) {
     scale_and_pose_kernel<<<1, 64, 0, s>>>(in, n, out);
     return hipGetLastError();

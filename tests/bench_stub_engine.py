@@ -26,6 +26,17 @@ class Engine:
     def estimate_batch(self, variant, pairs, o, c, device=None, num_streams=1):
         return [self.estimate(variant, (p["x0"],), o, c, device) for p in pairs]
 
+    def pose_errors(self, T, R, t):
+        from madpose_amd import utils
+
+        e = np.array([utils.compute_pose_error(T[k], R[k], t[k]) for k in range(len(T))]).reshape(-1, 2)
+        return e[:, 0], e[:, 1]
+
+    def pose_auc(self, errors, thresholds):
+        from madpose_amd import utils
+
+        return utils.pose_auc(errors, thresholds)
+
     def profile_reset(self):
         pass
 
