@@ -4,10 +4,11 @@ reference's compute_pose_error (madpose/utils.py:59-78) pinned by its recorded o
 sets with ties, exact-threshold values, NaN errors, several workgroups' worth of pairs
 and the empty set.
 
-Tolerances: errors 1e-9 degrees absolute (acos is ill-conditioned near 0 and 180
-degrees, so a one-ulp difference in the trace or dot product can move a tiny angle by
-~1e-10 degrees); AUCs 1e-12 relative (the same trapezoid terms, summed in another
-order)."""
+Tolerances: errors 1e-9 degrees absolute, except at angles within 1e-3 degrees of 0
+(after the translation fold, also of 180): there acos is ill-conditioned, and a
+one-ulp difference in the trace or dot product (summation order, FMA contraction)
+moves an exact 0 to deg(sqrt(2 eps)) ~ 1.2e-6 degrees, so the bound is 2e-6 there;
+AUCs 1e-12 relative (the same trapezoid terms, summed in another order)."""
 import os
 
 import numpy as np
@@ -26,6 +27,11 @@ def require_gpu():
         pytest.fail("no HIP device visible: the GPU tests must run on an MI355X")
 
 
+def _close_angles(dev, ref):
+    tol = np.where(np.abs(ref) < 1e-3, 2e-6, 1e-9)
+    return bool(np.all(np.abs(dev - ref) <= tol))
+
+
 def _rand_rot(rng):
     q = rng.normal(size=4)
     q /= np.linalg.norm(q)
@@ -38,8 +44,8 @@ def _rand_rot(rng):
 def test_pose_errors_match_reference_golden():
     g = np.load(os.path.join(GOLDEN, "utils.npz"))
     et, eR, _ = madpose.pose_eval_batch(g["pe_T"], g["pe_R"], g["pe_t"], thresholds=())
-    assert np.allclose(et, g["pe_err"][:, 0], rtol=0, atol=1e-9)
-    assert np.allclose(eR, g["pe_err"][:, 1], rtol=0, atol=1e-9)
+    assert _close_angles(et, g["pe_err"][:, 0])
+    assert _close_angles(eR, g["pe_err"][:, 1])
 
 
 def test_pose_errors_match_numpy_with_t_thres():
@@ -58,8 +64,8 @@ def test_pose_errors_match_numpy_with_t_thres():
     for t_thres in (None, 0.05):
         et, eR, _ = madpose.pose_eval_batch(T, R, t, thresholds=(), t_thres=t_thres)
         ref = np.array([utils.compute_pose_error(T[i], R[i], t[i], t_thres) for i in range(k)])
-        assert np.allclose(et, ref[:, 0], rtol=0, atol=1e-9)
-        assert np.allclose(eR, ref[:, 1], rtol=0, atol=1e-9)
+        assert _close_angles(et, ref[:, 0])
+        assert _close_angles(eR, ref[:, 1])
 
 
 @pytest.mark.parametrize("k", [1, 37, 1500, 5000])
