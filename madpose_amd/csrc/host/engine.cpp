@@ -319,7 +319,18 @@ class LoWorkers {
     std::exception_ptr err_;
 };
 
-constexpr int kLoLanes = 4; // concurrent LO steps (and sweep slots)
+constexpr int kLoLanes = 12; // most concurrent LO steps (and sweep slots) per context
+
+// concurrent LO steps of one estimator (MADPOSE_LO_LANES, 1..kLoLanes): the default
+// is 4 lanes; see DESIGN.md §8 for the measurements behind it
+inline int lo_lanes_setting() {
+    static const int v = [] {
+        const char *e = std::getenv("MADPOSE_LO_LANES");
+        const int n = e ? std::atoi(e) : 4;
+        return std::max(1, std::min(kLoLanes, n));
+    }();
+    return v;
+}
 
 // ---------------------------------------------------------------------------
 // Device context: stream + cached buffers (one per device and concurrent caller)
@@ -1136,8 +1147,9 @@ void Run::run(Model *best, Stats *S) {
         device_lm_ = d && d[0] == '1';
     }
     if (lo_parallel_) {
-        if (!X_.lo_workers) X_.lo_workers.reset(new LoWorkers(kLoLanes));
-        for (int l = 1; l < kLoLanes; ++l) {
+        const int nl = lo_lanes_setting();
+        if (!X_.lo_workers || X_.lo_workers->lanes() != nl) X_.lo_workers.reset(new LoWorkers(nl));
+        for (int l = 1; l < nl; ++l) {
             X_.sweep_slot[l].ensure(X_.cap_n, nullptr);
             lanes_[l].slot = &X_.sweep_slot[l];
         }

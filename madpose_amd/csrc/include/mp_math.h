@@ -2,6 +2,7 @@
 // Everything here is fixed-size and fully unrollable so hipcc keeps it in VGPRs
 // (no dynamically indexed private arrays -> no scratch traffic).
 #pragma once
+#include <cfloat>
 #include <cmath>
 
 #include "mp_types.h"
@@ -500,6 +501,105 @@ MP_HD void smallest_right_sv4(const double (&A0)[4][4], double *v) {
     for (int j = 0; j < 4; ++j) w[j] = (k == j) ? 1.0 : 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = w[0] * V[i][0] + w[1] * V[i][1] + w[2] * V[i][2] + w[3] * V[i][3];
+}
+
+// The same vector for the DLT triangulation of the depth fits (the chosen pose: A of
+// rank 3 up to noise) without the Jacobi sweeps: Householder QR of A (A^T A = R^T R,
+// backward stable), then inverse iteration on R^T R by triangular solves, starting
+// from R^-1 e4 -- for a rank-3 A that start is already the null vector (R[3][3] ~ 0),
+// and each step multiplies the error by (s4 / s3)^2.  The iteration stops once two
+// normalised iterates agree to 1e-14 (one to three steps for the depth fits); after
+// NIT steps without that it falls back to the sweeps (s3 ~ s4).  About 150-250 FP64
+// operations with 4 square roots and 5 reciprocals, against several thousand for
+// the sweeps; the accuracy is the SVD's (error ~ eps s1 / s3; agreement with the
+// sweeps to ~1e-12 in a host test over noisy two-view points).  Only the direction
+// matters to the callers (they dehomogenise).  A zero diagonal of R is replaced by
+// eps |R| (inverse iteration on a singular matrix; the DLT matrices have A[0][0] =
+// -f != 0, so R != 0).
+template <int NIT = 16> MP_HD void dlt_null4(const double (&A)[4][4], double *v) {
+    double R[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[i][j] = A[i][j];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double nn = 0.0;
+#pragma unroll
+        for (int i = k; i < 4; ++i) nn += R[i][k] * R[i][k];
+        const double nrm = sqrt(nn);
+        const double alpha = R[k][k] >= 0.0 ? -nrm : nrm;
+        double h[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = i < k ? 0.0 : R[i][k];
+        h[k] -= alpha;
+        const double hh = nn - 2.0 * alpha * R[k][k] + alpha * alpha; // |h|^2
+        const double f2 = hh > 0.0 ? 2.0 / hh : 0.0;
+#pragma unroll
+        for (int j = k; j < 4; ++j) {
+            double sdot = 0.0;
+#pragma unroll
+            for (int i = k; i < 4; ++i) sdot += h[i] * R[i][j];
+            const double f = sdot * f2;
+#pragma unroll
+            for (int i = k; i < 4; ++i) R[i][j] -= f * h[i];
+        }
+    }
+    double big = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j < 4; ++j) big = fmax(big, fabs(R[i][j]));
+    const double floor_ = big * 2.220446049250313e-16;
+    double d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double r = R[i][i];
+        d[i] = 1.0 / (fabs(r) > floor_ ? r : (r < 0.0 ? -floor_ : floor_));
+    }
+    // x = R^-1 e4
+    double x[4];
+    x[3] = d[3];
+    x[2] = -(R[2][3] * x[3]) * d[2];
+    x[1] = -(R[1][2] * x[2] + R[1][3] * x[3]) * d[1];
+    x[0] = -(R[0][1] * x[1] + R[0][2] * x[2] + R[0][3] * x[3]) * d[0];
+    bool conv = false;
+    for (int it = 0; it < NIT && !conv; ++it) {
+        double mx = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmax(mx, fabs(x[i]));
+        const double sc = 1.0 / mx;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] *= sc;
+        // R^T y = x (forward), then R z = y (back)
+        double y[4], z[4];
+        y[0] = x[0] * d[0];
+        y[1] = (x[1] - R[0][1] * y[0]) * d[1];
+        y[2] = (x[2] - R[0][2] * y[0] - R[1][2] * y[1]) * d[2];
+        y[3] = (x[3] - R[0][3] * y[0] - R[1][3] * y[1] - R[2][3] * y[2]) * d[3];
+        z[3] = y[3] * d[3];
+        z[2] = (y[2] - R[2][3] * z[3]) * d[2];
+        z[1] = (y[1] - R[1][2] * z[2] - R[1][3] * z[3]) * d[1];
+        z[0] = (y[0] - R[0][1] * z[1] - R[0][2] * z[2] - R[0][3] * z[3]) * d[0];
+        double mz = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mz = fmax(mz, fabs(z[i]));
+        const double rz = 1.0 / mz;
+        double diff = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            diff = fmax(diff, fabs(z[i] * rz - x[i]));
+            x[i] = z[i];
+        }
+        conv = diff < 1e-14;
+    }
+    if (!conv) {
+        smallest_right_sv4(A, v);
+        return;
+    }
+    const double n = 1.0 / sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = x[i] * n;
 }
 
 } // namespace mp

@@ -473,7 +473,7 @@ MP_HD void triangulate(const double *R, const double *t, double fa, double fb, c
         A[3][j] = p1[1] * P1[2][j] - P1[1][j];
     }
     double v[4];
-    smallest_right_sv4(A, v);
+    dlt_null4(A, v);
     X[0] = v[0] / v[3];
     X[1] = v[1] / v[3];
     X[2] = v[2] / v[3];

@@ -318,6 +318,9 @@ MP_HD bool recover_pose_good(const RecoverCands &rc, int k, const double *p0, co
         A[2][j] = p1[0] * P1[2][j] - P1[0][j];
         A[3][j] = p1[1] * P1[2][j] - P1[1][j];
     }
+    // one-sided Jacobi SVD (OpenCV's cv::SVD): for the wrong candidates the two
+    // smallest singular values are often close, where inverse iteration (dlt_null4)
+    // converges slowly and the cheirality signs rest on the exact SVD vector
     double Qh[4];
     smallest_right_sv4(A, Qh);
     bool ok = Qh[2] * Qh[3] > 0;
