@@ -213,7 +213,9 @@ int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *p
  * (shared-focal 6-point: the root stage of PoseLib relpose_6pt_shared_focal as
  * called at src/hybrid_pose_shared_focal_estimator.cpp:87; pts0/pts1: ns x 6 x 2
  * normalized points; cand per sample: the 3x9 epipolar null-space basis N, then the
- * positive roots u = f^2 of the degree-15 focal polynomial, ascending).  Test hook. */
+ * positive roots u = f^2 of the degree-15 focal polynomial, ascending); for the
+ * 6-point, impl 2 = one sample per 64-lane wave with the DFT nodes split over its four
+ * groups (MADPOSE_PT6_WAVE=1 in the estimator; default impl 1).  Test hook. */
 int mp_debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
                       int32_t *ncand, int device);
 

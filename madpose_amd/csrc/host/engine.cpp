@@ -1611,7 +1611,8 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
 
 void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
                     int *ncand, int device) {
-    if (impl < 0 || impl > 1) throw std::invalid_argument("impl must be 0 (lane) or 1 (group)");
+    if (impl < 0 || impl > (variant == 1 ? 2 : 1))
+        throw std::invalid_argument("impl must be 0 (lane), 1 (group) or, for the 6-point, 2 (wave)");
     if (variant != kCal && variant != kSF) throw std::invalid_argument("variant must be 0 (5pt) or 1 (6pt)");
     if (ns <= 0 || ns > (1 << 22)) throw std::invalid_argument("bad number of samples");
     CtxLease lease(device);

@@ -212,5 +212,122 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MP_G6_W
     G6_MARK(6);
 }
 
+// The same root stage with one sample per 64-lane workgroup: the four 16-lane groups
+// evaluate the nine DFT nodes of a pass in parallel (group g takes nodes g, g + 4,
+// g + 8), so a pass costs three determinant LUs in sequence instead of nine.  Every
+// group builds the pencil rows and runs the DFT and the Sturm search on the same
+// values (the barriers inside need every lane); group 0 writes.  Per value the
+// operations are those of pt_roots6_group_kernel, so the two agree bit for bit.
+// Measured slower at the shared-focal batch sizes (399 vs 291 us per launch: four
+// times the waves, and the LU steps are issue-bound, not latency-bound), so it is an
+// A/B option (MADPOSE_PT6_WAVE=1), not the default.
+struct Group6WaveShared {
+    double N[3][9];
+    double piv[kGrpPerWg][20];
+    double qv[9][2];
+    double q[kSixDeg + 1];
+    GroupSturm<kSixDeg> st[kGrpPerWg];
+};
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MP_G6_WAVES)))
+pt_roots6_wave_kernel(PairData D, PairConst C, const int *list, int nlist, const int *samples, double *cand,
+                      int *ncand, int cand_stride) {
+    __shared__ Group6WaveShared sh;
+    const int g = threadIdx.x / kGrp, r = threadIdx.x % kGrp;
+    const int idx = blockIdx.x;
+    const int *s = samples + (size_t)list[idx] * kSampleStride;
+
+    double m0[10], m1[10], m2[10];
+    {
+        double N[3][9];
+        {
+            double b0[6][3], b1[6][3];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int i = s[j];
+                const double a[3] = {D.x0u[i], D.x0v[i], 1.0}, c[3] = {D.x1u[i], D.x1v[i], 1.0};
+                const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    b0[j][q] = a[q] * na;
+                    b1[j][q] = c[q] * nc;
+                }
+            }
+            double Q[6][9];
+            epipolar_rows<6>(b0, b1, Q);
+            nullspace_kx9<6>(Q, N);
+        }
+        if (g == 0) {
+#pragma unroll
+            for (int q = 0; q < 27; ++q)
+                if (q % kGrp == r) sh.N[q / 9][q % 9] = N[q / 9][q % 9];
+        }
+    }
+    __syncthreads();
+    if (r < 10) {
+        sixpt_row([&](int e) { return Lin2{{sh.N[0][e], sh.N[1][e], sh.N[2][e]}}; }, r, m0, m1, m2);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 10; ++c) m0[c] = m1[c] = m2[c] = 0.0;
+    }
+    double poly[kSixDeg + 1];
+    double rho = 1.0;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll 1
+        for (int jb = 0; jb <= 8; jb += kGrpPerWg) {
+            const int j = jb + g; // node of this group (j > 8: a discarded LU that keeps the barriers in step)
+            const int jn = j <= 8 ? j : 8;
+            const double th = 2.0 * 3.14159265358979323846 * jn / 16.0;
+            const Cx u = {rho * cos(th), rho * sin(th)};
+            const Cx d = group_det_pencil10(m0, m1, m2, u, r, sh.piv[g]);
+            const double r5 = rho * rho * rho * rho * rho;
+            const Cx inv5 = {cos(5.0 * th) / r5, -sin(5.0 * th) / r5};
+            const Cx qj = cmul(d, inv5);
+            if (r == 0 && j <= 8) {
+                sh.qv[j][0] = qj.r;
+                sh.qv[j][1] = qj.i;
+            }
+        }
+        __syncthreads();
+        if (g == 0) {
+            const int k = r;
+            double acc = 0.0;
+#pragma unroll 1
+            for (int j = 0; j < 16; ++j) {
+                const int jj = (j <= 8) ? j : 16 - j;
+                const Cx q = (j <= 8) ? Cx{sh.qv[jj][0], sh.qv[jj][1]} : Cx{sh.qv[jj][0], -sh.qv[jj][1]};
+                const double th = -2.0 * 3.14159265358979323846 * j * k / 16.0;
+                acc += q.r * cos(th) - q.i * sin(th);
+            }
+            sh.q[k] = acc / 16.0 / pow(rho, (double)k);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k <= kSixDeg; ++k) poly[k] = sh.q[k];
+        __syncthreads();
+        if (pass == 0) {
+            if (poly[0] != 0.0 && poly[kSixDeg] != 0.0) {
+                rho = pow(fabs(poly[0] / poly[kSixDeg]), 1.0 / 15.0);
+                if (!(rho > 0.0) || !(rho < 1e300)) rho = 1.0;
+            }
+        }
+    }
+
+    double u = 0.0;
+    const bool has_root = group_sturm_roots<kSixDeg>(poly, r, sh.st[g], true, &u);
+    const bool keep = has_root && u > 0.0;
+    int nk;
+    const int at = gscan(keep ? 1 : 0, &nk);
+    if (g == 0) {
+        double *out = cand + (size_t)idx * cand_stride;
+#pragma unroll
+        for (int q = 0; q < 27; ++q)
+            if (q % kGrp == r) out[q] = sh.N[q / 9][q % 9];
+        if (keep) out[27 + at] = u;
+        if (r == 0) ncand[idx] = nk;
+    }
+}
+
 } // namespace
 } // namespace mp

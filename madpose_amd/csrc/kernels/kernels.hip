@@ -867,9 +867,15 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
         // one-lane-per-sample kernels (A/B measurements)
         static const bool lane5 = std::getenv("MADPOSE_PT5_LANE") != nullptr;
         static const bool lane6 = std::getenv("MADPOSE_PT6_LANE") != nullptr;
+        // MADPOSE_PT6_WAVE=1: one sample per wave, DFT nodes over the four groups
+        // (pt_roots6_wave_kernel, A/B: 399 vs 291 us per launch for the group kernel at
+        // the shared-focal batch sizes -- four times the waves, throughput-bound)
+        static const bool wave6 = std::getenv("MADPOSE_PT6_WAVE") != nullptr;
         if (v == kCal && !lane5)
             pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                           kCandStride);
+        else if (v == kSF && !lane6 && wave6)
+            pt_roots6_wave_kernel<<<nlist, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand, kCandStride);
         else if (v == kSF && !lane6)
             pt_roots6_group_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, C, list, nlist, samples,
                                                                                       W.cand, W.ncand, kCandStride);
@@ -942,6 +948,8 @@ hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C,
     } else if (C.variant == kSF) {
         if (impl == 1)
             pt_roots6_group_kernel<<<ggrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
+        else if (impl == 2)
+            pt_roots6_wave_kernel<<<nlist, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
         else
             pt_roots_kernel<kSF><<<lgrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
     } else {

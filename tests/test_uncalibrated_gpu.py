@@ -197,6 +197,26 @@ def _pt6_roots(impl, p0, p1):
     return cand, ncand
 
 
+def test_wave_6pt_kernel_matches_group_kernel():
+    """The one-sample-per-wave 6-point root kernel (DFT nodes of a pass split over the
+    wave's four 16-lane groups; MADPOSE_PT6_WAVE=1 in the estimator) against the
+    four-samples-per-wave group kernel: the same operations per value, so the null-space
+    bases, root counts and roots are bit-identical, on clean and noisy samples."""
+    rng = np.random.default_rng(12)
+    ns = 1200
+    p0 = np.zeros((ns, 6, 2))
+    p1 = np.zeros((ns, 6, 2))
+    for s in range(ns):
+        a, b, _, _, _, _ = _sample(rng, 6, True, False, 0.0 if s % 2 == 0 else 0.01)
+        p0[s], p1[s] = a, b
+    c1, n1 = _pt6_roots(1, p0, p1)
+    c2, n2 = _pt6_roots(2, p0, p1)
+    assert np.array_equal(n1, n2)
+    for s in range(ns):
+        k = 27 + n1[s]
+        assert np.array_equal(c1[s, :k], c2[s, :k]), s
+
+
 def test_group_6pt_kernel_matches_lane_kernel():
     """The 16-lane-group 6-point root kernel (the shared-focal estimator's default)
     against the one-lane-per-sample kernel on the same samples: both perform the same
