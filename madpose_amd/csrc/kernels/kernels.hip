@@ -457,36 +457,47 @@ __global__ void __launch_bounds__(64) pt_tail_kernel(PairData D, PairConst C, co
     }
 }
 
+// Compaction of a point sample's valid tail slots into its model slots, in slot
+// order: one lane per slot (G lanes per sample, G >= the slot count), the kept
+// slot's position from a ballot over the group, so the models' score records are
+// formed in parallel instead of one after another in one lane.  Shared focal: two
+// roots of the interpolated q(u) that the polish took to the same solution give the
+// same pose twice; a slot equal to an earlier valid one is dropped (the first stays).
+// At most maxm models are kept (the first ones).
 template <int V>
 __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *list, int nlist, const int *ncand,
                                                         const Model *slots, const int *valid, Model *models,
                                                         ScoreRec *recs, int *counts, int maxm) {
     using T = PtTraits<V>;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= nlist) return;
-    const int b = list[idx];
+    constexpr int kSlots = T::kPosesPerRoot * T::kRoots;
+    constexpr int G = kSlots <= 4 ? 4 : 32;
+    static_assert(kSlots <= G && kSlots <= kSlotStride && 64 % G == 0, "slot group");
+    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G), q = threadIdx.x % G;
+    const bool active = gid < nlist;
+    const int idx = active ? gid : nlist - 1;
     const int total = T::kPosesPerRoot * min(ncand[idx], T::kRoots);
-    int n = 0;
-    for (int q = 0; q < total; ++q) {
-        if (!valid[(size_t)idx * kSlotStride + q] || n >= maxm) continue;
-        const Model &m = slots[(size_t)idx * kSlotStride + q];
-        // shared focal: two roots of the interpolated q(u) that the polish took to the
-        // same solution of the system give the same pose twice; keep the first
-        if (V == kSF) {
-            bool dup = false;
-            for (int p = 0; p < q && !dup; ++p) {
-                if (!valid[(size_t)idx * kSlotStride + p]) continue;
-                const Model &o = slots[(size_t)idx * kSlotStride + p];
-                bool same = fabs(o.focal0 - m.focal0) <= 1e-8 * fabs(m.focal0);
-                for (int e = 0; e < 9 && same; ++e) same = fabs(o.R[e] - m.R[e]) <= 1e-6;
-                for (int e = 0; e < 3 && same; ++e) same = fabs(o.t[e] - m.t[e]) <= 1e-6 * (1.0 + fabs(m.t[e]));
-                dup = same;
-            }
-            if (dup) continue;
+    const size_t base = (size_t)idx * kSlotStride;
+    bool keep = active && q < total && valid[base + q];
+    if (V == kSF && keep) {
+        const Model &m = slots[base + q];
+        for (int p = 0; p < q && keep; ++p) {
+            if (!valid[base + p]) continue;
+            const Model &o = slots[base + p];
+            bool same = fabs(o.focal0 - m.focal0) <= 1e-8 * fabs(m.focal0);
+            for (int e = 0; e < 9 && same; ++e) same = fabs(o.R[e] - m.R[e]) <= 1e-6;
+            for (int e = 0; e < 3 && same; ++e) same = fabs(o.t[e] - m.t[e]) <= 1e-6 * (1.0 + fabs(m.t[e]));
+            keep = !same;
         }
-        put_model(C, m, b, n++, maxm, models, recs);
     }
-    counts[b] = n;
+    const unsigned long long ball = __ballot(keep);
+    const int lane = threadIdx.x & 63, g0 = lane & ~(G - 1);
+    const unsigned long long mine = (ball >> g0) & (G == 64 ? ~0ull : ((1ull << G) - 1));
+    const int pos = __popcll(mine & ((1ull << q) - 1));
+    if (keep && pos < maxm) put_model(C, slots[base + q], list[idx], pos, maxm, models, recs);
+    if (active && q == 0) {
+        const int n = __popcll(mine);
+        counts[list[idx]] = n < maxm ? n : maxm;
+    }
 }
 
 // FAST: score_type 0 (hybrid, no gating) and not scale-only, and for the calibrated
@@ -906,8 +917,9 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
         else
             pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                       W.slots, W.valid);
-        pt_compact_kernel<v><<<grid, 64, 0, s>>>(C, list, nlist, W.ncand, W.slots, W.valid, models, recs, counts,
-                                                 maxm);
+        constexpr int kCompactG = PtTraits<v>::kPosesPerRoot * PtTraits<v>::kRoots <= 4 ? 4 : 32;
+        pt_compact_kernel<v><<<(int)(((size_t)nlist * kCompactG + 63) / 64), 64, 0, s>>>(
+            C, list, nlist, W.ncand, W.slots, W.valid, models, recs, counts, maxm);
         return hipGetLastError();
     });
 }
