@@ -330,6 +330,53 @@ MP_HD bool recover_pose_good(const RecoverCands &rc, int k, const double *p0, co
     return ok && z1 > 0 && z1 < dist;
 }
 
+// The same test for the two candidates (R, t) and (R, -t) of one rotation (kr = 0: R1,
+// 1: R2) from one SVD.  Their DLT matrices differ by the sign of the last column (A' =
+// A diag(1, 1, 1, -1)); every operation of the one-sided Jacobi is odd or even in that
+// column's sign (rounding is sign-symmetric), so the sweeps on A' run the mirrored
+// rotations of those on A and end at diag(1, 1, 1, -1) times A's vector, up to the
+// overall sign: (Qh0, Qh1, Qh2, -Qh3) decides (R, -t) bit for bit as its own SVD would
+// (the one exception, zeta == 0 exactly in a rotation, has measure zero).
+MP_HD void recover_pose_good_pair(const RecoverCands &rc, int kr, const double *p0, const double *p1, double dist,
+                                  bool *good_pos, bool *good_neg) {
+    double P1[3][4];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) P1[r][c] = (kr & 1) ? opaque(rc.R2[3 * r + c]) : opaque(rc.R1[3 * r + c]);
+        P1[r][3] = rc.u2[r];
+    }
+    double A[4][4];
+    A[0][0] = -1.0;
+    A[0][1] = 0.0;
+    A[0][2] = p0[0];
+    A[0][3] = 0.0;
+    A[1][0] = 0.0;
+    A[1][1] = -1.0;
+    A[1][2] = p0[1];
+    A[1][3] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        A[2][j] = p1[0] * P1[2][j] - P1[0][j];
+        A[3][j] = p1[1] * P1[2][j] - P1[1][j];
+    }
+    double Qh[4];
+    smallest_right_sv4(A, Qh);
+#pragma unroll
+    for (int sgn = 0; sgn < 2; ++sgn) {
+        const double q3 = sgn ? -Qh[3] : Qh[3], t2 = sgn ? -P1[2][3] : P1[2][3];
+        bool ok = Qh[2] * q3 > 0;
+        const double X0 = Qh[0] / q3, X1 = Qh[1] / q3, X2 = Qh[2] / q3;
+        ok = ok && X2 < dist;
+        const double z1 = P1[2][0] * X0 + P1[2][1] * X1 + P1[2][2] * X2 + t2;
+        ok = ok && z1 > 0 && z1 < dist;
+        if (sgn)
+            *good_neg = ok;
+        else
+            *good_pos = ok;
+    }
+}
+
 // the candidate with the most good points (ties: the first); returns its count
 MP_HD int recover_pose_select(const RecoverCands &rc, const int (&good)[4], double *R, double *t) {
     int best = 3;
@@ -355,8 +402,13 @@ MP_HD int recover_pose_cv(const double *E_in, const double (&p0)[K][2], const do
     recover_pose_candidates(E_in, rc);
     int good[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        for (int i = 0; i < K; ++i) good[k] += recover_pose_good(rc, k, p0[i], p1[i], dist) ? 1 : 0;
+    for (int kr = 0; kr < 2; ++kr)
+        for (int i = 0; i < K; ++i) {
+            bool gp, gn;
+            recover_pose_good_pair(rc, kr, p0[i], p1[i], dist, &gp, &gn);
+            good[kr] += gp ? 1 : 0;
+            good[kr + 2] += gn ? 1 : 0;
+        }
     return recover_pose_select(rc, good, R, t);
 }
 

@@ -72,8 +72,14 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
     recover_pose_candidates(E, rc);
     int good[4];
     if (G == 8) {
+        // one SVD per rotation decides both signs of t (recover_pose_good_pair)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) good[c] = gsum8((has && recover_pose_good(rc, c, p0[0], p1[0], 1e9)) ? 1 : 0);
+        for (int kr = 0; kr < 2; ++kr) {
+            bool gp, gn;
+            recover_pose_good_pair(rc, kr, p0[0], p1[0], 1e9, &gp, &gn);
+            good[kr] = gsum8((has && gp) ? 1 : 0);
+            good[kr + 2] = gsum8((has && gn) ? 1 : 0);
+        }
     } else {
         const int mine = gsum8((has && recover_pose_good(rc, sub, p0[0], p1[0], 1e9)) ? 1 : 0);
         const int base = (threadIdx.x & 63) & ~(G - 1);
