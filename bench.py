@@ -547,6 +547,8 @@ def main(argv=None):
                     help="processes of the all-core CPU baseline leg (0 = one per physical core)")
     ap.add_argument("--pairs", type=int, default=0, help="scannet: total pairs (default 1500)")
     ap.add_argument("--streams", type=int, default=8, help="scannet: pairs in flight per GPU")
+    ap.add_argument("--in-flight", type=int, default=8,
+                    help="configs[1..3]: also time the pairs k at a time on the GPU (secondary figure; 1 = skip)")
     ap.add_argument("--no-point-only", dest="point_only", action="store_false",
                     help="scannet: skip the untimed point-only baseline pass")
     ap.add_argument("--engine-module", default=None, help=argparse.SUPPRESS)
@@ -572,12 +574,14 @@ def main(argv=None):
 
     eng = _engine(a)
     gpu = a.engine_module is None and torch.cuda.is_available()
+    # rehearsal knobs for one-GPU boxes (several ranks on one card need gloo: RCCL
+    # refuses two ranks on one device): MADPOSE_BENCH_DIST_BACKEND, MADPOSE_BENCH_DEVICE
+    dev = int(os.environ.get("MADPOSE_BENCH_DEVICE", local_rank)) if gpu else 0
     if world > 1:
-        backend = "nccl" if gpu else "gloo"
+        backend = os.environ.get("MADPOSE_BENCH_DIST_BACKEND", "nccl" if gpu else "gloo")
         if backend == "nccl":
-            torch.cuda.set_device(local_rank)
+            torch.cuda.set_device(dev)
         dist.init_process_group(backend=backend)
-    dev = local_rank if gpu else 0
 
     def barrier():
         if world > 1:
@@ -630,12 +634,28 @@ def main(argv=None):
     if rank == 0:
         out = summarize(allv, wl, a.steps, a.warmup, world)
         out["results"] = records_summary(allr)
+        if world == 1 and a.in_flight > 1:
+            out["pairs_in_flight"] = in_flight_leg(eng, wl, pairs[a.warmup:], o, c, dev, a.in_flight)
         if world == 1 and a.cpu_budget > 0:
             out["cpu_baseline"] = cpu_baseline(wl, pairs[a.warmup], a.cpu_budget, a.cpu_procs)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def in_flight_leg(eng, wl, pairs, o, c, dev, k):
+    """Secondary figure (never `value`): the same timed pairs with k estimators in flight
+    on the one GPU (estimate_batch: k host threads, one HIP stream context each). One
+    estimator leaves the GPU idle while its host LO runs; concurrent pairs fill it."""
+    eng.estimate_batch(wl["variant"], pairs[:k], o, c, device=dev, num_streams=k)  # warm the contexts
+    t0 = time.perf_counter()
+    res = eng.estimate_batch(wl["variant"], pairs, o, c, device=dev, num_streams=k)
+    el = time.perf_counter() - t0
+    hyps = sum(st.num_hypotheses for _, st in res)
+    return {"pairs": len(pairs), "in_flight": k, "hypotheses_per_s": hyps / el, "ms_per_pair": el / len(pairs) * 1e3,
+            "note": "the timed pairs again, k at a time on one GPU (host threads x streams); a secondary figure, "
+                    "not the bench value (which keeps configs[1]'s one pair per step)"}
 
 
 if __name__ == "__main__":
