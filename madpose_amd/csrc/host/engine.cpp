@@ -694,6 +694,9 @@ class Run {
         double t[3] = {0, 0, 0}; // launch / wait / copy seconds (MADPOSE_SWEEP_TIMING)
     };
     Lane lanes_[kLoLanes]; // lanes_[0]: the estimator thread
+    // LO phase seconds (MADPOSE_LO_TIMING): serial prefix, steps phase, LO count, sum of
+    // step times, longest step, step-0 time
+    double lo_t_[6] = {0, 0, 0, 0, 0, 0};
     bool lo_parallel_ = true;
 
     const double *sweep(Lane &L, const Model &m, double *score) {
@@ -992,6 +995,8 @@ class Run {
         const int k_nonmin = std::max(non_min_sample_size_,
                                       std::min(min_sample_size_ * o_.non_min_sample_multiplier, (int)base_all.size() / 2));
         const int R = o_.num_lo_steps;
+        lo_t_[0] += secs(t0); // serial prefix: initial fit, score, base inliers
+        auto t_steps = Clock::now();
         if (R > 0) {
             // step 0 solves on base_all as it is and then shuffles it down to
             // k_nonmin; later steps shuffle nothing (it is that size already) and all
@@ -1016,7 +1021,9 @@ class Run {
                     end.discard(pos - base_sel.draws());
                     predicted(end);
                 }
+                std::vector<double> step_s(R, 0.0);
                 X_.lo_workers->run(R, [&](int r, int lane) {
+                    auto ts = Clock::now();
                     if (lane != 0) MP_HIP(hipSetDevice(X_.device));
                     Mt19937 my = base_sel;
                     my.discard(start[r] - base_sel.draws());
@@ -1025,7 +1032,13 @@ class Run {
                     lo_step(L, st, r == 0 ? sample0 : sample1, m_init, thr, upd, outs[r]);
                     L.sel = lane == 0 ? &rs_.sel : nullptr;
                     outs[r].sel = my;
+                    step_s[r] = secs(ts);
                 });
+                for (int r = 0; r < R; ++r) {
+                    lo_t_[3] += step_s[r];
+                    lo_t_[4] = std::max(lo_t_[4], step_s[r]);
+                }
+                lo_t_[5] += step_s[0];
                 // steps 0..r are right while each one ended where the next one started
                 first_serial = R;
                 for (int r = 0; r + 1 < R; ++r)
@@ -1047,6 +1060,8 @@ class Run {
             for (int r = 0; r < R; ++r)
                 for (const auto &u : outs[r].updates) update_best(u.first, u.second, st, best_min_score, best_min, best_st);
         }
+        lo_t_[1] += secs(t_steps);
+        lo_t_[2] += 1.0;
         S_->seconds_lo += secs(t0);
     }
 
@@ -1370,6 +1385,10 @@ void Run::run(Model *best, Stats *S) {
         S->num_lo_sweeps += L.count;
         for (int k = 0; k < 3; ++k) tsum[k] += L.t[k];
     }
+    if (std::getenv("MADPOSE_LO_TIMING") && lo_t_[2] > 0)
+        std::fprintf(stderr, "[engine] %d LO: prefix %.1f us, steps %.1f us, step sum %.1f us, step0 %.1f us, longest "
+                     "step %.1f us (avg per LO)\n", (int)lo_t_[2], 1e6 * lo_t_[0] / lo_t_[2], 1e6 * lo_t_[1] / lo_t_[2],
+                     1e6 * lo_t_[3] / lo_t_[2], 1e6 * lo_t_[5] / lo_t_[2], 1e6 * lo_t_[4]);
     if (std::getenv("MADPOSE_SWEEP_TIMING") && S->num_lo_sweeps > 0)
         std::fprintf(stderr, "[engine] %llu sweeps: launch %.2f us, wait %.2f us, copy %.2f us (avg)\n",
                      (unsigned long long)S->num_lo_sweeps, 1e6 * tsum[0] / S->num_lo_sweeps,
