@@ -39,3 +39,30 @@ def test_batch_pose_auc_matches_oracle():
     auc_orc = utils.pose_auc(e_orc, (5, 10, 20))
     assert np.allclose(auc_dev, auc_orc, rtol=0, atol=1e-6), (auc_dev, auc_orc)
     assert auc_dev[2] > 0.5  # the synthetic set is solvable
+
+
+def test_full_size_scannet_pairs_match_oracle():
+    """configs[4] at its own sizes: the first 150 pairs of the stand-in set (seeds 0..149,
+    N ~ U{1500..2500}, the bench's example options with 1000 iterations) with 8 pairs in
+    flight, as bench.py runs them; every pair equals the oracle's, and the device pose
+    evaluator (mp_pose_eval) gives the oracle poses' AUC@5/10/20."""
+    pairs = [synthetic.scannet_pair(s) for s in range(150)]
+    o, c = synthetic.example_options("shared_focal", iterations=1000)
+    res = madpose.estimate_batch(1, pairs, o, c, num_streams=8)
+    Ro, to = [], []
+    for p, (m, st) in zip(pairs, res):
+        ref, rst, inl = oracle.estimate(1, p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], p["pp0"],
+                                        p["pp1"], oracle_opts(o), oracle_cfg(c))
+        assert st.num_iterations_total == rst.num_iterations_total
+        assert st.number_lo_iterations == rst.number_lo_iterations
+        assert rot_angle_deg(m.R(), ref["R"]) <= 1e-6
+        for t in range(3):
+            assert np.array_equal(np.sort(st.inlier_indices[t]), np.sort(inl[t]))
+        Ro.append(ref["R"])
+        to.append(ref["t"])
+    T = np.stack([p["T_0to1"] for p in pairs])
+    R = np.stack([np.asarray(m.R()) for m, _ in res])
+    t = np.stack([np.asarray(m.t()).reshape(3) for m, _ in res])
+    _, _, auc_dev = madpose.pose_eval_batch(T, R, t, (5, 10, 20))
+    e_orc = [max(utils.compute_pose_error(T[k], Ro[k], to[k])) for k in range(len(pairs))]
+    assert np.allclose(auc_dev, utils.pose_auc(e_orc, (5, 10, 20)), rtol=0, atol=1e-6)
