@@ -230,7 +230,19 @@ struct SweepSlot {
             if (borrowed) {
                 stream = borrowed;
             } else {
-                MP_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+                // MADPOSE_SWEEP_PRIORITY=1: the device's highest stream priority, so LO
+                // sweeps dispatch ahead of a speculative batch's queued workgroups
+                static const bool prio = [] {
+                    const char *e = std::getenv("MADPOSE_SWEEP_PRIORITY");
+                    return e && e[0] == '1';
+                }();
+                if (prio) {
+                    int lo = 0, hi = 0;
+                    MP_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                    MP_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+                } else {
+                    MP_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+                }
                 own_stream = true;
             }
         }
@@ -696,7 +708,9 @@ class Run {
     Lane lanes_[kLoLanes]; // lanes_[0]: the estimator thread
     // LO phase seconds (MADPOSE_LO_TIMING): serial prefix, steps phase, LO count, sum of
     // step times, longest step, step-0 time
-    double lo_t_[6] = {0, 0, 0, 0, 0, 0};
+    // + step 0's non-minimal fit and score, other steps' fit; step 0's first lsq_fit and
+    // lsq iterations, the other steps' (mean)
+    double lo_t_[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool lo_parallel_ = true;
 
     const double *sweep(Lane &L, const Model &m, double *score) {
@@ -943,6 +957,8 @@ class Run {
     struct StepOut {
         std::vector<std::pair<double, Model>> updates; // the step's update_best calls, in order
         Mt19937 sel;                                   // LO stream after the step
+        double nonmin_s = 0.0, score_s = 0.0;          // MADPOSE_LO_TIMING: non-minimal fit, its score,
+        double lsq_s = 0.0, iter_s = 0.0;              // the first lsq_fit, the lsq iterations
     };
     // One LO step (the loop body of src/hybrid_ransac.h:435-470) from m_init on the
     // non-minimal sample `sample_all`, drawing from *L.sel.
@@ -953,15 +969,23 @@ class Run {
         Model m = m_init;
         std::vector<int> smp[3];
         split(sample_all, n_, smp);
+        auto t_nm = Clock::now();
         least_squares(L, smp, &m, true);
+        out.nonmin_s = secs(t_nm);
+        auto t_sc = Clock::now();
         out.updates.emplace_back(score(L, m), m);
+        out.score_s = secs(t_sc);
+        auto t_l = Clock::now();
         lsq_fit(L, thr_, st, &m, false);
+        out.lsq_s = secs(t_l);
         double cur[3] = {thr[0], thr[1], thr[2]};
+        auto t_it = Clock::now();
         for (int i = 0; i < o_.num_lsq_iterations; ++i) {
             lsq_fit(L, cur, st, &m, false);
             out.updates.emplace_back(score(L, m), m);
             for (int t = 0; t < 3; ++t) cur[t] -= upd[t];
         }
+        out.iter_s = secs(t_it);
     }
 
     // LocalOptimization (src/hybrid_ransac.h:383-470).  The steps depend on each
@@ -1039,6 +1063,15 @@ class Run {
                     lo_t_[4] = std::max(lo_t_[4], step_s[r]);
                 }
                 lo_t_[5] += step_s[0];
+                lo_t_[6] += outs[0].nonmin_s;
+                lo_t_[7] += outs[0].score_s;
+                for (int r = 1; r < R; ++r) lo_t_[8] += outs[r].nonmin_s / (R - 1);
+                lo_t_[9] += outs[0].lsq_s;
+                lo_t_[10] += outs[0].iter_s;
+                for (int r = 1; r < R; ++r) {
+                    lo_t_[11] += outs[r].lsq_s / (R - 1);
+                    lo_t_[12] += outs[r].iter_s / (R - 1);
+                }
                 // steps 0..r are right while each one ended where the next one started
                 first_serial = R;
                 for (int r = 0; r + 1 < R; ++r)
@@ -1051,6 +1084,7 @@ class Run {
                     std::fprintf(stderr, "[engine] LO step %d started off its predicted draw; recomputing\n",
                                  first_serial);
             }
+            lo_t_[13] += R - first_serial; // steps recomputed in order
             for (int r = first_serial; r < R; ++r) {
                 L0.sel = &sel;
                 lo_step(L0, st, r == 0 ? sample0 : sample1, m_init, thr, upd, outs[r]);
@@ -1387,8 +1421,12 @@ void Run::run(Model *best, Stats *S) {
     }
     if (std::getenv("MADPOSE_LO_TIMING") && lo_t_[2] > 0)
         std::fprintf(stderr, "[engine] %d LO: prefix %.1f us, steps %.1f us, step sum %.1f us, step0 %.1f us, longest "
-                     "step %.1f us (avg per LO)\n", (int)lo_t_[2], 1e6 * lo_t_[0] / lo_t_[2], 1e6 * lo_t_[1] / lo_t_[2],
-                     1e6 * lo_t_[3] / lo_t_[2], 1e6 * lo_t_[5] / lo_t_[2], 1e6 * lo_t_[4]);
+                     "step %.1f us, step0 fit %.1f us, step0 score %.1f us, other fit %.1f us, step0 lsq %.1f us, "
+                     "step0 iters %.1f us, other lsq %.1f us, other iters %.1f us (avg per LO), recomputed %.2f us\n",
+                     (int)lo_t_[2], 1e6 * lo_t_[0] / lo_t_[2], 1e6 * lo_t_[1] / lo_t_[2], 1e6 * lo_t_[3] / lo_t_[2],
+                     1e6 * lo_t_[5] / lo_t_[2], 1e6 * lo_t_[4], 1e6 * lo_t_[6] / lo_t_[2], 1e6 * lo_t_[7] / lo_t_[2],
+                     1e6 * lo_t_[8] / lo_t_[2], 1e6 * lo_t_[9] / lo_t_[2], 1e6 * lo_t_[10] / lo_t_[2],
+                     1e6 * lo_t_[11] / lo_t_[2], 1e6 * lo_t_[12] / lo_t_[2], lo_t_[13] / lo_t_[2]);
     if (std::getenv("MADPOSE_SWEEP_TIMING") && S->num_lo_sweeps > 0)
         std::fprintf(stderr, "[engine] %llu sweeps: launch %.2f us, wait %.2f us, copy %.2f us (avg)\n",
                      (unsigned long long)S->num_lo_sweeps, 1e6 * tsum[0] / S->num_lo_sweeps,
