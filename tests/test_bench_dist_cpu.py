@@ -149,3 +149,16 @@ def test_records_summary_and_gather_single_rank():
     assert allr.shape == (4, w)
     s = bench.records_summary(allr)
     assert s["records"] == 4 and s["pairs_disjoint"] and s["median_pose_err_deg"] == np.median([0, 2, 4, 6])
+
+
+def test_single_rank_in_flight_leg_and_records():
+    """One rank: the pairs-in-flight secondary figure (estimate_batch k at a time) sits
+    beside `value` without replacing it, and the records carry the engine's pose errors."""
+    res = _run_bench(["--steps", "4", "--warmup", "1", "--cpu-budget", "0", "--in-flight", "3", "--engine-module",
+                      "tests.bench_stub_engine"])
+    assert res["n_gpus"] == 1 and res["value"] > 0
+    pf = res["pairs_in_flight"]
+    assert pf["pairs"] == 4 and pf["in_flight"] == 3 and pf["hypotheses_per_s"] > 0
+    assert res["results"]["records"] == 4
+    # the stub returns R = I, t = (1, 0, 0): its pose errors come from compute_pose_error
+    assert res["results"]["median_pose_err_deg"] >= 0.0

@@ -5,6 +5,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/pt5_bench.hip -o tools/pt5_bench
 //   tools/pt5_bench [samples]
 #define MP_GROUP5_PROFILE 1
+#define MP_GROUP_PROFILE 1
 #include "../madpose_amd/csrc/kernels/kernels.hip"
 
 #include <cstdio>
@@ -138,6 +139,7 @@ int main(int argc, char **argv) {
     for (int which = 0; which < 2; ++which) {
         unsigned long long z[8] = {0};
         CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g5_prof), z, sizeof(z)));
+        CHECK(hipMemcpyToSymbol(HIP_SYMBOL(gs_prof), z, 4 * sizeof(z[0])));
         const int reps = 10;
         CHECK(hipEventRecord(a));
         for (int r = 0; r < reps; ++r) which ? run_group() : run_lane();
@@ -155,6 +157,11 @@ int main(int argc, char **argv) {
             for (int i = 0; i < 8; ++i)
                 std::printf("  %-13s %5.1f%%  (%.0f ticks/group)\n", names[i], 100.0 * z[i] / tot,
                             (double)z[i] / (reps * (double)ns));
+            unsigned long long zs[4];
+            CHECK(hipMemcpyFromSymbol(zs, HIP_SYMBOL(gs_prof), sizeof(zs)));
+            const char *sn[4] = {"chain", "grid counts", "cells", "refine"};
+            for (int i = 0; i < 4; ++i)
+                std::printf("    sturm %-11s %.1f ticks/workgroup\n", sn[i], (double)zs[i] * kS5 / (reps * (double)ns));
         }
     }
     return cnt_diff == 0 ? 0 : 3;
