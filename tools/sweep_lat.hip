@@ -5,6 +5,9 @@
 //   dev    the same with the error rows in device memory (flag still host)
 //   flags  sweep_host_kernel as shipped: one flag per workgroup, host sums
 //   flag   a one-workgroup kernel that only raises the flag (the floor)
+//   ldonly / stonly / nold_nost   the shipped flag protocol with only the pair loads,
+//          only the error-row stores, neither (8 workgroups); nlns_wg1 the last on one
+//          workgroup; ls_1024 loads + stores on 1024-lane workgroups
 //   noeval / nofence / neither   the shipped protocol without the residuals, without
 //          the per-workgroup system fence, without both
 // Build + run (on an MI355X):
@@ -101,6 +104,28 @@ __global__ void __launch_bounds__(256) sweep_var_kernel(PairData D, PairConst C,
         }
     }
 }
+// isolating loads and stores: LOAD = false uses the index instead of the pair data,
+// STORE = false skips the error rows (the partial score and flag protocol stay)
+template <bool LOAD, bool STORE, int NT, bool FENCE = true>
+__global__ void __launch_bounds__(NT) sweep_ls_kernel(PairData D, PairConst C, double *out, int *flags, int seq) {
+    double acc = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < C.n; i += gridDim.x * NT) {
+        const double e0 = LOAD ? D.x0u[i] + D.x0v[i] + D.x1u[i] : (double)i;
+        const double e1 = LOAD ? D.x1v[i] + D.d0[i] + D.d1[i] : 1.0;
+        const double e2 = LOAD ? D.r0[i] + D.r1[i] : 2.0;
+        if (STORE) {
+            out[i] = e0;
+            out[C.n + i] = e1;
+            out[2 * C.n + i] = e2;
+        }
+        acc += e0 + e1 + e2;
+    }
+    const double v = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) out[3 * C.n + (NT / 64) * blockIdx.x + (threadIdx.x >> 6)] = v;
+    if (FENCE) __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 } // namespace
 
 using Clock = std::chrono::steady_clock;
@@ -190,17 +215,32 @@ int main(int argc, char **argv) {
                 sweep_var_kernel<kCal, true, false><<<sweep_blocks(n), 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q, part, cnt);
             else if (mode == 7)
                 sweep_var_kernel<kCal, false, false><<<sweep_blocks(n), 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q, part, cnt);
+            else if (mode == 9)
+                sweep_ls_kernel<true, false, 256><<<nbk, 256, 0, s>>>(D, C, d_out8, d_flags, q);
+            else if (mode == 10)
+                sweep_ls_kernel<false, true, 256><<<nbk, 256, 0, s>>>(D, C, d_out8, d_flags, q);
+            else if (mode == 11)
+                sweep_ls_kernel<false, false, 256><<<nbk, 256, 0, s>>>(D, C, d_out8, d_flags, q);
+            else if (mode == 12)
+                sweep_ls_kernel<false, false, 256><<<1, 256, 0, s>>>(D, C, d_out8, d_flags, q);
+            else if (mode == 13)
+                sweep_ls_kernel<true, true, 1024><<<(n + 1023) / 1024, 1024, 0, s>>>(D, C, d_out8, d_flags, q);
+            else if (mode == 14)
+                sweep_ls_kernel<false, false, 256, false><<<nbk, 256, 0, s>>>(D, C, d_out8, d_flags, q);
+            else if (mode == 15)
+                sweep_ls_kernel<false, false, 64, true><<<nbk, 64, 0, s>>>(D, C, d_out8, d_flags, q);
             else if (mode == 3)
                 sweep1_kernel<kCal, 1024><<<1, 1024, 0, s>>>(D, C, rec, d_out_h, d_flag, q);
             else
                 sweep1_kernel<kCal, 256><<<1, 256, 0, s>>>(D, C, rec, d_out_h, d_flag, q);
             auto t1 = Clock::now();
-            if (mode == 8) {
-                for (int b = 0; b < nbk; ++b)
+            if (mode >= 8) {
+                const int nbw = mode == 12 ? 1 : (mode == 13 ? (n + 1023) / 1024 : nbk);  // (15: nbk blocks of 64)
+                for (int b = 0; b < nbw; ++b)
                     while (__atomic_load_n(h_flags + b, __ATOMIC_ACQUIRE) != q) {
                     }
                 double tot = 0.0;
-                for (int b = 0; b < nbk; ++b) tot += h_out8[3 * n + b];
+                for (int b = 0; b < nbw; ++b) tot += h_out8[3 * n + b];
                 h_out[3 * n] = tot;
             } else {
                 while (__atomic_load_n(h_flag, __ATOMIC_ACQUIRE) != q) {
@@ -223,6 +263,15 @@ int main(int argc, char **argv) {
     run("noeval", 5);
     run("nofence", 6);
     run("neither", 7);
+    run("ldonly", 9);
+    run("stonly", 10);
+    run("nold_nost", 11);
+    run("nlns_wg1", 12);
+    run("ls_1024", 13);
+    run("nl_ns_nofence", 14);
+    run("nl_ns_wg64", 15);
+    run("one1024", 3);
+    run("one256", 4);
     run("host", 0);
     std::printf("score %.6f\n", h_out[3 * n]);
     run("flags", 8);
