@@ -40,6 +40,7 @@
 
 #include "../include/mp_score.h"
 #include "../kernels/kernels.h"
+#include "batch_draw.h"
 #include "rng.h"
 
 namespace mp {
@@ -58,41 +59,14 @@ double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::n
 
 const double kMax = DBL_MAX;
 
-// ---------------------------------------------------------------------------
-// Minimal-sample batches (host).  One batch holds its iterations' solver types and
-// samples (in a pinned host slot), plus snapshots of both random streams every
-// kSnap iterations so a rewind to iteration j replays fewer than kSnap iterations.
-constexpr uint32_t kSnap = 512;
-struct Batch {
-    uint32_t B = 0;
-    int nmd = 0, npt = 0, slot = 0;
-    std::vector<uint8_t> types;
-    std::vector<IterationStream> snaps;
-};
-
-// Draws B iterations from rs into g and the slot memory at `smp`: the samples
-// (8 ints per iteration), then right behind them the iteration lists -- MD iterations
-// ascending from the front, point iterations from the back (descending) -- so the
-// batch is one contiguous block of 9B ints (one upload).  Returns false if *abort was
-// raised first (checked every 256 iterations).
-bool draw_batch(IterationStream &rs, Batch &g, uint32_t B, int slot, int *smp, const std::atomic<bool> *abort) {
-    int *lists = smp + 8 * (size_t)B;
-    g.B = B;
-    g.slot = slot;
-    g.nmd = g.npt = 0;
-    g.types.resize(B);
-    g.snaps.clear();
-    for (uint32_t j = 0; j < B; ++j) {
-        if (j % kSnap == 0) g.snaps.push_back(rs);
-        if (abort && (j & 255) == 0 && abort->load(std::memory_order_relaxed)) return false;
-        const int st = rs.next(smp + 8 * j);
-        g.types[j] = (uint8_t)st;
-        if (st == 0)
-            lists[g.nmd++] = (int)j;
-        else
-            lists[B - 1 - g.npt++] = (int)j;
-    }
-    return true;
+// Minimal-sample batches and their drawing: batch_draw.h.  MADPOSE_SAMPLER_TWO_PASS=0
+// keeps the draw-by-draw loop for hybrid batches too (A/B; identical draws).
+bool sampler_two_pass() {
+    static const bool on = [] {
+        const char *e = std::getenv("MADPOSE_SAMPLER_TWO_PASS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // Background sampler: draws the next speculative batch while the current one is on
@@ -152,7 +126,7 @@ class Sampler {
             if (quit_) return;
             seen = gen_;
             lk.unlock();
-            const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, &abort_);
+            const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, &abort_, sampler_two_pass());
             std::exception_ptr err;
             if (ok && after_) {
                 try {
@@ -1111,7 +1085,7 @@ class Run {
     int *slot_ptr(int slot) const { return X_.h_samples + (size_t)slot * 9 * max_batch_; }
     void generate(Batch &g, uint32_t B, int slot) {
         auto t0 = Clock::now();
-        draw_batch(rs_, g, B, slot, slot_ptr(slot), nullptr);
+        draw_batch(rs_, g, B, slot, slot_ptr(slot), nullptr, sampler_two_pass());
         sample_s_ += secs(t0);
     }
     // both streams to the end of iteration j of batch g
