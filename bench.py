@@ -162,7 +162,8 @@ def pmc_traffic_model():
 
 COUNTERS = ["elapsed_s", "hypotheses", "iterations", "lo_runs", "lo_s", "score_ms", "solve_ms", "prof_hypotheses",
             "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms", "prof_iterations",
-            "sample_ms", "wait_ms", "run_ms", "lm_blocks", "lm_big_calls", "lm_big_ms"]
+            "sample_ms", "wait_ms", "run_ms", "lm_blocks", "lm_big_calls", "lm_big_ms", "model_trips",
+            "model_trips_full", "prof_accepted"]
 
 
 def gather_counters(local, world):
@@ -182,6 +183,27 @@ def gather_counters(local, world):
     else:
         dist.all_gather(out, t)
     return torch.stack(out).numpy()
+
+
+def dist_info(world):
+    """Backend and world size as torch.distributed saw them (the N-GPU runs show that
+    RCCL had every rank), plus the LO-pool spin setting of this process."""
+    info = {"backend": None, "world_size": world}
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            info["backend"] = dist.get_backend()
+            info["world_size"] = dist.get_world_size()
+    except Exception:  # pragma: no cover - informational only
+        pass
+    try:
+        from madpose_amd import _lib
+
+        info["lo_spin_us"] = int(_lib.lib().mp_lo_spin_us())
+    except Exception:  # the CPU stand-in engine of the tests has no library
+        info["lo_spin_us"] = None
+    return info
 
 
 def summarize(allv, wl, steps, warmup, world):
@@ -254,9 +276,25 @@ def summarize(allv, wl, steps, warmup, world):
             "avg_launch_us": score_ms * 1e3 / max(launches, 1),
             "bytes_per_hypothesis": BYTES_PER_CORR * wl["n"],
             "solve_ms_per_launch": float(c["solve_ms"].sum()) / max(launches, 1),
+            # exact early exit (row N1): the share of (model, 256-correspondence trip)
+            # evaluations the kernel actually ran, and the correspondence bytes those
+            # evaluations read (48 B each) per launch next to the algorithmic figure
+            "evaluated_frac": (float(c["model_trips"].sum()) / float(c["model_trips_full"].sum())
+                               if float(c["model_trips_full"].sum()) > 0 else None),
+            "evaluated_bytes_per_launch": (float(c["model_trips"].sum()) * 256 * BYTES_PER_CORR / launches
+                                           if launches > 0 else None),
+            "algorithmic_bytes_per_launch": (float(c["prof_correspondences"].sum()) * BYTES_PER_CORR / launches
+                                             if launches > 0 else None),
             "fp64_valu": fp64,
         },
         "cpu_baseline": None,
+        # speculative waste: every hypothesis scored on the GPU against those of the
+        # iterations the estimator consumed (batches cut at an LO, discarded post-LO
+        # speculation); the roofline above credits all scored work
+        "speculation": {"scored_hypotheses": int(c["prof_hypotheses"].sum()),
+                        "accepted_hypotheses": int(c["prof_accepted"].sum()),
+                        "scored_over_accepted": float(c["prof_hypotheses"].sum()) / max(float(c["prof_accepted"].sum()), 1.0)},
+        "dist": dist_info(world),
     }
 
 
@@ -299,6 +337,7 @@ def summarize_scannet(allv, errs, wl, steps, warmup, world, total, auc_fn=None):
         "hypotheses_per_s": float(allv[:, 2].sum()) / t_max,
         "iterations_per_s": float(allv[:, 3].sum()) / t_max,
         "pose_auc": {"5": auc[0], "10": auc[1], "20": auc[2], "pairs": int(len(e))},
+        "dist": dist_info(world),
         "cpu_baseline": None,
     }
 
@@ -628,7 +667,8 @@ def main(argv=None):
     local = [elapsed, hyps, iters, lo, t_lo, prof["score_ms"], prof["solve_ms"], prof["hypotheses"],
              prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
              prof["sweep_wall_ms"], prof["iterations"], prof["sample_wall_ms"], prof["wait_wall_ms"],
-             prof["run_wall_ms"], prof["lm_blocks"], prof["lm_big_calls"], prof["lm_big_wall_ms"]]
+             prof["run_wall_ms"], prof["lm_blocks"], prof["lm_big_calls"], prof["lm_big_wall_ms"],
+             prof["model_trips"], prof["model_trips_full"], prof["accepted"]]
     allv = gather_counters(local, world)
     allr = gather_records(recs, a.steps, world)
     if rank == 0:

@@ -259,12 +259,22 @@ typedef struct mp_kernel_profile {
     uint64_t lm_blocks;       /* residual blocks over all LM solves         */
     uint64_t lm_big_calls;    /* LM solves with >= 1024 residual blocks     */
     double lm_big_wall_ms;    /* host wall time of those                    */
+    uint64_t model_trips;     /* score_batch: (model, 256-correspondence trip)
+                                 pairs evaluated (early exit stops short)     */
+    uint64_t model_trips_full;/* the same without the early exit            */
+    uint64_t accepted;        /* hypotheses of the iterations the estimator
+                                 consumed (the rest was speculative)          */
 } mp_kernel_profile;
 int mp_profile_enable(int on);
 int mp_profile_reset(void);
 int mp_profile_read(mp_kernel_profile *out);
 
 const char *mp_last_error(void);
+
+/* The host LM pool's spin-before-block in microseconds (engine-internal): the
+ * MADPOSE_LO_SPIN environment value, else 300, or 0 when the process's CPU affinity
+ * share holds fewer than 12 CPUs per rank of LOCAL_WORLD_SIZE. */
+int mp_lo_spin_us(void);
 int mp_device_count(void);
 const char *mp_version(void);
 

@@ -105,6 +105,9 @@ class mp_kernel_profile(ctypes.Structure):
         ("lm_blocks", ctypes.c_uint64),
         ("lm_big_calls", ctypes.c_uint64),
         ("lm_big_wall_ms", ctypes.c_double),
+        ("model_trips", ctypes.c_uint64),
+        ("model_trips_full", ctypes.c_uint64),
+        ("accepted", ctypes.c_uint64),
     ]
 
 
@@ -163,6 +166,7 @@ EXPORTS = {
     "mp_profile_read": (ctypes.c_int, [ctypes.POINTER(mp_kernel_profile)]),
     "mp_last_error": (ctypes.c_char_p, []),
     "mp_device_count": (ctypes.c_int, []),
+    "mp_lo_spin_us": (ctypes.c_int, []),
     "mp_version": (ctypes.c_char_p, []),
 }
 

@@ -435,12 +435,17 @@ int mp_profile_read(mp_kernel_profile *out) {
     out->lm_blocks = p.lm_blocks;
     out->lm_big_calls = p.lm_big_calls;
     out->lm_big_wall_ms = p.lm_big_wall_ms;
+    out->model_trips = p.model_trips;
+    out->model_trips_full = p.model_trips_full;
+    out->accepted = p.accepted;
     return MP_OK;
 }
 
 const char *mp_last_error(void) { return g_last_error.c_str(); }
 
 int mp_device_count(void) { return mp::device_count(); }
+
+int mp_lo_spin_us(void) { return mp::lo_spin_us(); }
 
 const char *mp_version(void) { return "madpose-mi355x 0.1.0 (gfx950)"; }
 

@@ -329,6 +329,7 @@ struct DeviceCtx {
     int *d_samples = nullptr; // a batch's samples + iteration lists (draw_batch layout)
     int *d_counts = nullptr;
     IterResult *d_res = nullptr;
+    int *d_work = nullptr; // score_batch's evaluated (model, trip) pairs per iteration
     Model *d_models = nullptr;
     ScoreRec *d_recs = nullptr;
     double *d_scores = nullptr;
@@ -345,6 +346,7 @@ struct DeviceCtx {
     // pinned host mirrors
     int *h_samples = nullptr; // two slots of 9 * max_batch ints
     IterResult *h_res = nullptr;
+    int *h_work = nullptr;
     double *h_err = nullptr, *h_score1 = nullptr;
     ScoreRec *h_rec1 = nullptr;
     Model *h_model1 = nullptr;
@@ -357,16 +359,17 @@ struct DeviceCtx {
     void free_all() {
         hipSetDevice(device);
         for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_counts,
-                        (void *)d_res, (void *)d_models, (void *)d_recs, (void *)d_scores,
+                        (void *)d_res, (void *)d_work, (void *)d_models, (void *)d_recs, (void *)d_scores,
                         (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_ncand,
                         (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
-        for (void *p : {(void *)h_samples, (void *)h_res, (void *)h_err,
+        for (void *p : {(void *)h_samples, (void *)h_res, (void *)h_work, (void *)h_err,
                         (void *)h_score1, (void *)h_rec1, (void *)h_model1})
             if (p) hipHostFree(p);
         d_pair = d_err = d_scores = d_score1 = nullptr;
         d_samples = d_counts = nullptr;
         d_res = nullptr;
+        d_work = nullptr;
         d_models = nullptr;
         d_recs = d_rec1 = nullptr;
         d_pt_cand = nullptr;
@@ -374,6 +377,7 @@ struct DeviceCtx {
         d_pt_slots = nullptr;
         h_samples = nullptr;
         h_res = nullptr;
+        h_work = nullptr;
         h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
         h_model1 = nullptr;
@@ -393,6 +397,7 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_samples, sizeof(int) * 9 * bb));
         MP_HIP(hipMalloc(&d_counts, sizeof(int) * bb));
         MP_HIP(hipMalloc(&d_res, sizeof(IterResult) * bb));
+        MP_HIP(hipMalloc(&d_work, sizeof(int) * bb));
         MP_HIP(hipMalloc(&d_models, sizeof(Model) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_scores, sizeof(double) * (size_t)bb * mm));
@@ -405,6 +410,7 @@ struct DeviceCtx {
         // two slots each: the next batch is generated while the current one is in flight
         MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 9 * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_res, sizeof(IterResult) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_work, sizeof(int) * bb, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_err, sizeof(double) * 3 * nn, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
@@ -1117,8 +1123,9 @@ class Run {
     // Solves and scores batch g on the GPU (asynchronous, X_.stream): sample upload,
     // MD solver on the side stream, the point-solver stages, score_batch, and the
     // per-iteration best scores / slots / model counts back to pinned host memory.
+    // best: best_min_model_score when the batch starts (the scoring's early exit).
     bool batch_prof_ = false;
-    void launch_batch(const Batch &g) {
+    void launch_batch(const Batch &g, double best) {
         const uint32_t B = g.B;
         const int nmd = g.nmd, npt = g.npt;
         hipStream_t s = X_.stream;
@@ -1142,9 +1149,11 @@ class Run {
                                maxm_));
         if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
         if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
-        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res));
+        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res, best,
+                                  prof ? X_.d_work : nullptr));
         if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
         MP_HIP(hipMemcpyAsync(X_.h_res, X_.d_res, sizeof(IterResult) * B, hipMemcpyDeviceToHost, s));
+        if (prof) MP_HIP(hipMemcpyAsync(X_.h_work, X_.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     }
 
     Model fetch_model(int b, int slot) {
@@ -1251,7 +1260,7 @@ void Run::run(Model *best, Stats *S) {
         auto t_batch = Clock::now();
         const Batch &g = gen[cur];
         const uint32_t B = g.B;
-        if (!launched) launch_batch(g);
+        if (!launched) launch_batch(g, best_min_score);
         launched = false;
         const bool prof = batch_prof_;
         // While the batch is in flight, the sampler thread draws the next one into the
@@ -1274,9 +1283,14 @@ void Run::run(Model *best, Stats *S) {
             float ms_solve = 0.f, ms_score = 0.f;
             MP_HIP(hipEventElapsedTime(&ms_solve, X_.ev[0], X_.ev[1]));
             MP_HIP(hipEventElapsedTime(&ms_score, X_.ev[1], X_.ev[2]));
-            uint64_t h = 0;
-            for (uint32_t q = 0; q < B; ++q) h += (uint64_t)X_.h_res[q].count;
+            uint64_t h = 0, trips = 0;
+            for (uint32_t q = 0; q < B; ++q) {
+                h += (uint64_t)X_.h_res[q].count;
+                trips += (uint64_t)X_.h_work[q];
+            }
             std::lock_guard<std::mutex> lk(g_prof_mu);
+            g_prof.model_trips += trips;
+            g_prof.model_trips_full += h * (uint64_t)((n_ + 255) / 256);
             g_prof.batches += 1;
             g_prof.iterations += B;
             g_prof.hypotheses += h;
@@ -1323,12 +1337,14 @@ void Run::run(Model *best, Stats *S) {
                                     (uint64_t)max_batch_, std::max<uint64_t>((uint64_t)min_batch_, 4ull * at));
                                 const int slot = cur ^ 1;
                                 Batch *gs = &gen[slot];
+                                // LO leaves best_min_model_score alone (src/hybrid_ransac.h:149-155)
+                                const double bound = best_min_score;
                                 X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(slot),
-                                                  [this, gs] {
+                                                  [this, gs, bound] {
                                                       // the sampler thread is not bound to the
                                                       // estimator's device by itself
                                                       MP_HIP(hipSetDevice(X_.device));
-                                                      launch_batch(*gs);
+                                                      launch_batch(*gs, bound);
                                                   });
                                 spec = true;
                                 spec_draws = sel_end.draws();
@@ -1426,6 +1442,7 @@ void Run::run(Model *best, Stats *S) {
         g_prof.sample_wall_ms += 1e3 * sample_s_;
         g_prof.wait_wall_ms += 1e3 * S->seconds_gpu_wait;
         g_prof.run_wall_ms += 1e3 * S->seconds_total;
+        g_prof.accepted += S->num_hypotheses;
     }
 }
 
@@ -1467,6 +1484,19 @@ void estimate_pair(const PairInput &in, const RansacOptions &opts, const Estimat
     }
 }
 
+namespace {
+// device allocation freed on scope exit (error paths included)
+template <class T> struct DevArray {
+    T *p = nullptr;
+    explicit DevArray(size_t n) { MP_HIP(hipMalloc(&p, sizeof(T) * std::max<size_t>(n, 1))); }
+    ~DevArray() {
+        if (p) hipFree(p);
+    }
+    DevArray(const DevArray &) = delete;
+    DevArray &operator=(const DevArray &) = delete;
+};
+} // namespace
+
 void score_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
                   int nm, double *scores, double *errors, int device, double *norm_scale) {
     validate(in, opts);
@@ -1479,30 +1509,45 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
     upload_pair(X, P, &D);
     std::vector<ScoreRec> recs(std::max(nm, 1));
     for (int m = 0; m < nm; ++m) prepare_score_rec(P.C, models[m], recs[m]);
-    ScoreRec *d_recs = nullptr;
-    double *d_sc = nullptr;
-    MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * recs.size()));
-    MP_HIP(hipMalloc(&d_sc, sizeof(double) * recs.size()));
-    MP_HIP(hipMemcpyAsync(d_recs, recs.data(), sizeof(ScoreRec) * nm, hipMemcpyHostToDevice, X.stream));
-    MP_HIP(launch_score_models(X.stream, D, P.C, d_recs, nm, d_sc));
-    MP_HIP(hipMemcpyAsync(scores, d_sc, sizeof(double) * nm, hipMemcpyDeviceToHost, X.stream));
+    DevArray<ScoreRec> d_recs(recs.size());
+    DevArray<double> d_sc(recs.size());
+    MP_HIP(hipMemcpyAsync(d_recs.p, recs.data(), sizeof(ScoreRec) * nm, hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_score_models(X.stream, D, P.C, d_recs.p, nm, d_sc.p));
+    MP_HIP(hipMemcpyAsync(scores, d_sc.p, sizeof(double) * nm, hipMemcpyDeviceToHost, X.stream));
     if (errors) {
         for (int m = 0; m < nm; ++m) {
-            MP_HIP(launch_sweep(X.stream, D, P.C, d_recs + m, X.d_err, X.d_score1));
+            MP_HIP(launch_sweep(X.stream, D, P.C, d_recs.p + m, X.d_err, X.d_score1));
             MP_HIP(hipMemcpyAsync(errors + (size_t)m * 3 * in.n, X.d_err, sizeof(double) * 3 * in.n,
                                   hipMemcpyDeviceToHost, X.stream));
         }
     }
     MP_HIP(hipStreamSynchronize(X.stream));
-    hipFree(d_recs);
-    hipFree(d_sc);
 }
 
-// the same problems through the host LM (host/lm.cpp) -- test hook (mp_debug_lm_refine_host)
+namespace {
+// the problem lists of mp_lm_refine_batch: offsets[0] >= 0, non-decreasing, every
+// index inside the pair (checked once, before either LM touches them)
+void validate_lm_batch(const PairInput &in, int nprob, const int64_t *offsets, const int32_t *idx, const Model *models,
+                       const int32_t *status) {
+    if (nprob < 0) throw std::invalid_argument("negative problem count");
+    if (nprob == 0) return;
+    if (!offsets || !models || !status) throw std::invalid_argument("null offsets, models or status");
+    if (offsets[0] < 0) throw std::invalid_argument("sample offsets must be non-negative");
+    for (int64_t k = 0; k < 3 * (int64_t)nprob; ++k)
+        if (offsets[k + 1] < offsets[k]) throw std::invalid_argument("sample offsets must not decrease");
+    if (offsets[3 * (int64_t)nprob] > offsets[0] && !idx) throw std::invalid_argument("null index list");
+    for (int64_t k = offsets[0]; k < offsets[3 * (int64_t)nprob]; ++k)
+        if (idx[k] < 0 || idx[k] >= in.n) throw std::invalid_argument("sample index out of range");
+}
+} // namespace
+
+// the same problems through the host LM (host/lm.cpp) -- test hook (mp_debug_lm_refine_host);
+// kinds may be NULL (every problem a LeastSquares call)
 void lm_refine_batch_host(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nprob,
                           const int32_t *kinds, const int64_t *offsets, const int32_t *idx, Model *models,
                           int32_t *status) {
     validate(in, opts);
+    validate_lm_batch(in, nprob, offsets, idx, models, status);
     Problem P = make_problem(in, opts, cfg);
     const int v = P.C.variant;
     const int kmd = v == kCal ? 3 : 4, kpt = v == kCal ? 5 : (v == kSF ? 6 : 7);
@@ -1537,6 +1582,7 @@ void lm_refine_batch_device(const PairInput &in, const RansacOptions &opts, cons
                             const int32_t *kinds, const int64_t *offsets, const int32_t *idx, Model *models,
                             int32_t *status, int device) {
     validate(in, opts);
+    validate_lm_batch(in, nprob, offsets, idx, models, status);
     if (nprob <= 0) return;
     CtxLease lease(device);
     DeviceCtx &X = *lease.c;
@@ -1550,13 +1596,7 @@ void lm_refine_batch_device(const PairInput &in, const RansacOptions &opts, cons
     std::vector<int> which;
     for (int j = 0; j < nprob; ++j) {
         int sz[3];
-        for (int t = 0; t < 3; ++t) {
-            const int64_t a = offsets[3 * j + t], b = offsets[3 * j + t + 1];
-            if (b < a) throw std::invalid_argument("sample offsets must not decrease");
-            sz[t] = (int)(b - a);
-            for (int64_t k = a; k < b; ++k)
-                if (idx[k] < 0 || idx[k] >= in.n) throw std::invalid_argument("sample index out of range");
-        }
+        for (int t = 0; t < 3; ++t) sz[t] = (int)(offsets[3 * j + t + 1] - offsets[3 * j + t]);
         // too few data for the solver (the size test of least_squares)
         if ((sz[0] < kmd && sz[1] < kmd) || sz[2] < kpt) {
             status[j] = 3;
@@ -1567,26 +1607,21 @@ void lm_refine_batch_device(const PairInput &in, const RansacOptions &opts, cons
     }
     if (jobs.empty()) return;
     const int64_t nidx = offsets[3 * nprob];
-    LmJob *d_jobs;
-    int *d_idx, *d_status;
-    Model *d_out;
-    MP_HIP(hipMalloc(&d_jobs, sizeof(LmJob) * jobs.size()));
-    MP_HIP(hipMalloc(&d_idx, sizeof(int) * (size_t)std::max<int64_t>(nidx, 1)));
-    MP_HIP(hipMalloc(&d_status, sizeof(int) * jobs.size()));
-    MP_HIP(hipMalloc(&d_out, sizeof(Model) * jobs.size()));
-    MP_HIP(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(LmJob) * jobs.size(), hipMemcpyHostToDevice, X.stream));
-    if (nidx > 0) MP_HIP(hipMemcpyAsync(d_idx, idx, sizeof(int) * nidx, hipMemcpyHostToDevice, X.stream));
-    MP_HIP(launch_lm_batch(X.stream, D, P.C, d_jobs, (int)jobs.size(), d_idx, d_out, d_status));
+    DevArray<LmJob> d_jobs(jobs.size());
+    DevArray<int> d_idx((size_t)nidx), d_status(jobs.size());
+    DevArray<Model> d_out(jobs.size());
+    MP_HIP(hipMemcpyAsync(d_jobs.p, jobs.data(), sizeof(LmJob) * jobs.size(), hipMemcpyHostToDevice, X.stream));
+    if (nidx > 0) MP_HIP(hipMemcpyAsync(d_idx.p, idx, sizeof(int) * nidx, hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_lm_batch(X.stream, D, P.C, d_jobs.p, (int)jobs.size(), d_idx.p, d_out.p, d_status.p));
     std::vector<Model> out(jobs.size());
     std::vector<int> st(jobs.size());
-    MP_HIP(hipMemcpyAsync(out.data(), d_out, sizeof(Model) * out.size(), hipMemcpyDeviceToHost, X.stream));
-    MP_HIP(hipMemcpyAsync(st.data(), d_status, sizeof(int) * st.size(), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(out.data(), d_out.p, sizeof(Model) * out.size(), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(st.data(), d_status.p, sizeof(int) * st.size(), hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));
     for (size_t k = 0; k < which.size(); ++k) {
         models[which[k]] = out[k];
         status[which[k]] = st[k];
     }
-    for (void *q : {(void *)d_jobs, (void *)d_idx, (void *)d_status, (void *)d_out}) hipFree(q);
 }
 
 int solve_md_direct(int variant, const double *x, const double *y, const double *dx, const double *dy, double *sols,

@@ -123,6 +123,9 @@ struct KernelProfile {
     uint64_t lm_blocks = 0;        // residual blocks over all LM solves
     uint64_t lm_big_calls = 0;     // LM solves with >= kBigLM residual blocks
     double lm_big_wall_ms = 0.0;   // host wall time of those
+    uint64_t model_trips = 0;      // score_batch (model, 256-correspondence trip) pairs evaluated
+    uint64_t model_trips_full = 0; // ... and without the early exit (models x trips)
+    uint64_t accepted = 0;         // hypotheses of the iterations the estimator consumed
 };
 constexpr size_t kBigLM = 1024;
 void profile_enable(bool on);

@@ -40,6 +40,10 @@ struct LMSettings {
 // Solve() returning false); m is left unchanged in that case.
 bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettings &S, Model *m);
 
+// the LM pool's spin before blocking, in microseconds (MADPOSE_LO_SPIN, or the
+// affinity-based default of lm.cpp)
+int lo_spin_us();
+
 // quaternion helpers (w, x, y, z) -- Eigen::Quaternion(Matrix3) / toRotationMatrix
 void rot_to_quat(const double *R, double *q);
 void quat_to_rot(const double *q, double *R);

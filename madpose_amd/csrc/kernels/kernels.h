@@ -29,8 +29,13 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                            int maxm);
 // scoring sweep: one workgroup per iteration, every model of the iteration scored
 // over all correspondences; per-iteration argmin (first minimum wins) into res[b].
+// best: the best minimal-model score before the batch (DBL_MAX: none yet); a model
+// whose partial MSAC sum exceeds it cannot win and is dropped early (exact early
+// exit, kernels.hip ScoreBound), reporting DBL_MAX.  work (nullable): per iteration
+// the (model, 256-correspondence trip) pairs evaluated.
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
-                              const int *counts, int nb, int maxm, double *scores, IterResult *res);
+                              const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
+                              int *work);
 // single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);

@@ -17,6 +17,8 @@
 //                     to pinned host memory, one completion flag per workgroup
 #include <cfloat>
 #include <cstdlib>
+#include <cstring>
+#include <algorithm>
 
 #include "../include/mp_md_alt.h"
 #include "../include/mp_score.h"
@@ -32,10 +34,22 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// Sum over the 64 lanes of a wave (all lanes active), returned uniformly: DPP
+// butterflies inside each 16-lane row (every lane of a row ends with the same row
+// sum), then the four row sums read out by v_readlane and added in a fixed order --
+// no LDS permutes (ds_bpermute) and no lane-index arithmetic; deterministic.
 __device__ inline double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += dpp_d<dpp::kXor1>(v);
+    v += dpp_d<dpp::kXor2>(v);
+    v += dpp_d<dpp::kHalfMirror>(v);
+    v += dpp_d<dpp::kMirror>(v);
+    const long long bits = __double_as_longlong(v);
+    const int lo = (int)(bits & 0xffffffffLL), hi = (int)(bits >> 32);
+    auto row = [&](int l) {
+        const unsigned a = (unsigned)__builtin_amdgcn_readlane(lo, l), b = (unsigned)__builtin_amdgcn_readlane(hi, l);
+        return __longlong_as_double((long long)(((unsigned long long)b << 32) | a));
+    };
+    return (row(0) + row(16)) + (row(32) + row(48));
 }
 
 __device__ inline Corr load_corr(const PairConst &C, const PairData &D, int i, bool cal) {
@@ -503,15 +517,39 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
 // FAST: score_type 0 (hybrid, no gating) and not scale-only, and for the calibrated
 // variant intrinsics of the kstd shape (ray form, mp_score.h eval_corr_cal_ray);
 // everything else takes the general path (runtime gating, matrix form).
-template <int V, int MAXM, bool FAST>
+// Exact early exit (ScoreBound): `cut` is the best minimal-model score before the
+// batch (best_min_model_score of src/hybrid_ransac.h:74, 123-131), widened by a
+// relative 1e-12.  An iteration's best score is only ever compared with the running
+// best by a strict '<' (:123), the running best only decreases inside a batch, and
+// every MSAC term min(e, thr) * w is >= 0 -- so a model whose partial sum already
+// exceeds `cut` can never win, and the rest of its sweep is skipped.  The margin
+// keeps the decision away from the last-bit differences between this sum and the
+// reference's sequential one.  Checks run at trip boundaries (one trip = 256
+// correspondences): each live model's workgroup partial (wave sums, then the four
+// waves in LDS in a fixed order -- every lane forms the same value, so the live mask
+// stays uniform) is compared with `cut`; the workgroup leaves once no model is live.
+// Killed models report DBL_MAX and never enter the argmin; a model that could win is
+// never killed, so the winner and its score are those of the full sweep.
+struct ScoreBound {
+    double cut;          // +inf: no early exit
+    int first, every;    // first check after `first` trips, then every `every` trips
+    int *work;           // per iteration: (model, trip) pairs evaluated (profiling)
+};
+
+// EXIT = false (no finite bound yet, or MADPOSE_SCORE_EXIT=0): the plain sweep,
+// without the trip-boundary checks and their barriers.
+template <int V, int MAXM, bool FAST, bool EXIT>
 __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairConst C,
                                                              const ScoreRec *__restrict__ recs,
                                                              const int *__restrict__ counts, double *scores,
-                                                             IterResult *res) {
+                                                             IterResult *res, ScoreBound sb) {
     const int b = blockIdx.x;
     const int nm = counts[b];
     if (nm == 0) {
-        if (threadIdx.x == 0) res[b] = IterResult{DBL_MAX, 0, 0};
+        if (threadIdx.x == 0) {
+            res[b] = IterResult{DBL_MAX, 0, 0};
+            if (sb.work) sb.work[b] = 0;
+        }
         return;
     }
     const ScoreRec *R = recs + (size_t)b * MAXM;
@@ -521,27 +559,77 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     const double t0 = C.thr[0], t1 = C.thr[1], t2 = C.thr[2];
     const double w0 = C.w[0], w1 = C.w[1], w2 = C.w[2];
     const double tw0 = t0 * w0, tw1 = t1 * w1, tw2 = t2 * w2;
-    for (int i = threadIdx.x; i < C.n; i += kBlock) {
-        const Corr p = load_corr(C, D, i, V == kCal);
+    __shared__ double part[2][kBlock / 64][MAXM];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned live = (nm >= 32) ? ~0u : ((1u << nm) - 1u); // uniform
+    int checks = 0, work = 0;
+    const int ntrip = (C.n + kBlock - 1) / kBlock;
+    if (!EXIT) {
+        for (int i = threadIdx.x; i < C.n; i += kBlock) {
+            const Corr p = load_corr(C, D, i, V == kCal);
 #pragma unroll
-        for (int m = 0; m < MAXM; ++m) {
-            if (m < nm) {
-                double e0, e1, e2;
-                if (FAST && V == kCal)
-                    eval_corr_cal_ray(C, R[m], p, e0, e1, e2);
-                else
-                    eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2);
-                acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
+            for (int m = 0; m < MAXM; ++m) {
+                if (m < nm) {
+                    double e0, e1, e2;
+                    if (FAST && V == kCal)
+                        eval_corr_cal_ray(C, R[m], p, e0, e1, e2);
+                    else
+                        eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2);
+                    acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
+                }
             }
         }
+        work = nm * ntrip;
     }
-    __shared__ double part[kBlock / 64][MAXM];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int trip = 0; EXIT && trip < ntrip; ++trip) {
+        const int i = trip * kBlock + threadIdx.x;
+        if (i < C.n) {
+            const Corr p = load_corr(C, D, i, V == kCal);
+#pragma unroll
+            for (int m = 0; m < MAXM; ++m) {
+                if ((live >> m) & 1u) {
+                    double e0, e1, e2;
+                    if (FAST && V == kCal)
+                        eval_corr_cal_ray(C, R[m], p, e0, e1, e2);
+                    else
+                        eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2);
+                    acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
+                }
+            }
+        }
+        work += __popc(live);
+        const int done = trip + 1;
+        if (done < ntrip && done >= sb.first && (done - sb.first) % sb.every == 0) {
+            const int par = checks & 1; // double-buffered: one barrier per check
+#pragma unroll
+            for (int m = 0; m < MAXM; ++m) {
+                if ((live >> m) & 1u) {
+                    const double v = wave_sum(acc[m]);
+                    if (lane == 0) part[par][wave][m] = v;
+                }
+            }
+            __syncthreads();
+            unsigned keep = live;
+#pragma unroll
+            for (int m = 0; m < MAXM; ++m) {
+                if ((live >> m) & 1u) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int w = 0; w < kBlock / 64; ++w) v += part[par][w][m];
+                    if (v > sb.cut) keep &= ~(1u << m);
+                }
+            }
+            live = __builtin_amdgcn_readfirstlane(keep);
+            ++checks;
+            if (live == 0) break;
+        }
+    }
+    const int par = checks & 1;
 #pragma unroll
     for (int m = 0; m < MAXM; ++m) {
-        if (m < nm) {
+        if ((live >> m) & 1u) {
             const double v = wave_sum(acc[m]);
-            if (lane == 0) part[wave][m] = v;
+            if (lane == 0) part[par][wave][m] = v;
         }
     }
     __syncthreads();
@@ -549,9 +637,12 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         double bs = DBL_MAX;
         int bi = 0;
         for (int m = 0; m < nm; ++m) {
-            double v = 0.0;
+            double v = DBL_MAX; // killed: cannot win
+            if ((live >> m) & 1u) {
+                v = 0.0;
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) v += part[w][m];
+                for (int w = 0; w < kBlock / 64; ++w) v += part[par][w][m];
+            }
             scores[(size_t)b * MAXM + m] = v;
             if (v < bs) { // strict '<': first minimum wins (src/hybrid_ransac.h:258)
                 bs = v;
@@ -559,6 +650,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
             }
         }
         res[b] = IterResult{bs, bi, nm};
+        if (sb.work) sb.work[b] = work;
     }
 }
 
@@ -924,26 +1016,68 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
     });
 }
 
+// Early-exit schedule (MADPOSE_SCORE_EXIT=0 turns the exit off; MADPOSE_SCORE_CHECK
+// "first,every" in trips of 256 correspondences overrides the schedule).
+static ScoreBound score_bound(double best, int n, int *work) {
+    static const int mode = [] {
+        const char *e = std::getenv("MADPOSE_SCORE_EXIT");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    static const int sched[2] = {[] {
+                                     const char *e = std::getenv("MADPOSE_SCORE_CHECK");
+                                     return e ? std::max(1, std::atoi(e)) : 0;
+                                 }(),
+                                 [] {
+                                     const char *e = std::getenv("MADPOSE_SCORE_CHECK");
+                                     const char *c = e ? std::strchr(e, ',') : nullptr;
+                                     return c ? std::max(1, std::atoi(c + 1)) : 1;
+                                 }()};
+    ScoreBound sb;
+    const bool on = mode != 0 && best < DBL_MAX && best >= 0.0;
+    sb.cut = on ? best * (1.0 + 1e-12) : __builtin_inf();
+    const int ntrip = (n + kBlock - 1) / kBlock;
+    // default: first check after a quarter of the trips, then every quarter (each
+    // check costs a wave reduction per live model and a barrier; tools/score_bench.hip:
+    // at N = 2000 checks after trips 2, 4, 6 beat every trip from 2 on, 209 vs 233 us)
+    sb.first = sched[0] > 0 ? sched[0] : std::max(1, ntrip / 4);
+    sb.every = sched[0] > 0 ? sched[1] : std::max(1, ntrip / 4);
+    sb.work = work;
+    return sb;
+}
+
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
-                              const int *counts, int nb, int maxm, double *scores, IterResult *res) {
+                              const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
+                              int *work) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
     const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
+    const ScoreBound sb = score_bound(best, C.n, work);
+    const bool exit = sb.cut < __builtin_inf();
+    auto go = [&](auto V, auto M, auto F) {
+        constexpr int kV = decltype(V)::value, kM = decltype(M)::value;
+        constexpr bool kF = decltype(F)::value;
+        if (exit)
+            score_batch_kernel<kV, kM, kF, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res, sb);
+        else
+            score_batch_kernel<kV, kM, kF, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res, sb);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
     if (C.variant == kCal) {
         if (fast)
-            score_batch_kernel<kCal, kMaxModelsCal, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+            go(std::integral_constant<int, kCal>(), std::integral_constant<int, kMaxModelsCal>(), T());
         else
-            score_batch_kernel<kCal, kMaxModelsCal, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+            go(std::integral_constant<int, kCal>(), std::integral_constant<int, kMaxModelsCal>(), F());
     } else if (C.variant == kSF) {
         if (fast)
-            score_batch_kernel<kSF, kMaxModelsSF, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+            go(std::integral_constant<int, kSF>(), std::integral_constant<int, kMaxModelsSF>(), T());
         else
-            score_batch_kernel<kSF, kMaxModelsSF, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+            go(std::integral_constant<int, kSF>(), std::integral_constant<int, kMaxModelsSF>(), F());
     } else {
         if (fast)
-            score_batch_kernel<kTF, kMaxModelsTF, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+            go(std::integral_constant<int, kTF>(), std::integral_constant<int, kMaxModelsTF>(), T());
         else
-            score_batch_kernel<kTF, kMaxModelsTF, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res);
+            go(std::integral_constant<int, kTF>(), std::integral_constant<int, kMaxModelsTF>(), F());
     }
     return hipGetLastError();
 }

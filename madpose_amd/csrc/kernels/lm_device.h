@@ -431,7 +431,11 @@ template <int NA> struct LmShared {
     int has_lo[kLNFull];
     int col[kLNFull];
     int cur;
-    int action; // 0 stop, 1 evaluate the candidate sh.c, 2 propose a step
+    int action; // decision after an evaluation: 0 stop, 2 propose a step
+    int prop;   // proposal: 0 stop, 1 evaluate the candidate sh.c
+    // (two words: every wave reads `action` at the top of the loop while lane 0 is
+    // already writing the proposal; each word is rewritten only behind a barrier that
+    // all of its readers have passed)
 };
 
 __device__ inline int lm_up(int a, int b, int na) { return a * na - a * (a - 1) / 2 + (b - a); } // a <= b
@@ -646,7 +650,7 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
         if (t0) {
             // propose a step from x (repeated while the damped system is not positive definite)
             const double *R = sh.red[sh.cur];
-            sh.action = 0;
+            int prop = 0;
             while (iter < J.max_iter) {
                 ++iter;
                 double d[NA];
@@ -696,12 +700,13 @@ __global__ void __launch_bounds__(kLmBlock) lm_batch_kernel(PairData D, PairCons
                 }
                 if (sqrt(step2) <= J.ptol * (sqrt(lm_amb_norm2(x)) + J.ptol)) break; // parameter tolerance
                 sh.c = c;
-                sh.action = 1;
+                prop = 1;
                 break;
             }
+            sh.prop = prop;
         }
         __syncthreads();
-        if (sh.action == 0) break;
+        if (sh.prop == 0) break;
         lm_evaluate<V, NA>(D, C, J, idx, sh.c, sh, sh.red[sh.cur ^ 1]);
         if (t0) {
             const double *R = sh.red[sh.cur], *Rc = sh.red[sh.cur ^ 1];
