@@ -336,7 +336,7 @@ struct DeviceCtx {
     ScoreRec *d_rec1 = nullptr;
     double *d_err = nullptr, *d_score1 = nullptr;
     // staged point-solver workspace (kernels.h PtWorkspace)
-    double *d_pt_cand = nullptr;
+    double *d_pt_cand = nullptr, *d_pt_pen = nullptr;
     int *d_pt_ncand = nullptr, *d_pt_valid = nullptr;
     Model *d_pt_slots = nullptr;
     // LO sweep issuers: slot 0 on `stream` (the estimator thread), slots 1.. with
@@ -360,7 +360,7 @@ struct DeviceCtx {
         hipSetDevice(device);
         for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_counts,
                         (void *)d_res, (void *)d_work, (void *)d_models, (void *)d_recs, (void *)d_scores,
-                        (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_ncand,
+                        (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_pen, (void *)d_pt_ncand,
                         (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
         for (void *p : {(void *)h_samples, (void *)h_res, (void *)h_work, (void *)h_err,
@@ -372,7 +372,7 @@ struct DeviceCtx {
         d_work = nullptr;
         d_models = nullptr;
         d_recs = d_rec1 = nullptr;
-        d_pt_cand = nullptr;
+        d_pt_cand = d_pt_pen = nullptr;
         d_pt_ncand = d_pt_valid = nullptr;
         d_pt_slots = nullptr;
         h_samples = nullptr;
@@ -403,6 +403,8 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_scores, sizeof(double) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_rec1, sizeof(ScoreRec) * 64));
         MP_HIP(hipMalloc(&d_pt_cand, sizeof(double) * (size_t)bb * kPtCandStride));
+        // (the pencil workspace of the shared-focal root stage; a stub elsewhere)
+        MP_HIP(hipMalloc(&d_pt_pen, sizeof(double) * (mm == kMaxModelsSF ? (size_t)bb * kPtPenStride : 1)));
         MP_HIP(hipMalloc(&d_pt_ncand, sizeof(int) * (size_t)bb));
         MP_HIP(hipMalloc(&d_pt_valid, sizeof(int) * (size_t)bb * kPtSlotStride));
         MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb * kPtSlotStride));
@@ -1144,7 +1146,7 @@ class Run {
                                    X_.d_counts, maxm_));
             MP_HIP(hipEventRecord(X_.ev_join, X_.md_stream));
         }
-        const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid};
+        const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen};
         MP_HIP(launch_pt_solve(s, D_, P_.C, d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
                                maxm_));
         if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
@@ -1664,6 +1666,33 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
 
 int solve_point_direct(int kind, const double *x1, const double *x2, Model *poses, int max_poses, int device) {
     if (kind < 0 || kind > 2) throw std::invalid_argument("point solver kind must be 0, 1 or 2");
+    if (kind == 1 && !pt6_dft()) {
+        // the estimator's root stage (deflated eigenproblem) on this one sample, then
+        // its poses
+        double cand[kPtCandStride];
+        int nc = 0;
+        debug_pt_roots(kSF, 3, 1, x1, x2, cand, &nc, device);
+        CtxLease lease(device);
+        DeviceCtx &X = *lease.c;
+        double in[24];
+        std::memcpy(in, x1, sizeof(double) * 12);
+        std::memcpy(in + 12, x2, sizeof(double) * 12);
+        constexpr int kCap = 16;
+        DevArray<double> d_in(24), d_cand(kPtCandStride);
+        DevArray<int> d_nc(1), d_n(1);
+        DevArray<Model> d_poses(kCap);
+        MP_HIP(hipMemcpyAsync(d_in.p, in, sizeof(in), hipMemcpyHostToDevice, X.stream));
+        MP_HIP(hipMemcpyAsync(d_cand.p, cand, sizeof(cand), hipMemcpyHostToDevice, X.stream));
+        MP_HIP(hipMemcpyAsync(d_nc.p, &nc, sizeof(int), hipMemcpyHostToDevice, X.stream));
+        MP_HIP(launch_point_direct_6pt(X.stream, d_in.p, d_cand.p, d_nc.p, d_poses.p, d_n.p));
+        int hn = 0;
+        Model hp[kCap];
+        MP_HIP(hipMemcpyAsync(&hn, d_n.p, sizeof(int), hipMemcpyDeviceToHost, X.stream));
+        MP_HIP(hipMemcpyAsync(hp, d_poses.p, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
+        MP_HIP(hipStreamSynchronize(X.stream));
+        for (int i = 0; i < std::min(std::min(hn, kCap), max_poses); ++i) poses[i] = hp[i];
+        return hn;
+    }
     CtxLease lease(device);
     DeviceCtx &X = *lease.c;
     const int per = kind == 0 ? 15 : (kind == 1 ? 12 : 14);
@@ -1693,8 +1722,8 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
 
 void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
                     int *ncand, int device) {
-    if (impl < 0 || impl > (variant == 1 ? 2 : 1))
-        throw std::invalid_argument("impl must be 0 (lane), 1 (group) or, for the 6-point, 2 (wave)");
+    if (impl < 0 || impl > (variant == 1 ? 3 : 1))
+        throw std::invalid_argument("impl must be 0 (lane), 1 (group) or, for the 6-point, 2 (wave) or 3 (eigen)");
     if (variant != kCal && variant != kSF) throw std::invalid_argument("variant must be 0 (5pt) or 1 (6pt)");
     if (ns <= 0 || ns > (1 << 22)) throw std::invalid_argument("bad number of samples");
     CtxLease lease(device);
@@ -1734,7 +1763,8 @@ void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const
     C.variant = variant;
     C.n = (int)np;
     for (int k = 0; k < 9; ++k) C.K0[k] = C.K1[k] = C.K0i[k] = C.K1i[k] = (k % 4 == 0) ? 1.0 : 0.0;
-    MP_HIP(launch_pt_roots(X.stream, D, C, d_list, (int)ns, d_smp, d_cand, d_n, impl));
+    DevArray<double> d_pen(impl == 3 ? (size_t)ns * kPtPenStride : 1);
+    MP_HIP(launch_pt_roots(X.stream, D, C, d_list, (int)ns, d_smp, d_cand, d_n, impl, d_pen.p));
     MP_HIP(hipMemcpyAsync(cand, d_cand, sizeof(double) * kPtCandStride * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipMemcpyAsync(ncand, d_n, sizeof(int) * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));

@@ -888,6 +888,9 @@ MP_HD int sixpt_poses_for_root(const double (&M)[3][10][10], const double (&N)[3
     return added;
 }
 
+MP_HD int sixpt_poses_for_roots(const double (&M)[3][10][10], const double (&N)[3][9], const double *roots, int nr,
+                                const double (&x1)[6][3], const double (&x2)[6][3], Model *out, int kmax);
+
 // kStop < 4 truncates the solver after stage kStop (tools/solver_bench.hip timing).
 template <int kStop = 4>
 MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Model *out, int kmax) {
@@ -900,6 +903,13 @@ MP_HD int relpose_6pt_sf(const double (&x1)[6][3], const double (&x2)[6][3], Mod
     double roots[15];
     const int nr = sixpt_roots(M, roots);
     if (kStop <= 2) return nr;
+    return sixpt_poses_for_roots(M, N, roots, nr, x1, x2, out, kmax);
+}
+
+// Poses of the roots u of one sample (the stage after the root finder), duplicates
+// dropped; N, M: the sample's null space and pencil.
+MP_HD int sixpt_poses_for_roots(const double (&M)[3][10][10], const double (&N)[3][9], const double *roots, int nr,
+                                const double (&x1)[6][3], const double (&x2)[6][3], Model *out, int kmax) {
     int nout = 0;
     for (int k = 0; k < nr; ++k) nout += sixpt_poses_for_root(M, N, roots[k], x1, x2, out, nout, kmax);
     // two roots that the polish took to the same solution give the same pose twice:

@@ -17,11 +17,13 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
 // Workspace of the staged point solvers (per point sample: candidate roots and model
 // slots).  cand: kPtCandStride doubles, slots / valid: kPtSlotStride entries.
 constexpr int kPtCandStride = 96, kPtSlotStride = 32;
+constexpr int kPtPenStride = 300; // shared focal: the 3 x 10 x 10 pencil of a sample (eig6.h)
 struct PtWorkspace {
     double *cand;
     int *ncand;
     Model *slots;
     int *valid;
+    double *pen; // kPtPenStride doubles per point sample (shared focal)
 };
 // point minimal solver over the listed iterations (three launches, see kernels.hip).
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
@@ -40,10 +42,11 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);
 // point-solver root stage alone, C.variant kCal (5pt) or kSF (6pt); impl 0: lane
-// per sample, 1: 16-lane groups.  cand: kPtCandStride doubles per sample (cal: 9 per
+// per sample, 1: 16-lane groups, (6pt) 2: DFT nodes over a wave, 3: deflated
+// eigenproblem, one wave per sample (the estimator's default).  cand: kPtCandStride doubles per sample (cal: 9 per
 // essential matrix; sf: null-space basis N (27), then the positive roots u)
 hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                           const int *samples, double *cand, int *ncand, int impl);
+                           const int *samples, double *cand, int *ncand, int impl, double *pen = nullptr);
 // the single-model sweep writing straight to host-mapped memory: out[0, 3n) the errors,
 // out[3n + W b + w] the partial score of wave w of workgroup b (W =
 // sweep_waves_per_block()), flags[b] = seq (system scope) once workgroup b is done,
@@ -61,6 +64,13 @@ hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst
 hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *in /* x(3K) y(3K) dx(K) dy(K) */,
                             double *sols, int *nsols, Model *poses, int *nposes);
 hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes);
+// shared-focal 6pt poses from a root stage's output (cand: null space + roots of one
+// sample, ncand: root count); in: the 6 + 6 normalized 2-D points
+hipError_t launch_point_direct_6pt(hipStream_t s, const double *in, const double *cand, const int *ncand,
+                                   Model *poses, int *nposes);
+// MADPOSE_PT6_DFT=1: the shared-focal root stage by DFT + Sturm (A/B) instead of the
+// deflated eigenproblem
+bool pt6_dft();
 
 // batched device LM: one workgroup per job; out[j] the refined model, status[j] 1
 // refined, 0 no residuals, 2 infeasible constant block (unchanged)

@@ -25,6 +25,7 @@
 #include "group_5pt.h"
 #include "group_6pt.h"
 #include "group_tail.h"
+#include "eig6.h"
 #include "lm_device.h"
 #include "kernels.h"
 
@@ -958,6 +959,14 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
     });
 }
 
+bool pt6_dft() {
+    static const bool v = [] {
+        const char *e = std::getenv("MADPOSE_PT6_DFT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
                            int maxm) {
@@ -974,7 +983,15 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
         // (pt_roots6_wave_kernel, A/B: 399 vs 291 us per launch for the group kernel at
         // the shared-focal batch sizes -- four times the waves, throughput-bound)
         static const bool wave6 = std::getenv("MADPOSE_PT6_WAVE") != nullptr;
-        if (v == kCal && !lane5)
+        // shared focal default: the deflated eigenproblem (eig6.h); MADPOSE_PT6_DFT=1
+        // keeps the DFT + Sturm kernels above (A/B; they lose roots)
+        static const bool dft6 = pt6_dft();
+        if (v == kSF && !dft6) {
+            pt_pencil6_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, list, nlist, samples, W.cand,
+                                                                                 kCandStride, W.pen);
+            pt_defl6_kernel<<<nlist, 64, 0, s>>>(W.pen, false);
+            pt_eig6_kernel<<<nlist, 64, 0, s>>>(W.pen, W.cand, W.ncand, kCandStride);
+        } else if (v == kCal && !lane5)
             pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                           kCandStride);
         else if (v == kSF && !lane6 && wave6)
@@ -1083,7 +1100,7 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
 }
 
 hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                           const int *samples, double *cand, int *ncand, int impl) {
+                           const int *samples, double *cand, int *ncand, int impl, double *pen) {
     if (nlist <= 0) return hipSuccess;
     const int ggrid = (nlist + kGrpPerWg - 1) / kGrpPerWg, lgrid = (nlist + 63) / 64;
     if (C.variant == kCal) {
@@ -1096,6 +1113,13 @@ hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C,
             pt_roots6_group_kernel<<<ggrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
         else if (impl == 2)
             pt_roots6_wave_kernel<<<nlist, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
+        else if (impl == 3 && pen) {
+            pt_pencil6_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, list, nlist, samples, cand,
+                                                                                 kCandStride, pen);
+            pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, false);
+            pt_eig6_kernel<<<nlist, 64, 0, s>>>(pen, cand, ncand, kCandStride);
+        } else if (impl == 3)
+            return hipErrorInvalidValue;
         else
             pt_roots_kernel<kSF><<<lgrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
     } else {
@@ -1322,6 +1346,34 @@ hipError_t launch_pose_auc(hipStream_t s, int64_t k, const double *e, double *so
 
 hipError_t launch_scale_and_pose(hipStream_t s, const double *in, int64_t n, Model *out) {
     scale_and_pose_kernel<<<1, 64, 0, s>>>(in, n, out);
+    return hipGetLastError();
+}
+
+// the poses of a shared-focal 6-point sample from the root stage's output (null space
+// and roots in cand, as written by pt_roots6_eig_kernel); one lane
+__global__ void point_direct_6pt_kernel(const double *in, const double *cand, const int *ncand, Model *poses,
+                                        int *nposes) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double b0[6][3], b1[6][3];
+    for (int j = 0; j < 6; ++j) {
+        const double a[3] = {in[2 * j], in[2 * j + 1], 1.0}, c[3] = {in[12 + 2 * j], in[12 + 2 * j + 1], 1.0};
+        const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
+        for (int q = 0; q < 3; ++q) {
+            b0[j][q] = a[q] * na;
+            b1[j][q] = c[q] * nc;
+        }
+    }
+    double N[3][9];
+    for (int e = 0; e < 27; ++e) N[e / 9][e % 9] = cand[e];
+    double M[3][10][10];
+    sixpt_matrices(N, M);
+    const int nr = ncand[0] < 15 ? ncand[0] : 15;
+    *nposes = sixpt_poses_for_roots(M, N, cand + 27, nr, b0, b1, poses, kMaxModelsSF);
+}
+
+hipError_t launch_point_direct_6pt(hipStream_t s, const double *in, const double *cand, const int *ncand,
+                                   Model *poses, int *nposes) {
+    point_direct_6pt_kernel<<<1, 64, 0, s>>>(in, cand, ncand, poses, nposes);
     return hipGetLastError();
 }
 

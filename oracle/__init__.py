@@ -150,6 +150,13 @@ def relpose_5pt(b1, b2):
     return [model_to_dict(out[i]) for i in range(min(n, 32))]
 
 
+def sixpt_roots(b1, b2):
+    """Root stage of the 6pt restatement: positive real u = f^2 (deflated companion)."""
+    out = np.zeros(32)
+    n = lib().oracle_6pt_roots(_dp(_c(b1)), _dp(_c(b2)), _dp(out), 32)
+    return np.sort(out[:n])
+
+
 def relpose_6pt_shared_focal(b1, b2):
     """PoseLib relpose_6pt_shared_focal restatement: list of dicts (focal in focal0)."""
     out = (OrModel * 64)()

@@ -156,6 +156,12 @@ int oracle_recover_pose(const double *E, const double *p0, const double *p1, int
     return oracle::recover_pose(E, p0, p1, n, thresh, R, t);
 }
 
+int oracle_6pt_roots(const double *x1, const double *x2, double *out, int max_out) {
+    const auto r = oracle::sixpt_roots_of(x1, x2);
+    for (int k = 0; k < (int)r.size() && k < max_out; ++k) out[k] = r[k];
+    return (int)r.size();
+}
+
 int oracle_relpose_6pt(const double *x1, const double *x2, or_model *out, int max_out) {
     auto sols = oracle::relpose_6pt_shared_focal(x1, x2);
     int n = std::min((int)sols.size(), max_out);

@@ -107,6 +107,117 @@ static void lu_full(Mat &A, std::vector<int> &rp, std::vector<int> &cp) {
     }
 }
 
+void lu_full_steps(Mat &A, std::vector<int> &rp, std::vector<int> &cp, int steps) {
+    const int n = A.r, m = A.c;
+    rp.resize(n);
+    cp.resize(m);
+    for (int i = 0; i < n; ++i) rp[i] = i;
+    for (int j = 0; j < m; ++j) cp[j] = j;
+    for (int k = 0; k < steps; ++k) {
+        int pi = k, pj = k;
+        double best = -1;
+        for (int i = k; i < n; ++i)
+            for (int j = k; j < m; ++j)
+                if (std::fabs(A(i, j)) > best) {
+                    best = std::fabs(A(i, j));
+                    pi = i;
+                    pj = j;
+                }
+        if (pi != k) {
+            for (int j = 0; j < m; ++j) std::swap(A(k, j), A(pi, j));
+            std::swap(rp[k], rp[pi]);
+        }
+        if (pj != k) {
+            for (int i = 0; i < n; ++i) std::swap(A(i, k), A(i, pj));
+            std::swap(cp[k], cp[pj]);
+        }
+        if (A(k, k) == 0.0) continue;
+        for (int i = k + 1; i < n; ++i) {
+            double l = A(i, k) / A(k, k);
+            A(i, k) = l;
+            for (int j = k + 1; j < m; ++j) A(i, j) -= l * A(k, j);
+        }
+    }
+}
+
+Mat right_null_rank(const Mat &A0, int rank) {
+    const int m = A0.c;
+    Mat A = A0;
+    std::vector<int> rp, cp;
+    lu_full_steps(A, rp, cp, rank);
+    Mat Z(m, m - rank);
+    for (int f = 0; f < m - rank; ++f) {
+        std::vector<double> y(m, 0.0);
+        y[rank + f] = 1.0;
+        for (int i = rank - 1; i >= 0; --i) {
+            double s = 0.0;
+            for (int k = i + 1; k < m; ++k) s -= A(i, k) * y[k];
+            y[i] = (A(i, i) != 0.0) ? s / A(i, i) : 0.0;
+        }
+        for (int i = 0; i < m; ++i) Z(cp[i], f) = y[i];
+    }
+    return Z;
+}
+
+std::vector<double> particular_solution(const Mat &A0, const std::vector<double> &b, int rank) {
+    const int n = A0.r, m = A0.c;
+    Mat A = A0;
+    std::vector<int> rp, cp;
+    lu_full_steps(A, rp, cp, rank);
+    std::vector<double> y(n);
+    for (int i = 0; i < n; ++i) {
+        double s = b[rp[i]];
+        for (int k = 0; k < std::min(i, rank); ++k) s -= A(i, k) * y[k];
+        y[i] = s;
+    }
+    std::vector<double> z(m, 0.0);
+    for (int i = rank - 1; i >= 0; --i) {
+        double s = y[i];
+        for (int k = i + 1; k < rank; ++k) s -= A(i, k) * z[k];
+        z[i] = (A(i, i) != 0.0) ? s / A(i, i) : 0.0;
+    }
+    std::vector<double> x(m, 0.0);
+    for (int i = 0; i < m; ++i) x[cp[i]] = z[i];
+    return x;
+}
+
+void householder_deflate(Mat &C, Mat Z) {
+    const int n = Z.r, kz = Z.c;
+    for (int k = 0; k < kz; ++k) {
+        double nx = 0.0;
+        for (int i = k; i < n; ++i) nx += Z(i, k) * Z(i, k);
+        double alpha = std::sqrt(nx);
+        if (alpha == 0.0) continue;
+        if (Z(k, k) > 0) alpha = -alpha;
+        std::vector<double> v(n - k);
+        for (int i = k; i < n; ++i) v[i - k] = Z(i, k);
+        v[0] -= alpha;
+        double vn = 0.0;
+        for (double e : v) vn += e * e;
+        if (!(vn > 0.0)) continue;
+        // the rest of Z
+        for (int j = k; j < kz; ++j) {
+            double d = 0.0;
+            for (int i = k; i < n; ++i) d += v[i - k] * Z(i, j);
+            d = 2.0 * d / vn;
+            for (int i = k; i < n; ++i) Z(i, j) -= d * v[i - k];
+        }
+        // C <- H C (rows k..n-1), then C <- C H (columns k..n-1)
+        for (int j = 0; j < C.c; ++j) {
+            double d = 0.0;
+            for (int i = k; i < n; ++i) d += v[i - k] * C(i, j);
+            d = 2.0 * d / vn;
+            for (int i = k; i < n; ++i) C(i, j) -= d * v[i - k];
+        }
+        for (int i = 0; i < C.r; ++i) {
+            double d = 0.0;
+            for (int j = k; j < n; ++j) d += C(i, j) * v[j - k];
+            d = 2.0 * d / vn;
+            for (int j = k; j < n; ++j) C(i, j) -= d * v[j - k];
+        }
+    }
+}
+
 bool lu_full_solve(const Mat &A0, const Mat &B, Mat *X) {
     const int n = A0.r, m = B.c;
     Mat A = A0;

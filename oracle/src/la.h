@@ -71,4 +71,19 @@ void jacobi_svd(const Mat &A, Mat *U, std::vector<double> *s, Mat *V);
 
 double det3(const double M[9]);
 
+// LU with complete pivoting stopped after `steps` pivots (rank-revealing for a matrix
+// of known rank `steps`): A is overwritten by P A Q = L U (unit L below the diagonal
+// in the first `steps` columns; the trailing block is the rounding residue).
+void lu_full_steps(Mat &A, std::vector<int> &rp, std::vector<int> &cp, int steps);
+// Right null space (n - rank columns) of A of known rank, from lu_full_steps:
+// U11 y1 + U12 y2 = 0 with y2 = e_k, x = Q y.
+Mat right_null_rank(const Mat &A, int rank);
+// A particular solution of A x = b for A of known rank (b in the range of A): the
+// first `rank` variables of Q^T x from the LU, the others zero.
+std::vector<double> particular_solution(const Mat &A, const std::vector<double> &b, int rank);
+// C <- Q^T C Q with Q = H_0 ... H_{k-1} the Householder reflectors of the QR of the
+// n x k matrix Z (GvL 5.2.1, v = x - alpha e1, alpha = -sign(x_0) |x|): the first k
+// columns of Q span the columns of Z.
+void householder_deflate(Mat &C, Mat Z);
+
 } // namespace oracle

@@ -270,8 +270,62 @@ int recover_pose(const double E_in[9], const double *p0, const double *p1, int n
     return good[best];
 }
 
-std::vector<Model> relpose_6pt_shared_focal(const double *x1, const double *x2) {
-    std::vector<Model> out;
+// Positive real roots u = 1/w of det(u^2 M0 + u M1 + M2) / u^5, in eigen-solver
+// order.  The companion C on z = [v; u v] (20 x 20) carries a structural 5-fold
+// zero eigenvalue: the right null space of M2 (rank 6 -- row 0 is zero and every
+// other row is F_22 times a quadratic in (x, y)) and one Jordan vector [a; v] with v
+// in null(M2), M1 v in range(M2) and M2 a = -M1 v.  Rounding splits that eigenvalue
+// into a cluster reaching ~1e-4 of the largest root (measured over 6000 random
+// samples), where genuine roots also occur (down to ~5e-5 of it); no threshold
+// separates the two.  So the 5-dimensional invariant subspace is deflated exactly
+// (orthogonal similarity by the Householder reflectors of its basis) and the 15
+// remaining eigenvalues -- the roots of the degree-15 q(u) -- are computed alone.
+std::vector<double> sixpt_roots(const Mat &M0, const Mat &M1, const Mat &M2) {
+    std::vector<double> out;
+    Mat B(10, 20), X;
+    for (int r = 0; r < 10; ++r)
+        for (int c = 0; c < 10; ++c) {
+            B(r, c) = M2(r, c);
+            B(r, 10 + c) = M1(r, c);
+        }
+    if (!lu_full_solve(M0, B, &X)) return out;
+    Mat C(20, 20);
+    for (int i = 0; i < 10; ++i) C(i, 10 + i) = 1.0;
+    for (int r = 0; r < 10; ++r)
+        for (int c = 0; c < 20; ++c) C(10 + r, c) = -X(r, c);
+    const Mat Nr = right_null_rank(M2, 6);            // 10 x 4
+    const Mat Nl = right_null_rank(transpose(M2), 6); // left null vectors as columns
+    const Mat S = matmul(matmul(transpose(Nl), M1), Nr);
+    const Mat cv = right_null_rank(S, 3);
+    std::vector<double> v(10, 0.0), rhs(10, 0.0);
+    for (int i = 0; i < 10; ++i)
+        for (int f = 0; f < 4; ++f) v[i] += Nr(i, f) * cv(f, 0);
+    for (int i = 0; i < 10; ++i) {
+        double s = 0.0;
+        for (int c = 0; c < 10; ++c) s += M1(i, c) * v[c];
+        rhs[i] = -s;
+    }
+    const std::vector<double> a = particular_solution(M2, rhs, 6);
+    Mat Z(20, 5);
+    for (int i = 0; i < 10; ++i) {
+        for (int f = 0; f < 4; ++f) Z(i, f) = Nr(i, f);
+        Z(i, 4) = a[i];
+        Z(10 + i, 4) = v[i];
+    }
+    householder_deflate(C, Z);
+    Mat D(15, 15);
+    for (int r = 0; r < 15; ++r)
+        for (int c = 0; c < 15; ++c) D(r, c) = C(5 + r, 5 + c);
+    std::vector<double> wr, wi;
+    if (!eig_real(D, &wr, &wi)) return out;
+    for (int k = 0; k < 15; ++k)
+        if (wi[k] == 0.0 && wr[k] > 0.0) out.push_back(wr[k]);
+    return out;
+}
+
+// The ten equations of the 6-point system as (M0 + w M1 + w^2 M2) v = 0 over the
+// monomials of (x, y) (V: the epipolar null space, F = x V6 + y V7 + V8).
+void sixpt_pencil(const double *x1, const double *x2, Mat *Vout, Mat *M0out, Mat *M1out, Mat *M2out) {
     Mat V = epipolar_nullspace(x1, x2, 6);
     Q2 F[9];
     for (int e = 0; e < 9; ++e) {
@@ -312,35 +366,40 @@ std::vector<Model> relpose_6pt_shared_focal(const double *x1, const double *x2) 
                 M2(row, k) = T2.c[kMono[k][0]][kMono[k][1]];
             }
         }
-    // u = 1/w:  (u^2 M0 + u M1 + M2) v = 0  ->  companion on z = [v; u v]
-    Mat B(10, 20), X;
-    for (int r = 0; r < 10; ++r)
-        for (int c = 0; c < 10; ++c) {
-            B(r, c) = M2(r, c);
-            B(r, 10 + c) = M1(r, c);
-        }
-    if (!lu_full_solve(M0, B, &X)) return out;
-    Mat C(20, 20);
-    for (int i = 0; i < 10; ++i) C(i, 10 + i) = 1.0;
-    for (int r = 0; r < 10; ++r)
-        for (int c = 0; c < 20; ++c) C(10 + r, c) = -X(r, c);
-    std::vector<double> wr, wi;
-    if (!eig_real(C, &wr, &wi)) return out;
-    double umax = 0.0;
-    for (int k = 0; k < 20; ++k) umax = std::max(umax, std::hypot(wr[k], wi[k]));
-    for (int k = 0; k < 20; ++k) {
-        if (wi[k] != 0.0) continue;
-        const double uu = wr[k];
-        // the pencil has a 5-fold root u = 0 (w at infinity) that rounding splits
-        // into a small cluster; genuine roots that small mean f < 1e-3 sqrt(umax)
-        if (!(uu > 1e-6 * umax)) continue;
+    *Vout = V;
+    *M0out = M0;
+    *M1out = M1;
+    *M2out = M2;
+}
+
+std::vector<double> sixpt_roots_of(const double *x1, const double *x2) {
+    Mat V, M0, M1, M2;
+    sixpt_pencil(x1, x2, &V, &M0, &M1, &M2);
+    return sixpt_roots(M0, M1, M2);
+}
+
+std::vector<Model> relpose_6pt_shared_focal(const double *x1, const double *x2) {
+    std::vector<Model> out;
+    Mat V, M0, M1, M2;
+    sixpt_pencil(x1, x2, &V, &M0, &M1, &M2);
+    for (const double uu : sixpt_roots(M0, M1, M2)) {
         double w = 1.0 / uu;
         Mat Mw(10, 10);
         for (int r = 0; r < 10; ++r)
             for (int c = 0; c < 10; ++c) Mw(r, c) = M0(r, c) + w * (M1(r, c) + w * M2(r, c));
         std::vector<double> v = null_vector(Mw);
-        if (v[9] == 0.0) continue;
-        double x = v[7] / v[9], y = v[8] / v[9];
+        // (x, y) from the monomial ratio with the largest denominator (v ~ x^3, x^2 y,
+        // x y^2, y^3, x^2, x y, y^2, x, y, 1): v7/v9 alone loses the digits of a
+        // solution far from the origin, whose v9 is tiny next to |v|
+        const int xr[5][2] = {{7, 9}, {4, 7}, {0, 4}, {5, 8}, {2, 6}};
+        const int yr[5][2] = {{8, 9}, {6, 8}, {3, 6}, {5, 7}, {1, 4}};
+        int bx = 0, by = 0;
+        for (int k = 1; k < 5; ++k) {
+            if (std::fabs(v[xr[k][1]]) > std::fabs(v[xr[bx][1]])) bx = k;
+            if (std::fabs(v[yr[k][1]]) > std::fabs(v[yr[by][1]])) by = k;
+        }
+        if (v[xr[bx][1]] == 0.0 || v[yr[by][1]] == 0.0) continue;
+        double x = v[xr[bx][0]] / v[xr[bx][1]], y = v[yr[by][0]] / v[yr[by][1]];
         // Gauss-Newton polish of (x, y, w) on the ten equations
         for (int it = 0; it < 5; ++it) {
             double mv[10], dx[10], dy[10];

@@ -33,10 +33,10 @@ def six(n_trials, seed):
                     break
         if mism:
             bad += 1
-            print(json.dumps({"solver": "6pt", "trial": trial, "clean": clean, "f_gt": f0,
+            print(json.dumps({"solver": "6pt", "seed": seed, "trial": trial, "clean": clean, "f_gt": f0,
                               "dev_f": sorted(m.focal for m in dev), "orc_f": sorted(o["focal0"] for o in orc),
                               "p0": p0.tolist(), "p1": p1.tolist()}), flush=True)
-    print(json.dumps({"solver": "6pt", "trials": n_trials, "mismatch": bad}), flush=True)
+    print(json.dumps({"solver": "6pt", "seed": seed, "trials": n_trials, "mismatch": bad}), flush=True)
 
 
 def seven(n_trials, seed):
@@ -68,10 +68,15 @@ def seven(n_trials, seed):
             bad += 1
             print(json.dumps({"solver": "7pt", "trial": trial, "clean": clean, "ndev": len(dev), "norc": len(Fs),
                               "info": info, "p0": p0.tolist(), "p1": p1.tolist()}), flush=True)
-    print(json.dumps({"solver": "7pt", "trials": n_trials, "mismatch": bad}), flush=True)
+    print(json.dumps({"solver": "7pt", "seed": seed, "trials": n_trials, "mismatch": bad}), flush=True)
 
 
 if __name__ == "__main__":
+    # usage: diag_pt67.py [trials] [6pt seeds, comma-separated] [7pt seeds]
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
-    six(n, 21)
-    seven(n, 22)
+    s6 = [int(x) for x in sys.argv[2].split(",") if x] if len(sys.argv) > 2 else [21]
+    s7 = [int(x) for x in sys.argv[3].split(",") if x] if len(sys.argv) > 3 else [22]
+    for sd in s6:
+        six(n, sd)
+    for sd in s7:
+        seven(n, sd)
