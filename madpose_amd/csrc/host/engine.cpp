@@ -652,6 +652,8 @@ class Run {
         const char *env2 = std::getenv("MADPOSE_MIN_BATCH");
         min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 128;
         min_batch_ = std::min(min_batch_, max_batch_);
+        const char *env3 = std::getenv("MADPOSE_BATCH_GROWTH");
+        growth_ = env3 ? std::max(0.01, std::atof(env3)) : 1.0;
         trace_ = std::getenv("MADPOSE_TRACE") != nullptr;
     }
 
@@ -667,6 +669,7 @@ class Run {
     int min_sample_size_, non_min_sample_size_;
     double thr_[3], w_[3];
     int max_batch_, min_batch_;
+    double growth_; // batch = growth_ x iterations so far (MADPOSE_BATCH_GROWTH)
     bool trace_ = false;
     PairData D_;
     Stats *S_ = nullptr;
@@ -1226,7 +1229,25 @@ void Run::run(Model *best, Stats *S) {
     auto batch_size = [&](uint32_t at, uint32_t want) {
         uint32_t B = std::min<uint32_t>(want, max_total - at);
         if (at < lo_start) B = std::min<uint32_t>(B, lo_start - at);
+        // the loop stops once a solver type reaches its (termination-adjusted) cap:
+        // iterations past the expected stop would be scored for nothing.  Expected
+        // stop of type st from here: its remaining count over its selection share
+        // (+10 % and a few iterations of slack; a short batch only costs a round trip).
+        const double ps = prior[0] + prior[1];
+        double cap = 1e18;
+        for (int st = 0; st < 2; ++st) {
+            if (prior[st] <= 0.0) continue;
+            const double share = prior[st] / ps;
+            const double left = (double)max_per[st] - (double)S->num_iterations_per_solver[st] -
+                                share * (double)(at > it ? at - it : 0);
+            cap = std::min(cap, std::max(0.0, left) / share * 1.1 + 32.0);
+        }
+        if (cap < (double)B) B = std::max<uint32_t>(1, (uint32_t)cap);
         return B;
+    };
+    // speculation window at `at`: growth_ x at iterations, clamped to [min, max]
+    auto grow = [&](uint32_t at) {
+        return (uint32_t)std::min<double>((double)max_batch_, std::max<double>((double)min_batch_, growth_ * at));
     };
     Batch gen[2];
     // the worker may be drawing into gen[] when an exception unwinds this frame
@@ -1271,9 +1292,7 @@ void Run::run(Model *best, Stats *S) {
         // batch.
         const uint32_t it_next = it + B;
         const uint32_t Bn = (it_next < max_total && it_next != lo_start)
-                                ? batch_size(it_next, (uint32_t)std::min<uint64_t>(
-                                                          (uint64_t)max_batch_,
-                                                          std::max<uint64_t>((uint64_t)min_batch_, 4ull * it_next)))
+                                ? batch_size(it_next, grow(it_next))
                                 : 0;
         if (Bn > 0) X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(cur ^ 1));
         auto tw = Clock::now();
@@ -1335,8 +1354,7 @@ void Run::run(Model *best, Stats *S) {
                                 if (Bn > 0) X_.sampler->cancel(); // the no-LO continuation
                                 IterationStream from = rs_;
                                 from.sel = sel_end;
-                                const uint32_t bc = (uint32_t)std::min<uint64_t>(
-                                    (uint64_t)max_batch_, std::max<uint64_t>((uint64_t)min_batch_, 4ull * at));
+                                const uint32_t bc = grow(at);
                                 const int slot = cur ^ 1;
                                 Batch *gs = &gen[slot];
                                 // LO leaves best_min_model_score alone (src/hybrid_ransac.h:149-155)
@@ -1400,7 +1418,7 @@ void Run::run(Model *best, Stats *S) {
             if (Bn > 0) X_.sampler->cancel();
             have_next = false;
         }
-        bcur = (int)std::min<uint64_t>((uint64_t)max_batch_, std::max<uint64_t>((uint64_t)min_batch_, 4ull * it));
+        bcur = (int)grow(it);
     }
     if (!done) S->num_iterations_total = it;
 

@@ -984,14 +984,15 @@ constexpr int kN15 = 15;
 namespace mp {
 namespace {
 
-__global__ void __launch_bounds__(64) pt_eig6_reg_kernel(const double *pen, int nlist, double *eig, double *cand,
-                                                         int *ncand, int cand_stride) {
+__global__ void __launch_bounds__(64) pt_eig6_reg_kernel(double *pen, int nlist, double *cand, int *ncand,
+                                                         int cand_stride) {
     const int idx = blockIdx.x * 64 + threadIdx.x;
     const bool valid = idx < nlist;
     const int sidx = valid ? idx : nlist - 1;
-    const double *P = pen + (size_t)sidx * kPenStride;
+    double *P = pen + (size_t)sidx * kPenStride;
     const bool active = valid && P[225] != 0.0;
-    double *wr = eig + (size_t)sidx * 2 * kN15, *wi = wr + kN15;
+    // eigenvalues into the sample's own pencil slot past the block (free by now)
+    double *wr = P + 240, *wi = wr + kN15;
 #ifdef MP_EIG6_PROFILE
     const unsigned long long t_hqr0 = wall_clock64();
 #endif

@@ -43,7 +43,7 @@ hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, co
                         double *score);
 // point-solver root stage alone, C.variant kCal (5pt) or kSF (6pt); impl 0: lane
 // per sample, 1: 16-lane groups, (6pt) 2: DFT nodes over a wave, 3: deflated
-// eigenproblem, one wave per sample (the estimator's default).  cand: kPtCandStride doubles per sample (cal: 9 per
+// eigenproblem (the estimator default, eig6.h).  cand: kPtCandStride doubles per sample (cal: 9 per
 // essential matrix; sf: null-space basis N (27), then the positive roots u)
 hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, double *cand, int *ncand, int impl, double *pen = nullptr);

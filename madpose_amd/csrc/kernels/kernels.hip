@@ -959,6 +959,27 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
     });
 }
 
+// the shared-focal root stage by the deflated eigenproblem: the pencil, its
+// deflation + balanced Hessenberg form (one sample per wave), then the lockstep QR
+// (one sample per lane, eig6.h / eig15_gen.h); MADPOSE_PT6_EIG=wave: hqr with one
+// sample per wave instead (A/B)
+static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int nlist, const int *samples,
+                          double *cand, int *ncand, double *pen) {
+    static const bool wave = [] {
+        const char *e = std::getenv("MADPOSE_PT6_EIG");
+        return e && e[0] == 'w';
+    }();
+    pt_pencil6_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, list, nlist, samples, cand, kCandStride,
+                                                                         pen);
+    if (wave) {
+        pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, false);
+        pt_eig6_kernel<<<nlist, 64, 0, s>>>(pen, cand, ncand, kCandStride);
+    } else {
+        pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, true);
+        pt_eig6_reg_kernel<<<(nlist + 63) / 64, 64, 0, s>>>(pen, nlist, cand, ncand, kCandStride);
+    }
+}
+
 bool pt6_dft() {
     static const bool v = [] {
         const char *e = std::getenv("MADPOSE_PT6_DFT");
@@ -986,12 +1007,9 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
         // shared focal default: the deflated eigenproblem (eig6.h); MADPOSE_PT6_DFT=1
         // keeps the DFT + Sturm kernels above (A/B; they lose roots)
         static const bool dft6 = pt6_dft();
-        if (v == kSF && !dft6) {
-            pt_pencil6_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, list, nlist, samples, W.cand,
-                                                                                 kCandStride, W.pen);
-            pt_defl6_kernel<<<nlist, 64, 0, s>>>(W.pen, false);
-            pt_eig6_kernel<<<nlist, 64, 0, s>>>(W.pen, W.cand, W.ncand, kCandStride);
-        } else if (v == kCal && !lane5)
+        if (v == kSF && !dft6)
+            launch_sf_eig(s, D, list, nlist, samples, W.cand, W.ncand, W.pen);
+        else if (v == kCal && !lane5)
             pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                           kCandStride);
         else if (v == kSF && !lane6 && wave6)
@@ -1113,12 +1131,9 @@ hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C,
             pt_roots6_group_kernel<<<ggrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
         else if (impl == 2)
             pt_roots6_wave_kernel<<<nlist, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
-        else if (impl == 3 && pen) {
-            pt_pencil6_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, list, nlist, samples, cand,
-                                                                                 kCandStride, pen);
-            pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, false);
-            pt_eig6_kernel<<<nlist, 64, 0, s>>>(pen, cand, ncand, kCandStride);
-        } else if (impl == 3)
+        else if (impl == 3 && pen)
+            launch_sf_eig(s, D, list, nlist, samples, cand, ncand, pen);
+        else if (impl == 3)
             return hipErrorInvalidValue;
         else
             pt_roots_kernel<kSF><<<lgrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);

@@ -67,10 +67,13 @@ def test_single_rank_summary_fields():
         assert k in res
     assert res["scaling"] == "weak" and res["dtype"] == "f64" and res["vs_baseline"] is None
     rf = res["roofline"]
-    assert abs(rf["achieved"] - 3e5 * 2000 * 48 / 0.1 / 1e9) < 1e-6
+    # achieved: the bytes the early-exit kernel read (the evaluated share of the full
+    # figure) over the score time; effective_GBps credits the full figure
+    assert abs(rf["effective_GBps"] - 3e5 * 2000 * 48 / 0.1 / 1e9) < 1e-6
+    assert abs(rf["achieved"] - rf["effective_GBps"] * 1e6 / 2.4e6) < 1e-6
     assert abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-12
     assert abs(rf["evaluated_frac"] - 1e6 / 2.4e6) < 1e-12
-    assert abs(rf["evaluated_bytes_per_launch"] - 1e6 * 256 * 48 / 30) < 1e-6
+    assert abs(rf["evaluated_bytes_per_launch"] - 3e5 * 2000 * 48 * (1e6 / 2.4e6) / 30) < 1e-3
     assert abs(res["speculation"]["scored_over_accepted"] - 3e5 / 2.5e5) < 1e-12
 
 

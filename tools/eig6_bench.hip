@@ -109,7 +109,7 @@ int main(int argc, char **argv) {
         CHECK(hipEventRecord(ev[5]));
         pt_defl6_kernel<<<ns, 64>>>(d_pen2, true); // (the Hessenberg form for the lockstep kernel)
         CHECK(hipEventRecord(ev[6]));
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, d_eig, d_c4, d_n4, kCandStride);
+        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, d_c4, d_n4, kCandStride);
         CHECK(hipEventRecord(ev[7]));
         CHECK(hipEventSynchronize(ev[7]));
         if (timed)
