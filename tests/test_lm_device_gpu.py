@@ -79,6 +79,14 @@ def _close(m, ref, variant, tol=1e-7, epi_only=False):
     return bool(ok)
 
 
+def _near_start(ref, m0):
+    """The oracle's minimum lies near the start: rotation within 10 degrees, scale
+    within a factor 2, offsets within 10 x (1 + |start|) of the start."""
+    if rot_angle_deg(ref["R"], m0.R()) > 10.0 or not 0.5 < ref["scale"] / m0.scale < 2.0:
+        return False
+    return all(abs(ref[k] - getattr(m0, k)) <= 10.0 * (1.0 + abs(getattr(m0, k))) for k in ("offset0", "offset1"))
+
+
 def _oracle_model(m, variant):
     d = dict(R=m.R(), t=m.t(), scale=m.scale, offset0=m.offset0, offset1=m.offset1, focal0=1.0, focal1=1.0)
     if variant == 1:
@@ -105,27 +113,55 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
     mk = [madpose.PoseScaleOffset, madpose.PoseScaleOffsetSharedFocal, madpose.PoseScaleOffsetTwoFocal][variant]
     est = mk(m["R"], m["t"], m["scale"], m["offset0"], m["offset1"], *[[], [m["focal0"]],
                                                                          [m["focal0"], m["focal1"]]][variant])
-    probs = _problems(rng, p, variant, norm_scale, 24, est)
-    got = madpose.lm_refine_batch(variant, *args, o, c, probs)
-    host = madpose.lm_refine_batch(variant, *args, o, c, probs, on_host=True)
-    checked = chaotic = 0
-    for (kind, lists, m0), (m, st), (mh, sth) in zip(probs, got, host):
+    # 24 problems whose start lies in the basin of a nearby minimum: the oracle's
+    # solution stays near the start.  Some LO-like starts (found with 48 / 38 / 182
+    # residuals as with 5) let the non-monotonic evaluator run an offset away to ~1e7,
+    # where rounding-level differences between ANY two implementations grow; such a
+    # start is a property of the problem, decided by the oracle alone, before the
+    # device runs
+    probs, refs = [], []
+    for cand in _problems(rng, p, variant, norm_scale, 96, est):
+        kind, lists, m0 = cand
         ref, ran = oracle.least_squares(variant, *args, oracle_opts(o), oracle_cfg(c), kind, lists,
                                         _oracle_model(m0, variant))
+        if ran and not _near_start(ref, m0):
+            continue
+        probs.append(cand)
+        refs.append((ref, ran))
+        if len(probs) == 24:
+            break
+    assert len(probs) == 24
+    got = madpose.lm_refine_batch(variant, *args, o, c, probs)
+    host = madpose.lm_refine_batch(variant, *args, o, c, probs, on_host=True)
+    for (kind, lists, m0), (m, st), (mh, sth), (ref, ran) in zip(probs, got, host, refs):
         if not ran:
             assert st == 3 and sth == 3
             assert np.array_equal(m.pose, m0.pose)
             continue
         assert st in (0, 1, 2) and st == sth
-        # A few problems (far-from-inlier starts that the non-monotonic evaluator lets
-        # run away, e.g. offsets in the tens of thousands) are chaotic: rounding-level
-        # differences between ANY two implementations grow, and the engine's host LM
-        # disagrees with the oracle there as much as the device does.  Everywhere the
-        # two CPU implementations agree, the device must agree too.
-        if not _close(mh, ref, variant, epi_only=lo_type == 1):
-            chaotic += 1
-            continue
-        assert _close(m, ref, variant, epi_only=lo_type == 1), (kind, [len(x) for x in lists])
-        checked += 1
-    assert chaotic <= 3, chaotic
-    assert checked >= 12
+        # every problem: the engine's host LM and the device LM both agree with the oracle
+        sizes = [len(x) for x in lists]
+        assert _close(mh, ref, variant, epi_only=lo_type == 1), ("host", kind, sizes)
+        assert _close(m, ref, variant, epi_only=lo_type == 1), ("device", kind, sizes)
+
+
+def test_device_lm_many_problems_deterministic():
+    """Several hundred problems in one launch, twice: bit-identical refined models and
+    statuses (the proposal flag of lm_batch_kernel is published once per iteration
+    after a barrier; a wave reading it early would leave its loop and sum a stale
+    partial row -- ADVICE r02)."""
+    variant = 0
+    rng = np.random.default_rng(7)
+    p = synthetic.make_pair(44, n=800)
+    o, c = synthetic.example_options(KIND[variant], iterations=100)
+    args = (p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], p["K0"], p["K1"])
+    _, _, norm_scale = oracle.score_models(variant, *args[:4], p["K0"], p["K1"], oracle_opts(o), oracle_cfg(c), [])
+    m, _, _ = oracle.estimate(variant, *args, oracle_opts(o), oracle_cfg(c))
+    est = madpose.PoseScaleOffset(m["R"], m["t"], m["scale"], m["offset0"], m["offset1"])
+    probs = _problems(rng, p, variant, norm_scale, 384, est)
+    a = madpose.lm_refine_batch(variant, *args, o, c, probs)
+    b = madpose.lm_refine_batch(variant, *args, o, c, probs)
+    assert len(a) == len(b) == 384
+    for (ma, sa), (mb, sb) in zip(a, b):
+        assert sa == sb
+        assert np.array_equal(ma.pose, mb.pose)
