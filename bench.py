@@ -163,7 +163,7 @@ def pmc_traffic_model():
 COUNTERS = ["elapsed_s", "hypotheses", "iterations", "lo_runs", "lo_s", "score_ms", "solve_ms", "prof_hypotheses",
             "prof_correspondences", "prof_batches", "prof_sweeps", "lm_calls", "lm_ms", "sweep_ms", "prof_iterations",
             "sample_ms", "wait_ms", "run_ms", "lm_blocks", "lm_big_calls", "lm_big_ms", "model_trips",
-            "model_trips_full", "prof_accepted"]
+            "model_trips_full", "prof_accepted", "prof_scored"]
 
 
 def gather_counters(local, world):
@@ -293,12 +293,15 @@ def summarize(allv, wl, steps, warmup, world):
             "fp64_valu": fp64,
         },
         "cpu_baseline": None,
-        # speculative waste: every hypothesis scored on the GPU against those of the
-        # iterations the estimator consumed (batches cut at an LO, discarded post-LO
-        # speculation); the roofline above credits all scored work
-        "speculation": {"scored_hypotheses": int(c["prof_hypotheses"].sum()),
+        # speculative waste: every hypothesis the solvers produced ("solved") and every
+        # one whose scoring sweep ran ("scored": score_batch skips the iterations past a
+        # batch's first new best once LO cuts there) against those of the iterations
+        # the estimator consumed (batches cut at an LO, discarded post-LO speculation)
+        "speculation": {"solved_hypotheses": int(c["prof_hypotheses"].sum()),
+                        "scored_hypotheses": int(c["prof_scored"].sum()),
                         "accepted_hypotheses": int(c["prof_accepted"].sum()),
-                        "scored_over_accepted": float(c["prof_hypotheses"].sum()) / max(float(c["prof_accepted"].sum()), 1.0)},
+                        "solved_over_accepted": float(c["prof_hypotheses"].sum()) / max(float(c["prof_accepted"].sum()), 1.0),
+                        "scored_over_accepted": float(c["prof_scored"].sum()) / max(float(c["prof_accepted"].sum()), 1.0)},
         "dist": dist_info(world),
     }
 
@@ -673,7 +676,7 @@ def main(argv=None):
              prof["correspondences"], prof["batches"], prof["sweeps"], prof["lm_calls"], prof["lm_wall_ms"],
              prof["sweep_wall_ms"], prof["iterations"], prof["sample_wall_ms"], prof["wait_wall_ms"],
              prof["run_wall_ms"], prof["lm_blocks"], prof["lm_big_calls"], prof["lm_big_wall_ms"],
-             prof["model_trips"], prof["model_trips_full"], prof["accepted"]]
+             prof["model_trips"], prof["model_trips_full"], prof["accepted"], prof["scored"]]
     allv = gather_counters(local, world)
     allr = gather_records(recs, a.steps, world)
     if rank == 0:

@@ -264,6 +264,9 @@ typedef struct mp_kernel_profile {
     uint64_t model_trips_full;/* the same without the early exit            */
     uint64_t accepted;        /* hypotheses of the iterations the estimator
                                  consumed (the rest was speculative)          */
+    uint64_t scored;          /* hypotheses whose score_batch sweep ran (the
+                                 record skip drops iterations past a batch's
+                                 first new best; `hypotheses` counts them)     */
 } mp_kernel_profile;
 int mp_profile_enable(int on);
 int mp_profile_reset(void);

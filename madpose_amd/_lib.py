@@ -108,6 +108,7 @@ class mp_kernel_profile(ctypes.Structure):
         ("model_trips", ctypes.c_uint64),
         ("model_trips_full", ctypes.c_uint64),
         ("accepted", ctypes.c_uint64),
+        ("scored", ctypes.c_uint64),
     ]
 
 

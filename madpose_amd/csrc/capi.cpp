@@ -438,6 +438,7 @@ int mp_profile_read(mp_kernel_profile *out) {
     out->model_trips = p.model_trips;
     out->model_trips_full = p.model_trips_full;
     out->accepted = p.accepted;
+    out->scored = p.scored;
     return MP_OK;
 }
 

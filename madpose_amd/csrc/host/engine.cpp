@@ -330,6 +330,9 @@ struct DeviceCtx {
     int *d_counts = nullptr;
     IterResult *d_res = nullptr;
     int *d_work = nullptr; // score_batch's evaluated (model, trip) pairs per iteration
+    // score_batch's record word (kernels.hip ScoreBound::rec) and the batch epoch
+    unsigned long long *d_recword = nullptr;
+    uint32_t epoch = 0;
     Model *d_models = nullptr;
     ScoreRec *d_recs = nullptr;
     double *d_scores = nullptr;
@@ -359,7 +362,7 @@ struct DeviceCtx {
     void free_all() {
         hipSetDevice(device);
         for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_counts,
-                        (void *)d_res, (void *)d_work, (void *)d_models, (void *)d_recs, (void *)d_scores,
+                        (void *)d_res, (void *)d_work, (void *)d_recword, (void *)d_models, (void *)d_recs, (void *)d_scores,
                         (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_pen, (void *)d_pt_ncand,
                         (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
@@ -370,6 +373,7 @@ struct DeviceCtx {
         d_samples = d_counts = nullptr;
         d_res = nullptr;
         d_work = nullptr;
+        d_recword = nullptr;
         d_models = nullptr;
         d_recs = d_rec1 = nullptr;
         d_pt_cand = d_pt_pen = nullptr;
@@ -398,6 +402,8 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_counts, sizeof(int) * bb));
         MP_HIP(hipMalloc(&d_res, sizeof(IterResult) * bb));
         MP_HIP(hipMalloc(&d_work, sizeof(int) * bb));
+        MP_HIP(hipMalloc(&d_recword, sizeof(unsigned long long)));
+        MP_HIP(hipMemset(d_recword, 0xff, sizeof(unsigned long long)));
         MP_HIP(hipMalloc(&d_models, sizeof(Model) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * (size_t)bb * mm));
         MP_HIP(hipMalloc(&d_scores, sizeof(double) * (size_t)bb * mm));
@@ -1130,7 +1136,9 @@ class Run {
     // per-iteration best scores / slots / model counts back to pinned host memory.
     // best: best_min_model_score when the batch starts (the scoring's early exit).
     bool batch_prof_ = false;
-    void launch_batch(const Batch &g, double best) {
+    // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
+    // best runs LO and cuts it; score_batch then skips the iterations behind a record
+    void launch_batch(const Batch &g, double best, bool cut_on_record) {
         const uint32_t B = g.B;
         const int nmd = g.nmd, npt = g.npt;
         hipStream_t s = X_.stream;
@@ -1154,8 +1162,9 @@ class Run {
                                maxm_));
         if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
         if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
+        const unsigned epoch_hi = ~(++X_.epoch);
         MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res, best,
-                                  prof ? X_.d_work : nullptr));
+                                  prof ? X_.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi));
         if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
         MP_HIP(hipMemcpyAsync(X_.h_res, X_.d_res, sizeof(IterResult) * B, hipMemcpyDeviceToHost, s));
         if (prof) MP_HIP(hipMemcpyAsync(X_.h_work, X_.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
@@ -1283,7 +1292,7 @@ void Run::run(Model *best, Stats *S) {
         auto t_batch = Clock::now();
         const Batch &g = gen[cur];
         const uint32_t B = g.B;
-        if (!launched) launch_batch(g, best_min_score);
+        if (!launched) launch_batch(g, best_min_score, it >= lo_start);
         launched = false;
         const bool prof = batch_prof_;
         // While the batch is in flight, the sampler thread draws the next one into the
@@ -1304,10 +1313,11 @@ void Run::run(Model *best, Stats *S) {
             float ms_solve = 0.f, ms_score = 0.f;
             MP_HIP(hipEventElapsedTime(&ms_solve, X_.ev[0], X_.ev[1]));
             MP_HIP(hipEventElapsedTime(&ms_score, X_.ev[1], X_.ev[2]));
-            uint64_t h = 0, trips = 0;
+            uint64_t h = 0, trips = 0, scored = 0;
             for (uint32_t q = 0; q < B; ++q) {
                 h += (uint64_t)X_.h_res[q].count;
                 trips += (uint64_t)X_.h_work[q];
+                if (X_.h_work[q] > 0) scored += (uint64_t)X_.h_res[q].count;
             }
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.model_trips += trips;
@@ -1315,6 +1325,7 @@ void Run::run(Model *best, Stats *S) {
             g_prof.batches += 1;
             g_prof.iterations += B;
             g_prof.hypotheses += h;
+            g_prof.scored += scored;
             g_prof.correspondences += h * (uint64_t)n_;
             g_prof.solve_ms += ms_solve;
             g_prof.score_ms += ms_score;
@@ -1360,11 +1371,11 @@ void Run::run(Model *best, Stats *S) {
                                 // LO leaves best_min_model_score alone (src/hybrid_ransac.h:149-155)
                                 const double bound = best_min_score;
                                 X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(slot),
-                                                  [this, gs, bound] {
+                                                  [this, gs, bound, at, lo_start] {
                                                       // the sampler thread is not bound to the
                                                       // estimator's device by itself
                                                       MP_HIP(hipSetDevice(X_.device));
-                                                      launch_batch(*gs, bound);
+                                                      launch_batch(*gs, bound, at >= lo_start);
                                                   });
                                 spec = true;
                                 spec_draws = sel_end.draws();

@@ -126,6 +126,7 @@ struct KernelProfile {
     uint64_t model_trips = 0;      // score_batch (model, 256-correspondence trip) pairs evaluated
     uint64_t model_trips_full = 0; // ... and without the early exit (models x trips)
     uint64_t accepted = 0;         // hypotheses of the iterations the estimator consumed
+    uint64_t scored = 0;           // hypotheses whose score_batch sweep ran (not record-skipped)
 };
 constexpr size_t kBigLM = 1024;
 void profile_enable(bool on);

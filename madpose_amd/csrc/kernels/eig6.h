@@ -308,8 +308,10 @@ __device__ void e6_hessenberg(Eig15Shared &sh) {
 // balanced upper Hessenberg form (balance + elmhes) -- and pen[225] = 1 (0: M0
 // singular, no roots).
 struct Defl6Shared {
-    double G[10][31];  // Gauss-Jordan workspace
-    double M1[10][10], M2[10][10];
+    union {
+        double G[10][31]; // Gauss-Jordan workspace
+        Eig15Shared s15;  // balance + elmhes of the deflated block (after the last G use)
+    };
     double A[20][21];  // companion, deflated in place
     double Nr[10][4], Nl[10][4];
     double T[4][10], S[4][4];
@@ -347,19 +349,18 @@ __global__ void __launch_bounds__(64) pt_defl6_kernel(double *pen, bool hess) {
     __shared__ Defl6Shared sh;
     const int lane = threadIdx.x;
     double *P = pen + (size_t)blockIdx.x * kPenStride;
+    // M1, M2 are read from the pencil rows in global memory (L2-resident, written by
+    // pt_pencil6_kernel) instead of LDS copies: 1.6 KB less LDS per workgroup
+    const double *M1 = P + 100, *M2 = P + 200;
+#define M1_(r, c) M1[10 * (r) + (c)]
+#define M2_(r, c) M2[10 * (r) + (c)]
     // G = [M0 | M2 | M1]
     for (int e = lane; e < 300; e += 64) {
         const int a = e / 100, r = (e / 10) % 10, c = e % 10;
         const double x = P[e];
         if (a == 0) sh.G[r][c] = x;
-        if (a == 1) {
-            sh.M1[r][c] = x;
-            sh.G[r][20 + c] = x;
-        }
-        if (a == 2) {
-            sh.M2[r][c] = x;
-            sh.G[r][10 + c] = x;
-        }
+        if (a == 1) sh.G[r][20 + c] = x;
+        if (a == 2) sh.G[r][10 + c] = x;
     }
     e6_bar();
     // ---- C = [0 I; -M0^-1 [M2 M1]] ----
@@ -376,12 +377,12 @@ __global__ void __launch_bounds__(64) pt_defl6_kernel(double *pen, bool hess) {
     e6_bar();
     // ---- the zero-eigenvalue invariant subspace ----
     // left null space of M2 (Gauss-Jordan of M2^T, rank 6)
-    for (int e = lane; e < 100; e += 64) sh.G[e / 10][e % 10] = sh.M2[e % 10][e / 10];
+    for (int e = lane; e < 100; e += 64) sh.G[e / 10][e % 10] = M2_(e % 10, e / 10);
     e6_bar();
     e6_gauss_jordan<31>(sh.G, 10, 10, 10, 6, sh.mul, sh.prow, sh.pcol);
     e6_null_gj<31, 4>(sh.G, 10, 6, sh.prow, sh.pcol, sh.Nl);
     // right null space of M2
-    for (int e = lane; e < 100; e += 64) sh.G[e / 10][e % 10] = sh.M2[e / 10][e % 10];
+    for (int e = lane; e < 100; e += 64) sh.G[e / 10][e % 10] = M2_(e / 10, e % 10);
     e6_bar();
     e6_gauss_jordan<31>(sh.G, 10, 10, 10, 6, sh.mul, sh.prow, sh.pcol);
     e6_null_gj<31, 4>(sh.G, 10, 6, sh.prow, sh.pcol, sh.Nr);
@@ -390,7 +391,7 @@ __global__ void __launch_bounds__(64) pt_defl6_kernel(double *pen, bool hess) {
         const int i = lane / 10, c = lane % 10;
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < 10; ++k) acc += sh.Nl[k][i] * sh.M1[k][c];
+        for (int k = 0; k < 10; ++k) acc += sh.Nl[k][i] * M1_(k, c);
         sh.T[i][c] = acc;
     }
     e6_bar();
@@ -415,14 +416,14 @@ __global__ void __launch_bounds__(64) pt_defl6_kernel(double *pen, bool hess) {
     if (lane < 10) {
         double acc = 0.0;
 #pragma unroll
-        for (int c = 0; c < 10; ++c) acc += sh.M1[lane][c] * sh.v[c];
+        for (int c = 0; c < 10; ++c) acc += M1_(lane, c) * sh.v[c];
         sh.rhs[lane] = -acc;
     }
     e6_bar();
     // a particular solution of M2 a = rhs: Gauss-Jordan of [M2 | rhs], 6 pivots
     for (int e = lane; e < 110; e += 64) {
         const int i = e / 11, c = e % 11;
-        sh.G[i][c] = c < 10 ? sh.M2[i][c] : sh.rhs[i];
+        sh.G[i][c] = c < 10 ? M2_(i, c) : sh.rhs[i];
     }
     e6_bar();
     e6_gauss_jordan<31>(sh.G, 10, 11, 10, 6, sh.mul, sh.prow, sh.pcol);
@@ -487,8 +488,11 @@ __global__ void __launch_bounds__(64) pt_defl6_kernel(double *pen, bool hess) {
         if (lane == 0) P[225] = 1.0;
         return;
     }
-    // balanced upper Hessenberg form of the block (for pt_eig6_reg_kernel)
-    __shared__ Eig15Shared s15;
+#undef M1_
+#undef M2_
+    // balanced upper Hessenberg form of the block (for pt_eig6_reg_kernel), in the
+    // Gauss-Jordan workspace (free from here on)
+    Eig15Shared &s15 = sh.s15;
     for (int e = lane; e < 225; e += 64) s15.H[e / 15][e % 15] = sh.A[5 + e / 15][5 + e % 15];
     e6_bar();
     e6_balance(s15);
@@ -984,10 +988,15 @@ constexpr int kN15 = 15;
 namespace mp {
 namespace {
 
-__global__ void __launch_bounds__(64) pt_eig6_reg_kernel(double *pen, int nlist, double *cand, int *ncand,
+// spw: samples per wave (lanes spw..63 idle).  The kernel is issue-bound on one wave
+// per SIMD and a wave runs until its slowest lane's QR has converged, so the launch
+// spreads the samples over about one wave per SIMD (kernels.hip launch_sf_eig): fewer
+// lanes per wave, fewer rounds.  A lane's arithmetic does not depend on the others
+// (its updates are exact no-ops while it waits), so the roots are the same for any spw.
+__global__ void __launch_bounds__(64) pt_eig6_reg_kernel(double *pen, int nlist, int spw, double *cand, int *ncand,
                                                          int cand_stride) {
-    const int idx = blockIdx.x * 64 + threadIdx.x;
-    const bool valid = idx < nlist;
+    const int idx = blockIdx.x * spw + threadIdx.x;
+    const bool valid = (int)threadIdx.x < spw && idx < nlist;
     const int sidx = valid ? idx : nlist - 1;
     double *P = pen + (size_t)sidx * kPenStride;
     const bool active = valid && P[225] != 0.0;

@@ -531,10 +531,24 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
 // stays uniform) is compared with `cut`; the workgroup leaves once no model is live.
 // Killed models report DBL_MAX and never enter the argmin; a model that could win is
 // never killed, so the winner and its score are those of the full sweep.
+//
+// Record skip (ScoreBound::rec, batches at or past lo_starting_iterations only): there
+// every new best runs LO, which consumes the selection stream, so the host cuts the
+// batch at the first iteration whose best beats the pre-batch best
+// (src/hybrid_ransac.h:123-156) and discards every later one.  A workgroup whose
+// iteration scores below `best` (the same comparison on the same doubles as the
+// host's) publishes its index by an atomic minimum; a workgroup that starts after an
+// earlier record was published skips its sweep.  Iterations up to the first record
+// are always scored in full, so the host's walk never reads a skipped one.  The word
+// carries an epoch in its high half (complemented, so a new batch's first record
+// always wins the minimum) and needs no reset between batches.
 struct ScoreBound {
     double cut;          // +inf: no early exit
     int first, every;    // first check after `first` trips, then every `every` trips
     int *work;           // per iteration: (model, trip) pairs evaluated (profiling)
+    unsigned long long *rec; // nullptr: no record skip
+    unsigned epoch_hi;       // ~epoch of this batch
+    double best;             // the pre-batch best (exact)
 };
 
 // EXIT = false (no finite bound yet, or MADPOSE_SCORE_EXIT=0): the plain sweep,
@@ -552,6 +566,21 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
             if (sb.work) sb.work[b] = 0;
         }
         return;
+    }
+    if (sb.rec) {
+        __shared__ int s_skip;
+        if (threadIdx.x == 0) {
+            const unsigned long long k = __hip_atomic_load(sb.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_skip = (unsigned)(k >> 32) == sb.epoch_hi && (int)(unsigned)(k & 0xffffffffu) < b;
+        }
+        __syncthreads();
+        if (s_skip) { // (uniform) a record earlier in the batch: this iteration is discarded
+            if (threadIdx.x == 0) {
+                res[b] = IterResult{DBL_MAX, 0, nm};
+                if (sb.work) sb.work[b] = 0;
+            }
+            return;
+        }
     }
     const ScoreRec *R = recs + (size_t)b * MAXM;
     double acc[MAXM];
@@ -652,6 +681,8 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         }
         res[b] = IterResult{bs, bi, nm};
         if (sb.work) sb.work[b] = work;
+        if (sb.rec && bs < sb.best)
+            atomicMin(sb.rec, ((unsigned long long)sb.epoch_hi << 32) | (unsigned long long)(unsigned)b);
     }
 }
 
@@ -963,6 +994,16 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
 // deflation + balanced Hessenberg form (one sample per wave), then the lockstep QR
 // (one sample per lane, eig6.h / eig15_gen.h); MADPOSE_PT6_EIG=wave: hqr with one
 // sample per wave instead (A/B)
+// samples per wave of the lockstep QR: about one wave per SIMD (1024 on MI355X;
+// MADPOSE_EIG_WAVES overrides, MADPOSE_EIG_WAVES=16 packs 64 samples per wave at 1024)
+int eig_spw(int nlist) {
+    static const int waves = [] {
+        const char *e = std::getenv("MADPOSE_EIG_WAVES");
+        return e ? std::max(1, std::atoi(e)) : 1024;
+    }();
+    return std::min(64, std::max(1, (nlist + waves - 1) / waves));
+}
+
 static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int nlist, const int *samples,
                           double *cand, int *ncand, double *pen) {
     static const bool wave = [] {
@@ -976,7 +1017,8 @@ static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int
         pt_eig6_kernel<<<nlist, 64, 0, s>>>(pen, cand, ncand, kCandStride);
     } else {
         pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, true);
-        pt_eig6_reg_kernel<<<(nlist + 63) / 64, 64, 0, s>>>(pen, nlist, cand, ncand, kCandStride);
+        const int spw = eig_spw(nlist);
+        pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride);
     }
 }
 
@@ -1053,7 +1095,7 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
 
 // Early-exit schedule (MADPOSE_SCORE_EXIT=0 turns the exit off; MADPOSE_SCORE_CHECK
 // "first,every" in trips of 256 correspondences overrides the schedule).
-static ScoreBound score_bound(double best, int n, int *work) {
+static ScoreBound score_bound(double best, int n, int *work, unsigned long long *rec, unsigned epoch_hi) {
     static const int mode = [] {
         const char *e = std::getenv("MADPOSE_SCORE_EXIT");
         return (e && e[0] == '0') ? 0 : 1;
@@ -1077,16 +1119,23 @@ static ScoreBound score_bound(double best, int n, int *work) {
     sb.first = sched[0] > 0 ? sched[0] : std::max(1, ntrip / 4);
     sb.every = sched[0] > 0 ? sched[1] : std::max(1, ntrip / 4);
     sb.work = work;
+    static const bool skip = [] {
+        const char *e = std::getenv("MADPOSE_RECORD_SKIP");
+        return !(e && e[0] == '0');
+    }();
+    sb.rec = skip ? rec : nullptr;
+    sb.epoch_hi = epoch_hi;
+    sb.best = best;
     return sb;
 }
 
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
-                              int *work) {
+                              int *work, unsigned long long *rec, unsigned epoch_hi) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
     const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
-    const ScoreBound sb = score_bound(best, C.n, work);
+    const ScoreBound sb = score_bound(best, C.n, work, rec, epoch_hi);
     const bool exit = sb.cut < __builtin_inf();
     auto go = [&](auto V, auto M, auto F) {
         constexpr int kV = decltype(V)::value, kM = decltype(M)::value;

@@ -46,5 +46,5 @@ class Engine:
     def profile_read(self):
         keys = ["score_ms", "solve_ms", "hypotheses", "correspondences", "batches", "sweeps", "lm_calls",
                 "lm_wall_ms", "sweep_wall_ms", "iterations", "sample_wall_ms", "wait_wall_ms", "run_wall_ms",
-                "lm_blocks", "lm_big_calls", "lm_big_wall_ms", "model_trips", "model_trips_full", "accepted"]
+                "lm_blocks", "lm_big_calls", "lm_big_wall_ms", "model_trips", "model_trips_full", "accepted", "scored"]
         return {k: 1.0 for k in keys}

@@ -30,28 +30,30 @@ def _worker(rank, world, port, out_path):
     # rank r: elapsed 1 + r seconds, 1000 * (r + 1) hypotheses, ...
     local = [1.0 + rank, 1000.0 * (rank + 1), 500.0, 2.0, 0.5, 10.0, 5.0, 1000.0 * (rank + 1),
              2000.0 * 1000.0 * (rank + 1), 4.0, 7.0, 3.0, 1.0, 2.0, 400.0, 0.3, 0.4, 900.0, 5000.0, 1.0, 0.5,
-             4000.0 * (rank + 1), 8000.0 * (rank + 1), 700.0 * (rank + 1)]
+             4000.0 * (rank + 1), 8000.0 * (rank + 1), 700.0 * (rank + 1), 900.0 * (rank + 1)]
     allv = bench.gather_counters(local, world)
     if rank == 0:
         res = bench.summarize(allv, bench.WORKLOADS["cal"], 3, 1, world)
         assert res["dist"]["backend"] == "gloo" and res["dist"]["world_size"] == world
         np.save(out_path, np.array([res["value"], res["n_gpus"], res["pairs_per_s"], res["roofline"]["launches"],
                                     res["ms_per_step"], res["roofline"]["evaluated_frac"],
-                                    res["speculation"]["scored_over_accepted"]]))
+                                    res["speculation"]["scored_over_accepted"],
+                                    res["speculation"]["solved_over_accepted"]]))
     dist.destroy_process_group()
 
 
 def test_two_rank_gather_and_summary(tmp_path):
     out = str(tmp_path / "res.npy")
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    value, n_gpus, pairs_per_s, launches, ms, evaluated, waste = np.load(out)
+    value, n_gpus, pairs_per_s, launches, ms, evaluated, waste, solved = np.load(out)
     assert n_gpus == 2
     assert value == (1000.0 + 2000.0) / 2.0  # all ranks' hypotheses / slowest rank
     assert pairs_per_s == 2 * 3 / 2.0
     assert launches == 8
     assert abs(ms - 2.0 / 3 * 1e3) < 1e-9
     assert evaluated == 0.5  # (4000 + 8000) / (8000 + 16000)
-    assert abs(waste - 3000.0 / 2100.0) < 1e-12  # scored / accepted hypotheses
+    assert abs(waste - 2700.0 / 2100.0) < 1e-12  # scored / accepted hypotheses
+    assert abs(solved - 3000.0 / 2100.0) < 1e-12  # solved / accepted hypotheses
 
 
 def test_single_rank_summary_fields():
@@ -59,7 +61,7 @@ def test_single_rank_summary_fields():
     import bench
 
     allv = np.array([[2.0, 3e5, 3e5, 30, 1.0, 100.0, 50.0, 3e5, 3e5 * 2000, 30, 90, 10, 5.0, 6.0, 3e5, 1.0, 2.0, 2000.0,
-                      5e4, 3, 2.0, 1e6, 2.4e6, 2.5e5]])
+                      5e4, 3, 2.0, 1e6, 2.4e6, 2.5e5, 2.75e5]])
     assert allv.shape[1] == len(bench.COUNTERS)
     res = bench.summarize(allv, bench.WORKLOADS["cal"], 3, 1, 1)
     for k in ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -74,7 +76,8 @@ def test_single_rank_summary_fields():
     assert abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-12
     assert abs(rf["evaluated_frac"] - 1e6 / 2.4e6) < 1e-12
     assert abs(rf["evaluated_bytes_per_launch"] - 3e5 * 2000 * 48 * (1e6 / 2.4e6) / 30) < 1e-3
-    assert abs(res["speculation"]["scored_over_accepted"] - 3e5 / 2.5e5) < 1e-12
+    assert abs(res["speculation"]["solved_over_accepted"] - 3e5 / 2.5e5) < 1e-12
+    assert abs(res["speculation"]["scored_over_accepted"] - 2.75e5 / 2.5e5) < 1e-12
 
 
 def test_scannet_summary_and_gathered_errors():

@@ -79,10 +79,15 @@ def _close(m, ref, variant, tol=1e-7, epi_only=False):
     return bool(ok)
 
 
-def _near_start(ref, m0):
+def _near_start(ref, m0, variant):
     """The oracle's minimum lies near the start: rotation within 10 degrees, scale
-    within a factor 2, offsets within 10 x (1 + |start|) of the start."""
+    and focals within a factor 2, offsets within 10 x (1 + |start|) of the start.
+    (A two-focal EPI_ONLY fit can run a focal into its 1e-6 bound: Sampson residuals
+    alone leave it nearly unobserved, and there implementations part at rounding.)"""
     if rot_angle_deg(ref["R"], m0.R()) > 10.0 or not 0.5 < ref["scale"] / m0.scale < 2.0:
+        return False
+    f0 = [None, (m0.focal, m0.focal), (m0.focal0, m0.focal1)][variant]
+    if f0 is not None and not all(0.5 < ref[k] / f < 2.0 for k, f in zip(("focal0", "focal1"), f0)):
         return False
     return all(abs(ref[k] - getattr(m0, k)) <= 10.0 * (1.0 + abs(getattr(m0, k))) for k in ("offset0", "offset1"))
 
@@ -124,7 +129,7 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
         kind, lists, m0 = cand
         ref, ran = oracle.least_squares(variant, *args, oracle_opts(o), oracle_cfg(c), kind, lists,
                                         _oracle_model(m0, variant))
-        if ran and not _near_start(ref, m0):
+        if ran and not _near_start(ref, m0, variant):
             continue
         probs.append(cand)
         refs.append((ref, ran))

@@ -109,7 +109,7 @@ int main(int argc, char **argv) {
         CHECK(hipEventRecord(ev[5]));
         pt_defl6_kernel<<<ns, 64>>>(d_pen2, true); // (the Hessenberg form for the lockstep kernel)
         CHECK(hipEventRecord(ev[6]));
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, d_c4, d_n4, kCandStride);
+        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c4, d_n4, kCandStride);
         CHECK(hipEventRecord(ev[7]));
         CHECK(hipEventSynchronize(ev[7]));
         if (timed)
@@ -177,6 +177,36 @@ int main(int argc, char **argv) {
     {
         const double wg = (double)((ns + 63) / 64) * reps;
         std::printf("lockstep kernel per workgroup: hqr %.0f ticks, %.1f rounds\n", prof[6] / wg, prof[7] / wg);
+    }
+    {
+        // the lockstep QR at other samples-per-wave packings: time and bit-equality
+        // against 64 per wave (d_c4 / d_n4 from the last run above)
+        std::vector<int> n64(ns), nx(ns);
+        std::vector<double> c64((size_t)ns * kCandStride), cx((size_t)ns * kCandStride);
+        CHECK(hipMemcpy(n64.data(), d_n4, ns * 4, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(c64.data(), d_c4, c64.size() * 8, hipMemcpyDeviceToHost));
+        for (int spw : {64, 32, 16, 8, 4, 2, 1, eig_spw(ns)}) {
+            float t = 0.f, tt = 0.f;
+            for (int r = 0; r < 4; ++r) {
+                CHECK(hipEventRecord(ev[0]));
+                pt_eig6_reg_kernel<<<(ns + spw - 1) / spw, 64>>>(d_pen2, ns, spw, d_c3, d_n3, kCandStride);
+                CHECK(hipEventRecord(ev[1]));
+                CHECK(hipEventSynchronize(ev[1]));
+                CHECK(hipEventElapsedTime(&t, ev[0], ev[1]));
+                if (r > 0) tt += t / 3;
+            }
+            CHECK(hipMemcpy(nx.data(), d_n3, ns * 4, hipMemcpyDeviceToHost));
+            CHECK(hipMemcpy(cx.data(), d_c3, cx.size() * 8, hipMemcpyDeviceToHost));
+            long same = 0;
+            for (int s2 = 0; s2 < ns; ++s2) {
+                bool eq = nx[s2] == n64[s2];
+                for (int k = 0; eq && k < nx[s2]; ++k)
+                    eq = cx[(size_t)s2 * kCandStride + 27 + k] == c64[(size_t)s2 * kCandStride + 27 + k];
+                same += eq;
+            }
+            std::printf("lockstep QR, %2d samples per wave (%d waves): %.1f us, %ld of %d root sets bit-identical to 64\n",
+                        spw, (ns + spw - 1) / spw, 1e3 * tt, same, ns);
+        }
     }
     std::vector<int> n1(ns), n2(ns);
     std::vector<double> c1((size_t)ns * kCandStride), c2((size_t)ns * kCandStride);

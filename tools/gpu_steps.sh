@@ -6,6 +6,7 @@ mkdir -p gpurun_out
 worst=0
 for spec in "$@"; do
   secs=${spec%%:*}; rest=${spec#*:}; log=${rest%%:*}; cmd=${rest#*:}
+  mkdir -p "gpurun_out/$(dirname "$log")"
   echo "== step $log ($secs s): $cmd"
   timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$log.log" 2>&1
   rc=$?
