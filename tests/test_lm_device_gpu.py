@@ -86,7 +86,7 @@ def _near_start(ref, m0, variant):
     alone leave it nearly unobserved, and there implementations part at rounding.)"""
     if rot_angle_deg(ref["R"], m0.R()) > 10.0 or not 0.5 < ref["scale"] / m0.scale < 2.0:
         return False
-    f0 = [None, (m0.focal, m0.focal), (m0.focal0, m0.focal1)][variant]
+    f0 = None if variant == 0 else (m0.focal, m0.focal) if variant == 1 else (m0.focal0, m0.focal1)
     if f0 is not None and not all(0.5 < ref[k] / f < 2.0 for k, f in zip(("focal0", "focal1"), f0)):
         return False
     return all(abs(ref[k] - getattr(m0, k)) <= 10.0 * (1.0 + abs(getattr(m0, k))) for k in ("offset0", "offset1"))
