@@ -92,6 +92,12 @@ def _near_start(ref, m0, variant):
     return all(abs(ref[k] - getattr(m0, k)) <= 10.0 * (1.0 + abs(getattr(m0, k))) for k in ("offset0", "offset1"))
 
 
+def _close_dicts(a, b, variant, tol=1e-7, epi_only=False):
+    mk = [madpose.PoseScaleOffset, madpose.PoseScaleOffsetSharedFocal, madpose.PoseScaleOffsetTwoFocal][variant]
+    foc = [[], [a["focal0"]], [a["focal0"], a["focal1"]]][variant]
+    return _close(mk(a["R"], a["t"], a["scale"], a["offset0"], a["offset1"], *foc), b, variant, tol, epi_only)
+
+
 def _oracle_model(m, variant):
     d = dict(R=m.R(), t=m.t(), scale=m.scale, offset0=m.offset0, offset1=m.offset1, focal0=1.0, focal1=1.0)
     if variant == 1:
@@ -131,6 +137,15 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
                                         _oracle_model(m0, variant))
         if ran and not _near_start(ref, m0, variant):
             continue
+        if ran:
+            # ... and that minimum is stable: the oracle restarted from its own result
+            # stays there (Sampson-only two-focal fits can sit on a ridge from which a
+            # restart runs off to focals ~0.05, where the implementations' rounding-level
+            # differences decide where they stop)
+            again, _ = oracle.least_squares(variant, *args, oracle_opts(o), oracle_cfg(c), kind, lists,
+                                            dict(ref))
+            if not _close_dicts(again, ref, variant, epi_only=lo_type == 1):
+                continue
         probs.append(cand)
         refs.append((ref, ran))
         if len(probs) == 24:
