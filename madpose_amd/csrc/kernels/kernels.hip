@@ -26,6 +26,8 @@
 #include "group_6pt.h"
 #include "group_tail.h"
 #include "eig6.h"
+#include "eig6_grp.h"
+#include "eig6_defl_grp.h"
 #include "lm_device.h"
 #include "kernels.h"
 
@@ -1016,9 +1018,30 @@ static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int
         pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, false);
         pt_eig6_kernel<<<nlist, 64, 0, s>>>(pen, cand, ncand, kCandStride);
     } else {
-        pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, true);
-        const int spw = eig_spw(nlist);
-        pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride);
+        // deflation + balance + Hessenberg on 16-lane groups (eig6_defl_grp.h);
+        // MADPOSE_DEFL_WAVE=1: one sample per wave (pt_defl6_kernel, A/B)
+        static const bool defl_wave = [] {
+            const char *e = std::getenv("MADPOSE_DEFL_WAVE");
+            return e && e[0] == '1';
+        }();
+        if (defl_wave)
+            pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, true);
+        else
+            pt_defl6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist);
+        // MADPOSE_EIG_GRP_MAX=n: the 16-lane group QR (eig6_grp.h, bit-identical
+        // eigenvalues) for batches of up to n samples.  Off by default: measured no faster
+        // than one sample per lane even at 512 samples (293 vs 282-368 us), 1.5x slower
+        // at 16384 (613 vs 388 us), profiles/r03/s4
+        static const int grp_max = [] {
+            const char *e = std::getenv("MADPOSE_EIG_GRP_MAX");
+            return e ? std::atoi(e) : 0;
+        }();
+        if (nlist <= grp_max) {
+            pt_eig6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist, cand, ncand, kCandStride);
+        } else {
+            const int spw = eig_spw(nlist);
+            pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride);
+        }
     }
 }
 

@@ -185,7 +185,37 @@ int main(int argc, char **argv) {
         std::vector<double> c64((size_t)ns * kCandStride), cx((size_t)ns * kCandStride);
         CHECK(hipMemcpy(n64.data(), d_n4, ns * 4, hipMemcpyDeviceToHost));
         CHECK(hipMemcpy(c64.data(), d_c4, c64.size() * 8, hipMemcpyDeviceToHost));
-        for (int spw : {64, 32, 16, 8, 4, 2, 1, eig_spw(ns)}) {
+        {
+            // the 16-lane group kernel: time and bit-equality against the lane kernel
+            float t = 0.f, tt = 0.f;
+            for (int r = 0; r < 4; ++r) {
+                CHECK(hipEventRecord(ev[0]));
+                pt_eig6_grp_kernel<<<(ns + 3) / 4, 64>>>(d_pen2, ns, d_c3, d_n3, kCandStride);
+                CHECK(hipEventRecord(ev[1]));
+                CHECK(hipEventSynchronize(ev[1]));
+                CHECK(hipEventElapsedTime(&t, ev[0], ev[1]));
+                if (r > 0) tt += t / 3;
+            }
+            CHECK(hipMemcpy(nx.data(), d_n3, ns * 4, hipMemcpyDeviceToHost));
+            CHECK(hipMemcpy(cx.data(), d_c3, cx.size() * 8, hipMemcpyDeviceToHost));
+            long same = 0, shown = 0;
+            for (int s2 = 0; s2 < ns; ++s2) {
+                bool eq = nx[s2] == n64[s2];
+                for (int k = 0; eq && k < nx[s2]; ++k)
+                    eq = cx[(size_t)s2 * kCandStride + 27 + k] == c64[(size_t)s2 * kCandStride + 27 + k];
+                same += eq;
+                if (!eq && shown++ < 3) {
+                    std::printf("  sample %d: group %d roots, lane %d:", s2, nx[s2], n64[s2]);
+                    for (int k = 0; k < nx[s2]; ++k) std::printf(" %.17g", cx[(size_t)s2 * kCandStride + 27 + k]);
+                    std::printf(" |");
+                    for (int k = 0; k < n64[s2]; ++k) std::printf(" %.17g", c64[(size_t)s2 * kCandStride + 27 + k]);
+                    std::printf("\n");
+                }
+            }
+            std::printf("group QR (4 samples per wave, %d waves): %.1f us, %ld of %d root sets bit-identical to the lane kernel\n",
+                        (ns + 3) / 4, 1e3 * tt, same, ns);
+        }
+        for (int spw : {64, 16, 2, eig_spw(ns)}) {
             float t = 0.f, tt = 0.f;
             for (int r = 0; r < 4; ++r) {
                 CHECK(hipEventRecord(ev[0]));
@@ -207,6 +237,59 @@ int main(int argc, char **argv) {
             std::printf("lockstep QR, %2d samples per wave (%d waves): %.1f us, %ld of %d root sets bit-identical to 64\n",
                         spw, (ns + spw - 1) / spw, 1e3 * tt, same, ns);
         }
+    }
+    {
+        // group deflation (+ balance + Hessenberg) against the one-wave kernel: time, and
+        // the roots after the lane QR on either Hessenberg form (1e-9 relative)
+        double *d_pen3;
+        CHECK(hipMalloc(&d_pen3, (size_t)ns * kPenStride * 8));
+        pt_pencil6_kernel<<<(ns + kGrpPerWg - 1) / kGrpPerWg, 64>>>(D, d_list, ns, d_samples, d_c2, kCandStride, d_pen);
+        CHECK(hipMemcpy(d_pen2, d_pen, (size_t)ns * kPenStride * 8, hipMemcpyDeviceToDevice));
+        CHECK(hipMemcpy(d_pen3, d_pen, (size_t)ns * kPenStride * 8, hipMemcpyDeviceToDevice));
+        float tw = 0.f, tg = 0.f, t = 0.f;
+        for (int r = 0; r < 4; ++r) {
+            CHECK(hipMemcpy(d_pen2, d_pen, (size_t)ns * kPenStride * 8, hipMemcpyDeviceToDevice));
+            CHECK(hipMemcpy(d_pen3, d_pen, (size_t)ns * kPenStride * 8, hipMemcpyDeviceToDevice));
+            CHECK(hipEventRecord(ev[0]));
+            pt_defl6_kernel<<<ns, 64>>>(d_pen2, true);
+            CHECK(hipEventRecord(ev[1]));
+            pt_defl6_grp_kernel<<<(ns + 3) / 4, 64>>>(d_pen3, ns);
+            CHECK(hipEventRecord(ev[2]));
+            CHECK(hipEventSynchronize(ev[2]));
+            CHECK(hipEventElapsedTime(&t, ev[0], ev[1]));
+            if (r > 0) tw += t / 3;
+            CHECK(hipEventElapsedTime(&t, ev[1], ev[2]));
+            if (r > 0) tg += t / 3;
+        }
+        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c3, d_n3, kCandStride);
+        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen3, ns, 64, d_c4, d_n4, kCandStride);
+        CHECK(hipDeviceSynchronize());
+        std::vector<int> na(ns), nb(ns);
+        std::vector<double> ca((size_t)ns * kCandStride), cb((size_t)ns * kCandStride);
+        CHECK(hipMemcpy(na.data(), d_n3, ns * 4, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(nb.data(), d_n4, ns * 4, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(ca.data(), d_c3, ca.size() * 8, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(cb.data(), d_c4, cb.size() * 8, hipMemcpyDeviceToHost));
+        long same = 0, shown = 0, ra = 0, rb = 0;
+        for (int s2 = 0; s2 < ns; ++s2) {
+            ra += na[s2];
+            rb += nb[s2];
+            bool eq = na[s2] == nb[s2];
+            for (int k = 0; eq && k < na[s2]; ++k)
+                eq = std::fabs(ca[(size_t)s2 * kCandStride + 27 + k] - cb[(size_t)s2 * kCandStride + 27 + k]) <=
+                     1e-9 * std::fabs(ca[(size_t)s2 * kCandStride + 27 + k]);
+            same += eq;
+            if (!eq && shown++ < 3) {
+                std::printf("  sample %d: wave deflation %d roots, group %d:", s2, na[s2], nb[s2]);
+                for (int k = 0; k < na[s2]; ++k) std::printf(" %.12g", ca[(size_t)s2 * kCandStride + 27 + k]);
+                std::printf(" |");
+                for (int k = 0; k < nb[s2]; ++k) std::printf(" %.12g", cb[(size_t)s2 * kCandStride + 27 + k]);
+                std::printf("\n");
+            }
+        }
+        std::printf("deflation + Hessenberg: one wave per sample %.1f us, 16-lane groups %.1f us; roots after the "
+                    "lane QR agree (1e-9) on %ld of %d samples (roots %ld / %ld)\n",
+                    1e3 * tw, 1e3 * tg, same, ns, ra, rb);
     }
     std::vector<int> n1(ns), n2(ns);
     std::vector<double> c1((size_t)ns * kCandStride), c2((size_t)ns * kCandStride);
