@@ -17,6 +17,7 @@
 //
 // Local optimisation stays on the host (north star); its full-data sweeps
 // (ScoreModel / GetInliers) run on the GPU through the single-model sweep kernel.
+#include <immintrin.h>
 #include "engine.h"
 
 #include <hip/hip_runtime.h>
@@ -44,6 +45,12 @@
 #include "rng.h"
 
 namespace mp {
+
+// kCompactLut[m]: the lane numbers of the set bits of the 4-bit mask m, ascending
+// (inliers(): AVX2 stream compaction of the error rows)
+alignas(16) static const int32_t kCompactLut[16][4] = {
+    {0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 1, 0, 0}, {2, 0, 0, 0}, {0, 2, 0, 0}, {1, 2, 0, 0}, {0, 1, 2, 0},
+    {3, 0, 0, 0}, {0, 3, 0, 0}, {1, 3, 0, 0}, {0, 1, 3, 0}, {2, 3, 0, 0}, {0, 2, 3, 0}, {1, 2, 3, 0}, {0, 1, 2, 3}};
 
 #define MP_HIP(expr)                                                                                                    \
     do {                                                                                                               \
@@ -767,15 +774,28 @@ class Run {
         // Branch-free compaction: whether a correspondence is an inlier is close to a
         // coin flip along the index, so a conditional push_back mispredicts about every
         // other element (measured on the build host, 3 x 2000 errors at ~50 % inliers:
-        // 17.8 us branchy, 5.5 us like this).  Same lists (ascending indices).
+        // 17.8 us branchy, 5.5 us branch-free scalar).  AVX2: four errors per compare,
+        // the lanes below the threshold appended as one 4-index store through a table of
+        // the 16 masks (7.1-7.9 -> 3.1 us per 3 x 2000 on the build container).  Same
+        // lists (ascending indices).
         int c = 0;
+        const __m128i step = _mm_set1_epi32(4);
         for (int t = 0; t < 3; ++t) {
             std::vector<int> &o = out[t];
-            o.resize(n_);
-            int *w = o.data(), k = 0;
+            o.resize(n_ + 4);
+            int *w = o.data(), k = 0, i = 0;
             const double *et = e + (size_t)t * n_;
             const double th = thr[t];
-            for (int i = 0; i < n_; ++i) {
+            const __m256d tv = _mm256_set1_pd(th);
+            __m128i base = _mm_setzero_si128();
+            for (; i + 4 <= n_; i += 4) {
+                const int msk = _mm256_movemask_pd(_mm256_cmp_pd(_mm256_loadu_pd(et + i), tv, _CMP_LT_OQ));
+                _mm_storeu_si128((__m128i *)(w + k),
+                                 _mm_add_epi32(_mm_load_si128((const __m128i *)kCompactLut[msk]), base));
+                k += __builtin_popcount((unsigned)msk);
+                base = _mm_add_epi32(base, step);
+            }
+            for (; i < n_; ++i) {
                 w[k] = i;
                 k += et[i] < th;
             }
