@@ -39,8 +39,8 @@ def fit(x, y):
     return float(c[0]), float(c[1])
 
 
-def main(sq, fetch, out, source):
-    want = "score_batch_kernel<0, 10, true>"
+def main(sq, fetch, out, source, want="score_batch_kernel<0, 10, true, true>"):
+    # (round 2's kernel had three template arguments: "score_batch_kernel<0, 10, true>")
     d, meta = per_dispatch(sq, want)
     f, fmeta = per_dispatch(fetch, want)
     wg = [meta[k][0] for k in d]
@@ -84,4 +84,4 @@ def main(sq, fetch, out, source):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
