@@ -219,7 +219,11 @@ def summarize(allv, wl, steps, warmup, world):
     ev_share = float(c["model_trips"].sum()) / full_trips if full_trips > 0 else 1.0
     full_bytes = float(c["prof_correspondences"].sum()) * BYTES_PER_CORR
     achieved = full_bytes * ev_share / (score_ms * 1e-3) / 1e9 if score_ms > 0 else 0.0
-    effective = full_bytes / (score_ms * 1e-3) / 1e9 if score_ms > 0 else 0.0
+    # effective: the algorithmic 48 N bytes of every hypothesis the launches scored (the
+    # record skip's iterations, never scored, are not credited)
+    hyp = float(c["prof_hypotheses"].sum())
+    scored_share = float(c["prof_scored"].sum()) / hyp if hyp > 0 else 1.0
+    effective = full_bytes * scored_share / (score_ms * 1e-3) / 1e9 if score_ms > 0 else 0.0
     launches = int(c["prof_batches"].sum())
     traffic, traffic_note = None, None
     tm = pmc_traffic_model()

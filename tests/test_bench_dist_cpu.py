@@ -70,9 +70,10 @@ def test_single_rank_summary_fields():
     assert res["scaling"] == "weak" and res["dtype"] == "f64" and res["vs_baseline"] is None
     rf = res["roofline"]
     # achieved: the bytes the early-exit kernel read (the evaluated share of the full
-    # figure) over the score time; effective_GBps credits the full figure
-    assert abs(rf["effective_GBps"] - 3e5 * 2000 * 48 / 0.1 / 1e9) < 1e-6
-    assert abs(rf["achieved"] - rf["effective_GBps"] * 1e6 / 2.4e6) < 1e-6
+    # figure) over the score time; effective_GBps credits the full figure of the
+    # hypotheses that were scored (2.75e5 of 3e5: the rest were record-skipped)
+    assert abs(rf["effective_GBps"] - 2.75e5 * 2000 * 48 / 0.1 / 1e9) < 1e-6
+    assert abs(rf["achieved"] - 3e5 * 2000 * 48 / 0.1 / 1e9 * 1e6 / 2.4e6) < 1e-6
     assert abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-12
     assert abs(rf["evaluated_frac"] - 1e6 / 2.4e6) < 1e-12
     assert abs(rf["evaluated_bytes_per_launch"] - 3e5 * 2000 * 48 * (1e6 / 2.4e6) / 30) < 1e-3
