@@ -360,6 +360,9 @@ struct DeviceCtx {
     double *h_err = nullptr, *h_score1 = nullptr;
     ScoreRec *h_rec1 = nullptr;
     Model *h_model1 = nullptr;
+    // score_batch writes the models of the iterations that beat the pre-batch best here
+    // (mapped pinned memory, one slot per iteration of the batch)
+    Model *h_recmodel = nullptr, *d_recmodel = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr}; // solve start / score start / score end
     // the MD solver runs on md_stream, concurrently with the point-solver stages
     hipStream_t md_stream = nullptr;
@@ -374,7 +377,7 @@ struct DeviceCtx {
                         (void *)d_pt_valid, (void *)d_pt_slots})
             if (p) hipFree(p);
         for (void *p : {(void *)h_samples, (void *)h_res, (void *)h_work, (void *)h_err,
-                        (void *)h_score1, (void *)h_rec1, (void *)h_model1})
+                        (void *)h_score1, (void *)h_rec1, (void *)h_model1, (void *)h_recmodel})
             if (p) hipHostFree(p);
         d_pair = d_err = d_scores = d_score1 = nullptr;
         d_samples = d_counts = nullptr;
@@ -392,6 +395,7 @@ struct DeviceCtx {
         h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
         h_model1 = nullptr;
+        h_recmodel = d_recmodel = nullptr;
         for (auto &sl : sweep_slot) sl.release();
         cap_n = 0;
         cap_b = cap_m = 0;
@@ -430,6 +434,8 @@ struct DeviceCtx {
         MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_model1, sizeof(Model) * 64, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_recmodel, sizeof(Model) * (size_t)bb, hipHostMallocMapped | hipHostMallocCoherent));
+        MP_HIP(hipHostGetDevicePointer((void **)&d_recmodel, h_recmodel, 0));
         // (a stream of its own: the post-LO batch runs on `stream` while LO sweeps)
         sweep_slot[0].ensure(nn, nullptr);
         cap_n = nn;
@@ -1187,13 +1193,22 @@ class Run {
         if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
         MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res, best,
-                                  prof ? X_.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi));
+                                  prof ? X_.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
+                                  X_.d_models, X_.d_recmodel));
         if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
         MP_HIP(hipMemcpyAsync(X_.h_res, X_.d_res, sizeof(IterResult) * B, hipMemcpyDeviceToHost, s));
         if (prof) MP_HIP(hipMemcpyAsync(X_.h_work, X_.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     }
 
+    // the model of a new best: score_batch wrote it to the mapped record slot of its
+    // iteration (the batch's stream has been synchronized); MADPOSE_FETCH_MODEL=1 copies
+    // it from the device instead (A/B)
     Model fetch_model(int b, int slot) {
+        static const bool copy = [] {
+            const char *e = std::getenv("MADPOSE_FETCH_MODEL");
+            return e && e[0] == '1';
+        }();
+        if (!copy) return X_.h_recmodel[b];
         MP_HIP(hipMemcpyAsync(X_.h_model1, X_.d_models + (size_t)b * maxm_ + slot, sizeof(Model),
                               hipMemcpyDeviceToHost, X_.stream));
         MP_HIP(hipStreamSynchronize(X_.stream));

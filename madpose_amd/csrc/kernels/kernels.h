@@ -36,10 +36,13 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
 // exit, kernels.hip ScoreBound), reporting DBL_MAX.  work (nullable): per iteration
 // the (model, 256-correspondence trip) pairs evaluated.  rec (nullable): the record
 // word of a batch that is cut at its first new best (kernels.hip ScoreBound), with
-// epoch_hi = ~epoch, a value unique to the batch.
+// epoch_hi = ~epoch, a value unique to the batch.  rec_out (nullable, device-mapped
+// host memory, nb Models): iterations whose best beats `best` write that model (from
+// models, nb x maxm) to rec_out[b].
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
-                              int *work, unsigned long long *rec = nullptr, unsigned epoch_hi = 0);
+                              int *work, unsigned long long *rec = nullptr, unsigned epoch_hi = 0,
+                              const Model *models = nullptr, Model *rec_out = nullptr);
 // single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);

@@ -551,6 +551,11 @@ struct ScoreBound {
     unsigned long long *rec; // nullptr: no record skip
     unsigned epoch_hi;       // ~epoch of this batch
     double best;             // the pre-batch best (exact)
+    // record models (nullable): an iteration whose best beats `best` writes that model
+    // to rec_out[b] (mapped host memory), so the host reads a new best's model without
+    // a copy round trip (every new best of a batch beats the pre-batch best)
+    const Model *models;
+    Model *rec_out;
 };
 
 // EXIT = false (no finite bound yet, or MADPOSE_SCORE_EXIT=0): the plain sweep,
@@ -685,6 +690,12 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         if (sb.work) sb.work[b] = work;
         if (sb.rec && bs < sb.best)
             atomicMin(sb.rec, ((unsigned long long)sb.epoch_hi << 32) | (unsigned long long)(unsigned)b);
+        if (sb.rec_out && bs < sb.best) {
+            const double *src = (const double *)(sb.models + (size_t)b * MAXM + bi);
+            double *dst = (double *)(sb.rec_out + b);
+#pragma unroll
+            for (int q = 0; q < (int)(sizeof(Model) / sizeof(double)); ++q) dst[q] = src[q];
+        }
     }
 }
 
@@ -1118,7 +1129,8 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
 
 // Early-exit schedule (MADPOSE_SCORE_EXIT=0 turns the exit off; MADPOSE_SCORE_CHECK
 // "first,every" in trips of 256 correspondences overrides the schedule).
-static ScoreBound score_bound(double best, int n, int *work, unsigned long long *rec, unsigned epoch_hi) {
+static ScoreBound score_bound(double best, int n, int *work, unsigned long long *rec, unsigned epoch_hi,
+                              const Model *models, Model *rec_out) {
     static const int mode = [] {
         const char *e = std::getenv("MADPOSE_SCORE_EXIT");
         return (e && e[0] == '0') ? 0 : 1;
@@ -1149,16 +1161,19 @@ static ScoreBound score_bound(double best, int n, int *work, unsigned long long 
     sb.rec = skip ? rec : nullptr;
     sb.epoch_hi = epoch_hi;
     sb.best = best;
+    sb.models = models;
+    sb.rec_out = rec_out;
     return sb;
 }
 
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
-                              int *work, unsigned long long *rec, unsigned epoch_hi) {
+                              int *work, unsigned long long *rec, unsigned epoch_hi, const Model *models,
+                              Model *rec_out) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
     const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
-    const ScoreBound sb = score_bound(best, C.n, work, rec, epoch_hi);
+    const ScoreBound sb = score_bound(best, C.n, work, rec, epoch_hi, models, rec_out);
     const bool exit = sb.cut < __builtin_inf();
     auto go = [&](auto V, auto M, auto F) {
         constexpr int kV = decltype(V)::value, kM = decltype(M)::value;
