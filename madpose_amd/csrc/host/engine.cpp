@@ -1353,8 +1353,9 @@ void Run::run(Model *best, Stats *S) {
             MP_HIP(hipEventElapsedTime(&ms_score, X_.ev[1], X_.ev[2]));
             uint64_t h = 0, trips = 0, scored = 0;
             for (uint32_t q = 0; q < B; ++q) {
+                // (record-skipped iterations report their partial trips negated)
                 h += (uint64_t)X_.h_res[q].count;
-                trips += (uint64_t)X_.h_work[q];
+                trips += (uint64_t)std::abs(X_.h_work[q]);
                 if (X_.h_work[q] > 0) scored += (uint64_t)X_.h_res[q].count;
             }
             std::lock_guard<std::mutex> lk(g_prof_mu);

@@ -539,8 +539,10 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
 // batch at the first iteration whose best beats the pre-batch best
 // (src/hybrid_ransac.h:123-156) and discards every later one.  A workgroup whose
 // iteration scores below `best` (the same comparison on the same doubles as the
-// host's) publishes its index by an atomic minimum; a workgroup that starts after an
-// earlier record was published skips its sweep.  Iterations up to the first record
+// host's) publishes its index by an atomic minimum; a workgroup that sees an earlier
+// published record at one of its early-exit checks (the word is read at the start and
+// after each check, the check's barrier shares the verdict) stops there.  Only
+// batches with a finite pre-batch best (the EXIT kernel) skip.  Iterations up to the first record
 // are always scored in full, so the host's walk never reads a skipped one.  The word
 // carries an epoch in its high half (complemented, so a new batch's first record
 // always wins the minimum) and needs no reset between batches.
@@ -574,21 +576,13 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         }
         return;
     }
-    if (sb.rec) {
-        __shared__ int s_skip;
-        if (threadIdx.x == 0) {
-            const unsigned long long k = __hip_atomic_load(sb.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_skip = (unsigned)(k >> 32) == sb.epoch_hi && (int)(unsigned)(k & 0xffffffffu) < b;
-        }
-        __syncthreads();
-        if (s_skip) { // (uniform) a record earlier in the batch: this iteration is discarded
-            if (threadIdx.x == 0) {
-                res[b] = IterResult{DBL_MAX, 0, nm};
-                if (sb.work) sb.work[b] = 0;
-            }
-            return;
-        }
-    }
+    // the record word, read at the start and decided on at the early-exit checks (their
+    // barrier publishes thread 0's verdict), so the load's latency hides behind the
+    // first trips instead of stalling the workgroup at entry; reloaded after each check
+    unsigned long long recw = ~0ull;
+    if (EXIT && sb.rec && threadIdx.x == 0) recw = __hip_atomic_load(sb.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __shared__ int s_skip[2];
+    bool skipped = false;
     const ScoreRec *R = recs + (size_t)b * MAXM;
     double acc[MAXM];
 #pragma unroll
@@ -638,6 +632,10 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         const int done = trip + 1;
         if (done < ntrip && done >= sb.first && (done - sb.first) % sb.every == 0) {
             const int par = checks & 1; // double-buffered: one barrier per check
+            if (threadIdx.x == 0) {
+                s_skip[par] = (unsigned)(recw >> 32) == sb.epoch_hi && (int)(unsigned)(recw & 0xffffffffu) < b;
+                if (sb.rec) recw = __hip_atomic_load(sb.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
 #pragma unroll
             for (int m = 0; m < MAXM; ++m) {
                 if ((live >> m) & 1u) {
@@ -657,6 +655,10 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                 }
             }
             live = __builtin_amdgcn_readfirstlane(keep);
+            if (s_skip[par]) { // (uniform) a record earlier in the batch: this iteration is discarded
+                live = 0;
+                skipped = true;
+            }
             ++checks;
             if (live == 0) break;
         }
@@ -686,11 +688,12 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                 bi = m;
             }
         }
-        res[b] = IterResult{bs, bi, nm};
-        if (sb.work) sb.work[b] = work;
-        if (sb.rec && bs < sb.best)
+        res[b] = skipped ? IterResult{DBL_MAX, 0, nm} : IterResult{bs, bi, nm};
+        // (a record-skipped iteration reports its trips negated: profiling only)
+        if (sb.work) sb.work[b] = skipped ? -work : work;
+        if (sb.rec && !skipped && bs < sb.best)
             atomicMin(sb.rec, ((unsigned long long)sb.epoch_hi << 32) | (unsigned long long)(unsigned)b);
-        if (sb.rec_out && bs < sb.best) {
+        if (sb.rec_out && !skipped && bs < sb.best) {
             const double *src = (const double *)(sb.models + (size_t)b * MAXM + bi);
             double *dst = (double *)(sb.rec_out + b);
 #pragma unroll
