@@ -515,6 +515,9 @@ MP_HD bool point_model_tail_r(const double (&p0)[K][2], const double (&p1)[K][2]
 #pragma unroll
     for (int j = 0; j < K; ++j) triangulate(m.R, m.t, fa, fb, p0[j], p1[j], X[j]);
     double t[3] = {m.t[0], m.t[1], m.t[2]};
+    // (the depth fit's outputs are written to m once, at the end: assigned in both
+    // branches they kept three fields of m in scratch on the device)
+    double sc_o, o0_o, o1_o;
     if (!use_shift) {
         double num = 0, den = 0;
 #pragma unroll
@@ -533,8 +536,8 @@ MP_HD bool point_model_tail_r(const double (&p0)[K][2], const double (&p1)[K][2]
             num += use[j] ? dd1[j] * zz : 0.0;
             den += use[j] ? dd1[j] * dd1[j] : 0.0;
         }
-        m.scale = sum(num) / sum(den);
-        m.offset0 = m.offset1 = 0.0;
+        sc_o = sum(num) / sum(den);
+        o0_o = o1_o = 0.0;
     } else {
 #pragma unroll
         for (int j = 0; j < K; ++j) z[j] = X[j][2];
@@ -553,10 +556,13 @@ MP_HD bool point_model_tail_r(const double (&p0)[K][2], const double (&p1)[K][2]
         ls_affine<K>(dd1, z, use, n, sum, &sc, &b1);
         const double offset1 = b1 / sc;
         if (min_depth_constraint && offset1 < -min_depth[1]) return false;
-        m.scale = sc;
-        m.offset0 = offset0;
-        m.offset1 = offset1;
+        sc_o = sc;
+        o0_o = offset0;
+        o1_o = offset1;
     }
+    m.scale = sc_o;
+    m.offset0 = o0_o;
+    m.offset1 = o1_o;
     m.t[0] = t[0];
     m.t[1] = t[1];
     m.t[2] = t[2];

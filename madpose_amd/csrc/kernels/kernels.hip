@@ -1151,11 +1151,15 @@ static ScoreBound score_bound(double best, int n, int *work, unsigned long long 
     const bool on = mode != 0 && best < DBL_MAX && best >= 0.0;
     sb.cut = on ? best * (1.0 + 1e-12) : __builtin_inf();
     const int ntrip = (n + kBlock - 1) / kBlock;
-    // default: first check after a quarter of the trips, then every quarter (each
-    // check costs a wave reduction per live model and a barrier; tools/score_bench.hip:
-    // at N = 2000 checks after trips 2, 4, 6 beat every trip from 2 on, 209 vs 233 us)
-    sb.first = sched[0] > 0 ? sched[0] : std::max(1, ntrip / 4);
-    sb.every = sched[0] > 0 ? sched[1] : std::max(1, ntrip / 4);
+    // default: a check every quarter of the trips, at most every two trips (512
+    // correspondences; each check costs a wave reduction per live model and a barrier).
+    // tools/score_bench.hip, round 2: at N = 2000 checks after trips 2, 4, 6 beat every
+    // trip from 2 on, 209 vs 233 us; round 3 (profiles/r03/s11, HIP-event launch
+    // averages): cal 44.7 / 45.5 / 47.7 us at 2,2 / 1,1 / 3,3, sf 33.1 / 35.2 us at 2,2 /
+    // 1,1, tf (N = 4000) 56.7 us at 2,2 against 60.2 at 4,4
+    const int q = std::min(2, std::max(1, ntrip / 4));
+    sb.first = sched[0] > 0 ? sched[0] : q;
+    sb.every = sched[0] > 0 ? sched[1] : q;
     sb.work = work;
     static const bool skip = [] {
         const char *e = std::getenv("MADPOSE_RECORD_SKIP");
