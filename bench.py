@@ -578,6 +578,11 @@ def spawn_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # ranks pinned to one device (the one-card rehearsal) share one host CPU share,
+        # where spinning LM workers cost more than they save; the
+        # process's affinity mask does not show the share, so say it here
+        if "MADPOSE_BENCH_DEVICE" in os.environ and "MADPOSE_LO_SPIN" not in os.environ:
+            env["MADPOSE_LO_SPIN"] = "0"
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
     rcs = [p.wait() for p in procs]
     bad = [rc for rc in rcs if rc != 0]
