@@ -665,8 +665,10 @@ def solve_scale_shift_pose_two_focal_4p4d(x_homo, y_homo, depth_x, depth_y):
     return _solve_pose(L.TWO_FOCAL, x_homo, y_homo, depth_x, depth_y, alt=2)
 
 
-def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, models, with_errors=False):
-    """Device ScoreModel over explicit models given in problem units (tests / diagnostics)."""
+def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, models, with_errors=False,
+                 host_lo=False):
+    """Device ScoreModel over explicit models given in problem units (tests / diagnostics).
+    host_lo=True: the engine's host LO sweep instead (mp_debug_lo_sweep; no device)."""
     x0 = _pts(x0, "x0")
     x1 = _pts(x1, "x1")
     n = x0.shape[0]
@@ -680,9 +682,14 @@ def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_confi
     errors = np.zeros((max(nm, 1), 3, n)) if with_errors else None
     o = options._to_c()
     c = (est_config or EstimatorConfig())._to_c()
-    code = L.lib().mp_score_models(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1), ctypes.byref(o),
-                                   ctypes.byref(c), arr, nm, _dp(scores),
-                                   _dp(errors) if with_errors else None, _DEFAULT_DEVICE)
+    if host_lo:
+        code = L.lib().mp_debug_lo_sweep(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1),
+                                         ctypes.byref(o), ctypes.byref(c), arr, nm, _dp(scores),
+                                         _dp(errors) if with_errors else None)
+    else:
+        code = L.lib().mp_score_models(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1),
+                                       ctypes.byref(o), ctypes.byref(c), arr, nm, _dp(scores),
+                                       _dp(errors) if with_errors else None, _DEFAULT_DEVICE)
     L.check(code)
     return (scores[:nm], errors[:nm]) if with_errors else scores[:nm]
 

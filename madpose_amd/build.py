@@ -22,6 +22,11 @@ SOURCES = [
     os.path.join(CSRC, "host", "lm.cpp"),
     os.path.join(CSRC, "capi.cpp"),
 ]
+# host-only translation units (plain C++, no device pass): the LO sweep carries an
+# AVX-512 function beside its x86-64-v3 baseline, chosen at run time (host/lo_sweep.cpp)
+HOST_SOURCES = [
+    os.path.join(CSRC, "host", "lo_sweep.cpp"),
+]
 HEADERS = [
     os.path.join(dp, f)
     for dp, _, fs in os.walk(CSRC)
@@ -30,6 +35,9 @@ HEADERS = [
 ] + [os.path.join(ROOT, "include", "madpose_mi355x.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+HOSTCXX = os.environ.get("MADPOSE_HOSTCXX", "/opt/rocm/llvm/bin/clang++")
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function",
+              "-march=x86-64-v3", "-mprefer-vector-width=512"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"), "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result",
@@ -48,7 +56,10 @@ def _newer(target, deps):
 def _compile(src):
     obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
     if _newer(obj, [src, __file__] + HEADERS):
-        cmd = [HIPCC, "-x", "hip"] + FLAGS + ["-c", src, "-o", obj]
+        if src in HOST_SOURCES:
+            cmd = [HOSTCXX] + HOST_FLAGS + ["-c", src, "-o", obj]
+        else:
+            cmd = [HIPCC, "-x", "hip"] + FLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
@@ -58,7 +69,7 @@ def _compile(src):
 def build_library(verbose=False):
     os.makedirs(OBJDIR, exist_ok=True)
     with ThreadPoolExecutor(max_workers=4) as ex:
-        objs = list(ex.map(_compile, SOURCES))
+        objs = list(ex.map(_compile, SOURCES + HOST_SOURCES))
     if _newer(LIB, objs):
         cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -289,9 +289,21 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
         mp::PairInput in = make_input(variant, n, x0, x1, d0, d1, md, cam0, cam1);
         std::vector<mp::Model> ms(num_models);
         std::memcpy(ms.data(), models, sizeof(mp_model) * num_models);
-        mp::score_models(in, to_opts(options), to_cfg(config), ms.data(), num_models, scores, errors, device, nullptr);
+        if (device == -1000) // mp_debug_lo_sweep
+            mp::lo_sweep_models(in, to_opts(options), to_cfg(config), ms.data(), num_models, scores, errors);
+        else
+            mp::score_models(in, to_opts(options), to_cfg(config), ms.data(), num_models, scores, errors, device,
+                             nullptr);
         return MP_OK;
     });
+}
+
+int mp_debug_lo_sweep(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
+                      const double *cam0, const double *cam1, const mp_ransac_options *options,
+                      const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
+                      double *errors) {
+    return mp_score_models(variant, n, x0, x1, d0, d1, cam0, cam1, options, config, models, num_models, scores, errors,
+                           -1000);
 }
 
 int mp_lm_refine_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,

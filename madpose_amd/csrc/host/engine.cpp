@@ -42,6 +42,7 @@
 #include "../include/mp_score.h"
 #include "../kernels/kernels.h"
 #include "batch_draw.h"
+#include "lo_sweep.h"
 #include "rng.h"
 
 namespace mp {
@@ -589,7 +590,10 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
             H.x0[2 * i + 1] = a1;
             H.x1[2 * i] = b0;
             H.x1[2 * i + 1] = b1;
-            scale += std::sqrt(a0 * a0 + a1 * a1) + std::sqrt(b0 * b0 + b1 * b1);
+            // (two accumulations per correspondence, as PoseLib's normalize_points and the
+            // oracle: the scale, hence every normalized coordinate, to the bit)
+            scale += std::sqrt(a0 * a0 + a1 * a1);
+            scale += std::sqrt(b0 * b0 + b1 * b1);
         }
         scale = (n > 0) ? scale / (std::sqrt(2.0) * n) : 1.0;
         for (int i = 0; i < 2 * n; ++i) {
@@ -607,7 +611,8 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
     std::memcpy(H.K0i, C.K0i, sizeof(H.K0i));
     std::memcpy(H.K1i, C.K1i, sizeof(H.K1i));
     const double w0 = o.data_type_weights[0];
-    const double ws = o.data_type_weights[1] * 2.0 * thr0 / thr1;
+    // data_type_weights_[1] *= 2 * thr0 / thr1 (src/hybrid_pose_estimator.cpp:16-17)
+    const double ws = o.data_type_weights[1] * (2 * thr0 / thr1);
     H.sampson_squared_weight = ws;
     C.thr[0] = C.thr[1] = thr0;
     C.thr[2] = thr1;
@@ -708,7 +713,8 @@ class Run {
         Model model;
         bool valid = false;
         double score = 0.0;
-        const double *err = nullptr; // the slot buffer holding the last result
+        const double *err = nullptr; // the buffer holding the last result
+        std::vector<double> herr;    // host sweeps' errors (3 x n)
         uint64_t count = 0;
         double t[3] = {0, 0, 0}; // launch / wait / copy seconds (MADPOSE_SWEEP_TIMING)
     };
@@ -720,12 +726,33 @@ class Run {
     double lo_t_[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool lo_parallel_ = true;
 
+    // LO sweeps on the issuing thread's core (host/lo_sweep.h; the default) or through
+    // the device kernel sweep_host (MADPOSE_LO_SWEEP=device, A/B)
+    bool host_sweep_ = true;
+    LoSweepData hsw_;
     const double *sweep(Lane &L, const Model &m, double *score) {
         if (L.valid && std::memcmp(&m, &L.model, sizeof(Model)) == 0) {
             *score = L.score;
             return L.err;
         }
         auto t_sw = Clock::now();
+        if (host_sweep_) {
+            if (L.herr.size() < 3 * (size_t)n_) L.herr.resize(3 * (size_t)n_);
+            L.score = lo_sweep(P_.C, hsw_, m, L.herr.data());
+            L.err = L.herr.data();
+            L.model = m;
+            L.valid = true;
+            L.count++;
+            const double dt = secs(t_sw);
+            L.t[1] += dt;
+            if (g_prof_on.load(std::memory_order_relaxed)) {
+                std::lock_guard<std::mutex> lk(g_prof_mu);
+                g_prof.sweeps += 1;
+                g_prof.sweep_wall_ms += 1e3 * dt;
+            }
+            *score = L.score;
+            return L.err;
+        }
         ScoreRec rec;
         prepare_score_rec(P_.C, m, rec);
         SweepSlot &sl = *L.slot;
@@ -1245,6 +1272,8 @@ void Run::run(Model *best, Stats *S) {
         lo_parallel_ = !(e && e[0] == '0') && o_.num_lo_steps > 1;
         const char *d = std::getenv("MADPOSE_DEVICE_LM");
         device_lm_ = d && d[0] == '1';
+        const char *hs = std::getenv("MADPOSE_LO_SWEEP");
+        host_sweep_ = !(hs && std::strcmp(hs, "device") == 0);
     }
     if (lo_parallel_) {
         const int nl = lo_lanes_setting();
@@ -1255,6 +1284,7 @@ void Run::run(Model *best, Stats *S) {
         }
     }
     upload_pair(X_, P_, &D_);
+    if (host_sweep_) lo_sweep_prepare(P_.C, P_.H.x0.data(), P_.H.x1.data(), P_.H.d0.data(), P_.H.d1.data(), &hsw_);
     rs_.n = n_;
     rs_.seed(o_.random_seed);
 
@@ -1592,6 +1622,19 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
         }
     }
     MP_HIP(hipStreamSynchronize(X.stream));
+}
+
+void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
+                     int nm, double *scores, double *errors) {
+    validate(in, opts);
+    Problem P = make_problem(in, opts, cfg);
+    LoSweepData D;
+    lo_sweep_prepare(P.C, P.H.x0.data(), P.H.x1.data(), P.H.d0.data(), P.H.d1.data(), &D);
+    std::vector<double> err(3 * (size_t)std::max<int64_t>(in.n, 1));
+    for (int m = 0; m < nm; ++m) {
+        scores[m] = lo_sweep(P.C, D, models[m], err.data());
+        if (errors) std::memcpy(errors + (size_t)m * 3 * in.n, err.data(), sizeof(double) * 3 * in.n);
+    }
 }
 
 namespace {

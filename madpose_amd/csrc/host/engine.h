@@ -61,6 +61,11 @@ void estimate_pair(const PairInput &in, const RansacOptions &opts, const Estimat
 void score_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
                   int nm, double *scores, double *errors, int device, double *norm_scale);
 
+// The engine's host LO sweep (host/lo_sweep.h) over explicit models (problem units):
+// the errors and ScoreModel sums LO uses (mp_debug_lo_sweep, test hook; no device)
+void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
+                     int nm, double *scores, double *errors);
+
 // Batched device LM (mp_lm_refine_batch): problem j refines models[j] (problem units)
 // over the residual blocks idx[offsets[3j] .. offsets[3j+1]) (reproj 0->1),
 // [offsets[3j+1] .. offsets[3j+2]) (1->0), [offsets[3j+2] .. offsets[3j+3]) (Sampson),
