@@ -19,19 +19,24 @@ LIB = os.path.join(LIBDIR, "libmadpose_mi355x.so")
 SOURCES = [
     os.path.join(CSRC, "kernels", "kernels.hip"),
     os.path.join(CSRC, "host", "engine.cpp"),
-    os.path.join(CSRC, "host", "lm.cpp"),
     os.path.join(CSRC, "capi.cpp"),
 ]
 # host-only translation units (plain C++, no device pass): the LO sweep carries an
 # AVX-512 function beside its x86-64-v3 baseline, chosen at run time (host/lo_sweep.cpp)
 HOST_SOURCES = [
     os.path.join(CSRC, "host", "lo_sweep.cpp"),
+    os.path.join(CSRC, "host", "lm.cpp"),
+    os.path.join(CSRC, "host", "lm_eval_w4.cpp"),
+    os.path.join(CSRC, "host", "lm_eval_w8.cpp"),
 ]
+# per-file host flags: the AVX-512 build of the LM's residual evaluation (chosen at run
+# time, host/lm.cpp lm_eval_avx512)
+HOST_EXTRA = {os.path.join(CSRC, "host", "lm_eval_w8.cpp"): ["-march=x86-64-v4"]}
 HEADERS = [
     os.path.join(dp, f)
     for dp, _, fs in os.walk(CSRC)
     for f in fs
-    if f.endswith(".h")
+    if f.endswith(".h") or f.endswith(".inc")
 ] + [os.path.join(ROOT, "include", "madpose_mi355x.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -57,7 +62,7 @@ def _compile(src):
     obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
     if _newer(obj, [src, __file__] + HEADERS):
         if src in HOST_SOURCES:
-            cmd = [HOSTCXX] + HOST_FLAGS + ["-c", src, "-o", obj]
+            cmd = [HOSTCXX] + HOST_FLAGS + HOST_EXTRA.get(src, []) + ["-c", src, "-o", obj]
         else:
             cmd = [HIPCC, "-x", "hip"] + FLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)

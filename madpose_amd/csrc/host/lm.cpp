@@ -1,5 +1,6 @@
 // Host LM for LO -- see lm.h.
 #include "lm.h"
+#include "lm_eval.h"
 
 #include <sched.h>
 
@@ -18,7 +19,6 @@ namespace mp {
 
 namespace {
 
-enum Full { kD0 = 0, kD1, kD2, kT0, kT1, kT2, kS, kO0, kO1, kF0, kF1, kNFull };
 
 inline void skew(const double *v, double *S) {
     S[0] = 0;
@@ -57,7 +57,6 @@ struct Ctx {
 
 // Normal-equation accumulator in the full parameter layout (packed upper triangle).
 // Inactive parameters accumulate harmlessly and are dropped by scatter().
-constexpr int kNPack = kNFull * (kNFull + 1) / 2;
 struct Acc {
     double H[kNPack];
     double g[kNFull];
@@ -235,616 +234,17 @@ Pool &lo_pool() {
     return pool;
 }
 
-// Residual blocks [b0, b1) of the concatenated block list (reproj0, reproj1, Sampson)
-// into acc; with jac == false only the cost is accumulated (in the same order).
-void evaluate_range(const Ctx &C, const Params &p, bool jac, size_t b0, size_t b1, Acc &acc) {
-    const HostPair &P = *C.P;
-    const bool cal = P.variant == kCal;
-    const bool sf = P.variant == kSF;
-    const double f0 = p.f0, f1 = sf ? p.f0 : p.f1;
-    double &cost = acc.cost;
-    const size_t n0 = C.S.use_reproj ? C.sample[0].size() : 0, n1 = C.S.use_reproj ? C.sample[1].size() : 0;
-    const size_t n2 = C.S.use_sampson ? C.sample[2].size() : 0;
-    const double *R = p.R, *t = p.t;
-    if (n0 > 0 && b0 < n0) {
-        // LiftProjectionFunctor0 and variants: x1_hat = K1 (R c0 (d0 + o0) + t)
-        for (size_t bi = b0; bi < std::min(b1, n0); ++bi) {
-            const int i = C.sample[0][bi];
-            double c[3];
-            const double xh[3] = {P.x0[2 * i], P.x0[2 * i + 1], 1.0};
-            if (cal)
-                mv3(P.K0i, xh, c);
-            else {
-                c[0] = xh[0] / f0;
-                c[1] = xh[1] / f0;
-                c[2] = 1.0;
-            }
-            const double a = P.d0[i] + p.o0;
-            const double pp[3] = {c[0] * a, c[1] * a, c[2] * a};
-            double v[3], y[3], h[3];
-            mv3(R, pp, v);
-            for (int k = 0; k < 3; ++k) y[k] = v[k] + t[k];
-            if (cal)
-                mv3(P.K1, y, h);
-            else {
-                h[0] = f1 * y[0];
-                h[1] = f1 * y[1];
-                h[2] = y[2];
-            }
-            const double iz = 1.0 / h[2];
-            const double r0 = h[0] * iz - P.x1[2 * i], r1 = h[1] * iz - P.x1[2 * i + 1];
-            if (!jac) {
-                cost += 0.5 * r0 * r0;
-                cost += 0.5 * r1 * r1;
-                continue;
-            }
-            // dr/dh
-            const double Dh[2][3] = {{iz, 0, -h[0] * iz * iz}, {0, iz, -h[1] * iz * iz}};
-            double G[2][3]; // dr/dy
-            for (int rr = 0; rr < 2; ++rr)
-                for (int k = 0; k < 3; ++k) {
-                    if (cal)
-                        G[rr][k] = Dh[rr][0] * P.K1[k] + Dh[rr][1] * P.K1[3 + k] + Dh[rr][2] * P.K1[6 + k];
-                    else
-                        G[rr][k] = Dh[rr][k] * (k < 2 ? f1 : 1.0);
-                }
-            double Sv[9];
-            skew(v, Sv);
-            double Rc[3];
-            mv3(R, c, Rc);
-            double dcf[3] = {0, 0, 0}, Rdcf[3] = {0, 0, 0};
-            if (!cal) {
-                dcf[0] = -xh[0] / (f0 * f0) * a;
-                dcf[1] = -xh[1] / (f0 * f0) * a;
-                mv3(R, dcf, Rdcf);
-            }
-            for (int rr = 0; rr < 2; ++rr) {
-                double gf[kNFull] = {0};
-                for (int k = 0; k < 3; ++k) {
-                    // dy/ddelta = -2 [v]x
-                    gf[kD0 + k] = -2.0 * (G[rr][0] * Sv[k] + G[rr][1] * Sv[3 + k] + G[rr][2] * Sv[6 + k]);
-                    gf[kT0 + k] = G[rr][k];
-                }
-                gf[kO0] = G[rr][0] * Rc[0] + G[rr][1] * Rc[1] + G[rr][2] * Rc[2];
-                if (!cal) {
-                    const double dyf0 = G[rr][0] * Rdcf[0] + G[rr][1] * Rdcf[1] + G[rr][2] * Rdcf[2];
-                    const double dhf1 = Dh[rr][0] * y[0] + Dh[rr][1] * y[1];
-                    if (sf)
-                        gf[kF0] = dyf0 + dhf1;
-                    else {
-                        gf[kF0] = dyf0;
-                        gf[kF1] = dhf1;
-                    }
-                }
-                acc.add(rr == 0 ? r0 : r1, gf);
-            }
-        }
-    }
-    if (n1 > 0 && b1 > n0 && b0 < n0 + n1) {
-        // LiftProjectionFunctor1: x0_hat = K0 R^T (c1 (d1 + o1) s - t)
-        for (size_t bi = std::max(b0, n0); bi < std::min(b1, n0 + n1); ++bi) {
-            const int i = C.sample[1][bi - n0];
-            double c[3];
-            const double xh[3] = {P.x1[2 * i], P.x1[2 * i + 1], 1.0};
-            if (cal)
-                mv3(P.K1i, xh, c);
-            else {
-                c[0] = xh[0] / f1;
-                c[1] = xh[1] / f1;
-                c[2] = 1.0;
-            }
-            const double dep = P.d1[i] + p.o1;
-            const double a = dep * p.s;
-            const double u[3] = {c[0] * a - t[0], c[1] * a - t[1], c[2] * a - t[2]};
-            double y[3], h[3];
-            mtv3(R, u, y);
-            if (cal)
-                mv3(P.K0, y, h);
-            else {
-                h[0] = f0 * y[0];
-                h[1] = f0 * y[1];
-                h[2] = y[2];
-            }
-            const double iz = 1.0 / h[2];
-            const double r0 = h[0] * iz - P.x0[2 * i], r1 = h[1] * iz - P.x0[2 * i + 1];
-            if (!jac) {
-                cost += 0.5 * r0 * r0;
-                cost += 0.5 * r1 * r1;
-                continue;
-            }
-            const double Dh[2][3] = {{iz, 0, -h[0] * iz * iz}, {0, iz, -h[1] * iz * iz}};
-            double G[2][3];
-            for (int rr = 0; rr < 2; ++rr)
-                for (int k = 0; k < 3; ++k) {
-                    if (cal)
-                        G[rr][k] = Dh[rr][0] * P.K0[k] + Dh[rr][1] * P.K0[3 + k] + Dh[rr][2] * P.K0[6 + k];
-                    else
-                        G[rr][k] = Dh[rr][k] * (k < 2 ? f0 : 1.0);
-                }
-            // dy/ddelta = 2 R^T [u]x ; dy/dt = -R^T ; dy/ds = R^T c dep ; dy/do1 = R^T c s
-            double Su[9], RtSu[9];
-            skew(u, Su);
-            for (int r = 0; r < 3; ++r)
-                for (int cc = 0; cc < 3; ++cc)
-                    RtSu[3 * r + cc] = R[r] * Su[cc] + R[3 + r] * Su[3 + cc] + R[6 + r] * Su[6 + cc];
-            double Rtc[3];
-            mtv3(R, c, Rtc);
-            double Rtdcf[3] = {0, 0, 0};
-            if (!cal) {
-                const double dcf[3] = {-xh[0] / (f1 * f1) * a, -xh[1] / (f1 * f1) * a, 0.0};
-                mtv3(R, dcf, Rtdcf);
-            }
-            for (int rr = 0; rr < 2; ++rr) {
-                double gf[kNFull] = {0};
-                for (int k = 0; k < 3; ++k) {
-                    gf[kD0 + k] =
-                        2.0 * (G[rr][0] * RtSu[k] + G[rr][1] * RtSu[3 + k] + G[rr][2] * RtSu[6 + k]);
-                    gf[kT0 + k] = -(G[rr][0] * R[3 * k] + G[rr][1] * R[3 * k + 1] + G[rr][2] * R[3 * k + 2]);
-                }
-                const double gRtc = G[rr][0] * Rtc[0] + G[rr][1] * Rtc[1] + G[rr][2] * Rtc[2];
-                gf[kS] = gRtc * dep;
-                gf[kO1] = gRtc * p.s;
-                if (!cal) {
-                    const double dyf1 = G[rr][0] * Rtdcf[0] + G[rr][1] * Rtdcf[1] + G[rr][2] * Rtdcf[2];
-                    const double dhf0 = Dh[rr][0] * y[0] + Dh[rr][1] * y[1];
-                    if (sf)
-                        gf[kF0] = dyf1 + dhf0;
-                    else {
-                        gf[kF0] = dhf0;
-                        gf[kF1] = dyf1;
-                    }
-                }
-                acc.add(rr == 0 ? r0 : r1, gf);
-            }
-        }
-    }
-    if (n2 > 0 && b1 > n0 + n1) {
-        // SampsonError*Functor: r = w C / |(e0, e1, g0, g1)|
-        double Tx[9], E[9];
-        skew(t, Tx);
-        mm3(Tx, R, E);
-        double s0[3] = {1, 1, 1}, s1[3] = {1, 1, 1};
-        if (!cal) {
-            s0[0] = s0[1] = 1.0 / f0;
-            s1[0] = s1[1] = 1.0 / f1;
-        }
-        double F[9];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) F[3 * r + c] = E[3 * r + c] * s1[r] * s0[c];
-        // derivative building blocks: dE/dt_k = [e_k]x R, dE/ddelta_k = 2 [t]x [e_k]x R
-        double dEt[3][9], dEd[3][9];
-        if (jac) {
-            for (int k = 0; k < 3; ++k) {
-                double ek[3] = {0, 0, 0};
-                ek[k] = 1.0;
-                double Sk[9];
-                skew(ek, Sk);
-                mm3(Sk, R, dEt[k]);
-                mm3(Tx, dEt[k], dEd[k]);
-                for (int e = 0; e < 9; ++e) dEd[k][e] *= 2.0;
-            }
-        }
-        for (size_t bi = std::max(b0, n0 + n1); bi < std::min(b1, n0 + n1 + n2); ++bi) {
-            const int i = C.sample[2][bi - n0 - n1];
-            double a[3], b[3];
-            if (cal) {
-                const double xa[3] = {P.x0[2 * i], P.x0[2 * i + 1], 1.0}, xb[3] = {P.x1[2 * i], P.x1[2 * i + 1], 1.0};
-                mv3(P.K0i, xa, a);
-                mv3(P.K1i, xb, b);
-            } else {
-                a[0] = P.x0[2 * i];
-                a[1] = P.x0[2 * i + 1];
-                b[0] = P.x1[2 * i];
-                b[1] = P.x1[2 * i + 1];
-            }
-            a[2] = b[2] = 1.0; // the functor uses the first two coordinates and an implicit 1
-            const double e0 = F[0] * a[0] + F[1] * a[1] + F[2];
-            const double e1 = F[3] * a[0] + F[4] * a[1] + F[5];
-            const double e2 = F[6] * a[0] + F[7] * a[1] + F[8];
-            const double g0 = F[0] * b[0] + F[3] * b[1] + F[6];
-            const double g1 = F[1] * b[0] + F[4] * b[1] + F[7];
-            const double Cc = b[0] * e0 + b[1] * e1 + e2;
-            const double D = e0 * e0 + e1 * e1 + g0 * g0 + g1 * g1;
-            const double sD = std::sqrt(D);
-            const double r = C.S.w_sampson * Cc / sD;
-            if (!jac) {
-                cost += 0.5 * r * r;
-                continue;
-            }
-            const double ev[3] = {e0, e1, e2}, gv[3] = {g0, g1, 0.0};
-            double W[9]; // dr/dF
-            const double k1 = C.S.w_sampson / sD, k2 = C.S.w_sampson * Cc / (D * sD);
-            for (int ii = 0; ii < 3; ++ii)
-                for (int jj = 0; jj < 3; ++jj) {
-                    const double dD = (ii < 2 ? ev[ii] * a[jj] : 0.0) + (jj < 2 ? gv[jj] * b[ii] : 0.0);
-                    W[3 * ii + jj] = k1 * b[ii] * a[jj] - k2 * dD;
-                }
-            double WE[9]; // dr/dE
-            for (int ii = 0; ii < 3; ++ii)
-                for (int jj = 0; jj < 3; ++jj) WE[3 * ii + jj] = W[3 * ii + jj] * s1[ii] * s0[jj];
-            double gf[kNFull] = {0};
-            for (int k = 0; k < 3; ++k) {
-                double dt = 0, dd = 0;
-                for (int e = 0; e < 9; ++e) {
-                    dt += WE[e] * dEt[k][e];
-                    dd += WE[e] * dEd[k][e];
-                }
-                gf[kT0 + k] = dt;
-                gf[kD0 + k] = dd;
-            }
-            if (!cal) {
-                const double ds0[3] = {-1.0 / (f0 * f0), -1.0 / (f0 * f0), 0.0};
-                const double ds1[3] = {-1.0 / (f1 * f1), -1.0 / (f1 * f1), 0.0};
-                double df0 = 0, df1 = 0;
-                for (int ii = 0; ii < 3; ++ii)
-                    for (int jj = 0; jj < 3; ++jj) {
-                        df0 += W[3 * ii + jj] * E[3 * ii + jj] * s1[ii] * ds0[jj];
-                        df1 += W[3 * ii + jj] * E[3 * ii + jj] * ds1[ii] * s0[jj];
-                    }
-                if (sf)
-                    gf[kF0] = df0 + df1;
-                else {
-                    gf[kF0] = df0;
-                    gf[kF1] = df1;
-                }
-            }
-            acc.add(r, gf);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Four residual blocks at a time (GCC/Clang vector extension; AVX2 on the build
-// flags): the per-block Jacobian algebra of evaluate_range with every per-block value
-// a 4-lane vector and the parameters broadcast.  Lanes past the end of the block list
-// repeat the last block with a zero weight.  NA = number of leading full-layout
-// parameters that can be active for the variant (cal 9, sf 10, tf 11).
-typedef double V4 __attribute__((vector_size(32)));
-inline V4 vs(double a) { return V4{a, a, a, a}; }
-inline V4 vsqrt(V4 v) { return V4{std::sqrt(v[0]), std::sqrt(v[1]), std::sqrt(v[2]), std::sqrt(v[3])}; }
-inline double hsum(V4 v) { return (v[0] + v[1]) + (v[2] + v[3]); }
-
-template <int NA> struct AccV {
-    static constexpr int kPack = NA * (NA + 1) / 2;
-    V4 H[kPack];
-    V4 g[NA];
-    V4 cost;
-    void clear() {
-        for (int q = 0; q < kPack; ++q) H[q] = vs(0.0);
-        for (int a = 0; a < NA; ++a) g[a] = vs(0.0);
-        cost = vs(0.0);
-    }
-    inline void add(V4 r, const V4 *gf) {
-        cost += 0.5 * r * r;
-        int q = 0;
-        for (int a = 0; a < NA; ++a) {
-            g[a] += gf[a] * r;
-            const V4 ja = gf[a];
-            for (int b = a; b < NA; ++b) H[q++] += ja * gf[b];
-        }
-    }
-    // lane sums into the scalar full-layout accumulator
-    void reduce_into(Acc &acc) const {
-        acc.cost += hsum(cost);
-        int q = 0;
-        for (int a = 0; a < kNFull; ++a) {
-            if (a < NA) acc.g[a] += hsum(g[a]);
-            for (int b = a; b < kNFull; ++b, ++q)
-                if (a < NA && b < NA) acc.H[q] += hsum(H[a * NA - a * (a - 1) / 2 + (b - a)]);
-        }
-    }
-};
-
-inline void mv3v(const double *A, const V4 *v, V4 *o) {
-    for (int r = 0; r < 3; ++r) o[r] = A[3 * r] * v[0] + A[3 * r + 1] * v[1] + A[3 * r + 2] * v[2];
-}
-inline void mtv3v(const double *A, const V4 *v, V4 *o) {
-    for (int r = 0; r < 3; ++r) o[r] = A[r] * v[0] + A[3 + r] * v[1] + A[6 + r] * v[2];
-}
-
-template <int NA>
-void evaluate_range_v(const Ctx &C, const Params &p, bool jac, size_t b0, size_t b1, Acc &acc_out) {
-    const HostPair &P = *C.P;
-    const bool cal = P.variant == kCal;
-    const bool sf = P.variant == kSF;
-    const double f0 = p.f0, f1 = sf ? p.f0 : p.f1;
-    const size_t n0 = C.S.use_reproj ? C.sample[0].size() : 0, n1 = C.S.use_reproj ? C.sample[1].size() : 0;
-    const size_t n2 = C.S.use_sampson ? C.sample[2].size() : 0;
-    const double *R = p.R, *t = p.t;
-    AccV<NA> acc;
-    acc.clear();
-    V4 gf0[kNFull], gf1[kNFull]; // only the first NA slots are accumulated
-    // gathers the lanes of blocks [bi, bi + 4) of list `idx` (clamped), weight 0 past `end`
-    auto gather = [&](const std::vector<int> &idx, size_t bi, size_t off, size_t end, int *ii, V4 &w) {
-        for (int l = 0; l < 4; ++l) {
-            const size_t b = std::min(bi + l, end - 1);
-            ii[l] = idx[b - off];
-            w[l] = (bi + l < end) ? 1.0 : 0.0;
-        }
-    };
-    if (n0 > 0 && b0 < n0) {
-        // LiftProjectionFunctor0 and variants: x1_hat = K1 (R c0 (d0 + o0) + t)
-        const size_t end = std::min(b1, n0);
-        for (size_t bi = b0; bi < end; bi += 4) {
-            int ii[4];
-            V4 w;
-            gather(C.sample[0], bi, 0, end, ii, w);
-            V4 xh[3], x1u, x1v, dd;
-            for (int l = 0; l < 4; ++l) {
-                xh[0][l] = P.x0[2 * ii[l]];
-                xh[1][l] = P.x0[2 * ii[l] + 1];
-                x1u[l] = P.x1[2 * ii[l]];
-                x1v[l] = P.x1[2 * ii[l] + 1];
-                dd[l] = P.d0[ii[l]];
-            }
-            xh[2] = vs(1.0);
-            V4 c[3];
-            if (cal)
-                mv3v(P.K0i, xh, c);
-            else {
-                c[0] = xh[0] / f0;
-                c[1] = xh[1] / f0;
-                c[2] = vs(1.0);
-            }
-            const V4 a = dd + p.o0;
-            const V4 pp[3] = {c[0] * a, c[1] * a, c[2] * a};
-            V4 v[3], y[3], h[3];
-            mv3v(R, pp, v);
-            for (int k = 0; k < 3; ++k) y[k] = v[k] + t[k];
-            if (cal)
-                mv3v(P.K1, y, h);
-            else {
-                h[0] = f1 * y[0];
-                h[1] = f1 * y[1];
-                h[2] = y[2];
-            }
-            const V4 iz = 1.0 / h[2];
-            const V4 r0 = (h[0] * iz - x1u) * w, r1 = (h[1] * iz - x1v) * w;
-            if (!jac) {
-                acc.cost += 0.5 * r0 * r0;
-                acc.cost += 0.5 * r1 * r1;
-                continue;
-            }
-            const V4 Dh[2][3] = {{iz, vs(0.0), -h[0] * iz * iz}, {vs(0.0), iz, -h[1] * iz * iz}};
-            V4 G[2][3];
-            for (int rr = 0; rr < 2; ++rr)
-                for (int k = 0; k < 3; ++k) {
-                    if (cal)
-                        G[rr][k] = (Dh[rr][0] * P.K1[k] + Dh[rr][1] * P.K1[3 + k] + Dh[rr][2] * P.K1[6 + k]) * w;
-                    else
-                        G[rr][k] = Dh[rr][k] * (k < 2 ? f1 : 1.0) * w;
-                }
-            // [v]x columns: Sv[0][k], Sv[1][k], Sv[2][k]
-            const V4 Sv[3][3] = {{vs(0.0), -v[2], v[1]}, {v[2], vs(0.0), -v[0]}, {-v[1], v[0], vs(0.0)}};
-            V4 Rc[3];
-            mv3v(R, c, Rc);
-            V4 Rdcf[3] = {vs(0.0), vs(0.0), vs(0.0)};
-            if (!cal) {
-                const V4 dcf[3] = {-xh[0] / (f0 * f0) * a, -xh[1] / (f0 * f0) * a, vs(0.0)};
-                mv3v(R, dcf, Rdcf);
-            }
-            for (int rr = 0; rr < 2; ++rr) {
-                V4 *gf = rr == 0 ? gf0 : gf1;
-                for (int k = 0; k < kNFull; ++k) gf[k] = vs(0.0);
-                for (int k = 0; k < 3; ++k) {
-                    gf[kD0 + k] = -2.0 * (G[rr][0] * Sv[0][k] + G[rr][1] * Sv[1][k] + G[rr][2] * Sv[2][k]);
-                    gf[kT0 + k] = G[rr][k];
-                }
-                gf[kO0] = G[rr][0] * Rc[0] + G[rr][1] * Rc[1] + G[rr][2] * Rc[2];
-                if (!cal) {
-                    const V4 dyf0 = G[rr][0] * Rdcf[0] + G[rr][1] * Rdcf[1] + G[rr][2] * Rdcf[2];
-                    const V4 dhf1 = (Dh[rr][0] * y[0] + Dh[rr][1] * y[1]) * w;
-                    if (sf)
-                        gf[kF0] = dyf0 + dhf1;
-                    else {
-                        gf[kF0] = dyf0;
-                        gf[kF1] = dhf1;
-                    }
-                }
-            }
-            acc.add(r0, gf0);
-            acc.add(r1, gf1);
-        }
-    }
-    if (n1 > 0 && b1 > n0 && b0 < n0 + n1) {
-        // LiftProjectionFunctor1: x0_hat = K0 R^T (c1 (d1 + o1) s - t)
-        const size_t start = std::max(b0, n0), end = std::min(b1, n0 + n1);
-        for (size_t bi = start; bi < end; bi += 4) {
-            int ii[4];
-            V4 w;
-            gather(C.sample[1], bi, n0, end, ii, w);
-            V4 xh[3], x0u, x0v, dd;
-            for (int l = 0; l < 4; ++l) {
-                xh[0][l] = P.x1[2 * ii[l]];
-                xh[1][l] = P.x1[2 * ii[l] + 1];
-                x0u[l] = P.x0[2 * ii[l]];
-                x0v[l] = P.x0[2 * ii[l] + 1];
-                dd[l] = P.d1[ii[l]];
-            }
-            xh[2] = vs(1.0);
-            V4 c[3];
-            if (cal)
-                mv3v(P.K1i, xh, c);
-            else {
-                c[0] = xh[0] / f1;
-                c[1] = xh[1] / f1;
-                c[2] = vs(1.0);
-            }
-            const V4 dep = dd + p.o1;
-            const V4 a = dep * p.s;
-            const V4 u[3] = {c[0] * a - t[0], c[1] * a - t[1], c[2] * a - t[2]};
-            V4 y[3], h[3];
-            mtv3v(R, u, y);
-            if (cal)
-                mv3v(P.K0, y, h);
-            else {
-                h[0] = f0 * y[0];
-                h[1] = f0 * y[1];
-                h[2] = y[2];
-            }
-            const V4 iz = 1.0 / h[2];
-            const V4 r0 = (h[0] * iz - x0u) * w, r1 = (h[1] * iz - x0v) * w;
-            if (!jac) {
-                acc.cost += 0.5 * r0 * r0;
-                acc.cost += 0.5 * r1 * r1;
-                continue;
-            }
-            const V4 Dh[2][3] = {{iz, vs(0.0), -h[0] * iz * iz}, {vs(0.0), iz, -h[1] * iz * iz}};
-            V4 G[2][3];
-            for (int rr = 0; rr < 2; ++rr)
-                for (int k = 0; k < 3; ++k) {
-                    if (cal)
-                        G[rr][k] = (Dh[rr][0] * P.K0[k] + Dh[rr][1] * P.K0[3 + k] + Dh[rr][2] * P.K0[6 + k]) * w;
-                    else
-                        G[rr][k] = Dh[rr][k] * (k < 2 ? f0 : 1.0) * w;
-                }
-            // dy/ddelta = 2 R^T [u]x
-            const V4 Su[3][3] = {{vs(0.0), -u[2], u[1]}, {u[2], vs(0.0), -u[0]}, {-u[1], u[0], vs(0.0)}};
-            V4 RtSu[3][3];
-            for (int r = 0; r < 3; ++r)
-                for (int cc = 0; cc < 3; ++cc) RtSu[r][cc] = R[r] * Su[0][cc] + R[3 + r] * Su[1][cc] + R[6 + r] * Su[2][cc];
-            V4 Rtc[3];
-            mtv3v(R, c, Rtc);
-            V4 Rtdcf[3] = {vs(0.0), vs(0.0), vs(0.0)};
-            if (!cal) {
-                const V4 dcf[3] = {-xh[0] / (f1 * f1) * a, -xh[1] / (f1 * f1) * a, vs(0.0)};
-                mtv3v(R, dcf, Rtdcf);
-            }
-            for (int rr = 0; rr < 2; ++rr) {
-                V4 *gf = rr == 0 ? gf0 : gf1;
-                for (int k = 0; k < kNFull; ++k) gf[k] = vs(0.0);
-                for (int k = 0; k < 3; ++k) {
-                    gf[kD0 + k] = 2.0 * (G[rr][0] * RtSu[0][k] + G[rr][1] * RtSu[1][k] + G[rr][2] * RtSu[2][k]);
-                    gf[kT0 + k] = -(G[rr][0] * R[3 * k] + G[rr][1] * R[3 * k + 1] + G[rr][2] * R[3 * k + 2]);
-                }
-                const V4 gRtc = G[rr][0] * Rtc[0] + G[rr][1] * Rtc[1] + G[rr][2] * Rtc[2];
-                gf[kS] = gRtc * dep;
-                gf[kO1] = gRtc * p.s;
-                if (!cal) {
-                    const V4 dyf1 = G[rr][0] * Rtdcf[0] + G[rr][1] * Rtdcf[1] + G[rr][2] * Rtdcf[2];
-                    const V4 dhf0 = (Dh[rr][0] * y[0] + Dh[rr][1] * y[1]) * w;
-                    if (sf)
-                        gf[kF0] = dyf1 + dhf0;
-                    else {
-                        gf[kF0] = dhf0;
-                        gf[kF1] = dyf1;
-                    }
-                }
-            }
-            acc.add(r0, gf0);
-            acc.add(r1, gf1);
-        }
-    }
-    if (n2 > 0 && b1 > n0 + n1) {
-        // SampsonError*Functor: r = w C / |(e0, e1, g0, g1)|
-        double Tx[9], E[9];
-        skew(t, Tx);
-        mm3(Tx, R, E);
-        double s0[3] = {1, 1, 1}, s1[3] = {1, 1, 1};
-        if (!cal) {
-            s0[0] = s0[1] = 1.0 / f0;
-            s1[0] = s1[1] = 1.0 / f1;
-        }
-        double F[9];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) F[3 * r + c] = E[3 * r + c] * s1[r] * s0[c];
-        double dEt[3][9], dEd[3][9];
-        for (int k = 0; k < 3; ++k) {
-            double ek[3] = {0, 0, 0};
-            ek[k] = 1.0;
-            double Sk[9];
-            skew(ek, Sk);
-            mm3(Sk, R, dEt[k]);
-            mm3(Tx, dEt[k], dEd[k]);
-            for (int e = 0; e < 9; ++e) dEd[k][e] *= 2.0;
-        }
-        // the f-derivative weights of W (uniform): E_ij s1_i ds0_j and E_ij ds1_i s0_j
-        double Ef0[9] = {0}, Ef1[9] = {0};
-        if (!cal)
-            for (int ii = 0; ii < 3; ++ii)
-                for (int jj = 0; jj < 3; ++jj) {
-                    Ef0[3 * ii + jj] = E[3 * ii + jj] * s1[ii] * (jj < 2 ? -1.0 / (f0 * f0) : 0.0);
-                    Ef1[3 * ii + jj] = E[3 * ii + jj] * (ii < 2 ? -1.0 / (f1 * f1) : 0.0) * s0[jj];
-                }
-        const double ws = C.S.w_sampson;
-        const size_t start = std::max(b0, n0 + n1), end = std::min(b1, n0 + n1 + n2);
-        for (size_t bi = start; bi < end; bi += 4) {
-            int ii4[4];
-            V4 w;
-            gather(C.sample[2], bi, n0 + n1, end, ii4, w);
-            V4 a[3], b[3];
-            {
-                V4 xa[3], xb[3];
-                for (int l = 0; l < 4; ++l) {
-                    xa[0][l] = P.x0[2 * ii4[l]];
-                    xa[1][l] = P.x0[2 * ii4[l] + 1];
-                    xb[0][l] = P.x1[2 * ii4[l]];
-                    xb[1][l] = P.x1[2 * ii4[l] + 1];
-                }
-                xa[2] = xb[2] = vs(1.0);
-                if (cal) {
-                    mv3v(P.K0i, xa, a);
-                    mv3v(P.K1i, xb, b);
-                } else {
-                    for (int k = 0; k < 2; ++k) {
-                        a[k] = xa[k];
-                        b[k] = xb[k];
-                    }
-                }
-                a[2] = b[2] = vs(1.0); // the functor uses the first two coordinates and an implicit 1
-            }
-            const V4 e0 = F[0] * a[0] + F[1] * a[1] + F[2];
-            const V4 e1 = F[3] * a[0] + F[4] * a[1] + F[5];
-            const V4 e2 = F[6] * a[0] + F[7] * a[1] + F[8];
-            const V4 g0 = F[0] * b[0] + F[3] * b[1] + F[6];
-            const V4 g1 = F[1] * b[0] + F[4] * b[1] + F[7];
-            const V4 Cc = b[0] * e0 + b[1] * e1 + e2;
-            const V4 D = e0 * e0 + e1 * e1 + g0 * g0 + g1 * g1;
-            const V4 sD = vsqrt(D);
-            const V4 r = ws * Cc / sD * w;
-            if (!jac) {
-                acc.cost += 0.5 * r * r;
-                continue;
-            }
-            const V4 ev[3] = {e0, e1, e2}, gv[3] = {g0, g1, vs(0.0)};
-            const V4 k1 = ws / sD * w, k2 = ws * Cc / (D * sD) * w;
-            V4 W[9];
-            for (int i3 = 0; i3 < 3; ++i3)
-                for (int j3 = 0; j3 < 3; ++j3) {
-                    V4 dD = vs(0.0);
-                    if (i3 < 2) dD += ev[i3] * a[j3];
-                    if (j3 < 2) dD += gv[j3] * b[i3];
-                    W[3 * i3 + j3] = k1 * b[i3] * a[j3] - k2 * dD;
-                }
-            for (int k = 0; k < kNFull; ++k) gf0[k] = vs(0.0);
-            for (int k = 0; k < 3; ++k) {
-                V4 dt = vs(0.0), ddl = vs(0.0);
-                for (int i3 = 0; i3 < 3; ++i3)
-                    for (int j3 = 0; j3 < 3; ++j3) {
-                        const V4 we = W[3 * i3 + j3] * (s1[i3] * s0[j3]);
-                        dt += we * dEt[k][3 * i3 + j3];
-                        ddl += we * dEd[k][3 * i3 + j3];
-                    }
-                gf0[kT0 + k] = dt;
-                gf0[kD0 + k] = ddl;
-            }
-            if (!cal) {
-                V4 df0 = vs(0.0), df1 = vs(0.0);
-                for (int e = 0; e < 9; ++e) {
-                    df0 += W[e] * Ef0[e];
-                    df1 += W[e] * Ef1[e];
-                }
-                if (sf)
-                    gf0[kF0] = df0 + df1;
-                else {
-                    gf0[kF0] = df0;
-                    gf0[kF1] = df1;
-                }
-            }
-            acc.add(r, gf0);
-        }
-    }
-    acc.reduce_into(acc_out);
+// the 8-lane residual evaluation runs as AVX-512 when the CPU has it (identical results
+// either way, lm_eval.inc); MADPOSE_LM_ISA=avx2 forces the AVX2 build (A/B)
+bool lm_eval_avx512() {
+    static const bool on = [] {
+        const char *e = std::getenv("MADPOSE_LM_ISA");
+        if (e && std::strcmp(e, "avx2") == 0) return false;
+        __builtin_cpu_init();
+        return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
+               __builtin_cpu_supports("avx512vl");
+    }();
+    return on;
 }
 
 size_t num_blocks(const Ctx &C) {
@@ -861,15 +261,34 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
     const bool jac = H != nullptr;
     Acc total;
     total.clear();
-    const int variant = C.P->variant;
-    auto range = [&](size_t a, size_t b, Acc &acc) {
-        if (variant == kTF)
-            evaluate_range_v<kNFull>(C, p, jac, a, b, acc);
-        else if (variant == kSF)
-            evaluate_range_v<kF0 + 1>(C, p, jac, a, b, acc);
-        else
-            evaluate_range_v<kF0>(C, p, jac, a, b, acc);
-    };
+    const HostPair &P = *C.P;
+    LmEvalIn E;
+    E.variant = P.variant;
+    E.x0 = P.x0.data();
+    E.x1 = P.x1.data();
+    E.d0 = P.d0.data();
+    E.d1 = P.d1.data();
+    E.K0 = P.K0;
+    E.K1 = P.K1;
+    E.K0i = P.K0i;
+    E.K1i = P.K1i;
+    E.s0 = C.sample[0].data();
+    E.s1 = C.sample[1].data();
+    E.s2 = C.sample[2].data();
+    E.n0 = C.S.use_reproj ? C.sample[0].size() : 0;
+    E.n1 = C.S.use_reproj ? C.sample[1].size() : 0;
+    E.n2 = C.S.use_sampson ? C.sample[2].size() : 0;
+    E.w_sampson = C.S.w_sampson;
+    LmEvalParams ep;
+    std::memcpy(ep.R, p.R, sizeof(ep.R));
+    std::memcpy(ep.t, p.t, sizeof(ep.t));
+    ep.s = p.s;
+    ep.o0 = p.o0;
+    ep.o1 = p.o1;
+    ep.f0 = p.f0;
+    ep.f1 = p.f1;
+    const auto eval = lm_eval_avx512() ? lm_eval_range_w8 : lm_eval_range_w4;
+    auto range = [&](size_t a, size_t b, Acc &acc) { eval(E, ep, jac, a, b, acc.H, acc.g, &acc.cost); };
     if (nchunks <= 1) {
         range(0, nb, total);
     } else {
