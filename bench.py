@@ -173,16 +173,21 @@ def gather_counters(local, world):
     import torch.distributed as dist
 
     t = torch.tensor(local, dtype=torch.float64)
-    if world == 1:
-        return t.numpy()[None]
+    if not (dist.is_available() and dist.is_initialized()):
+        return t.numpy()[None]  # one rank, no process group
     out = [torch.zeros_like(t) for _ in range(world)]
     if dist.get_backend() == "nccl":
         gl = [g.cuda() for g in out]
         dist.all_gather(gl, t.cuda())
         out = [g.cpu() for g in gl]
+        GATHER_LOG.append({"backend": "nccl", "device": str(gl[0].device), "doubles": int(t.numel())})
     else:
         dist.all_gather(out, t)
+        GATHER_LOG.append({"backend": dist.get_backend(), "device": "cpu", "doubles": int(t.numel())})
     return torch.stack(out).numpy()
+
+
+GATHER_LOG = []  # the all_gathers this process issued (reported under "dist")
 
 
 def dist_info(world):
@@ -195,6 +200,7 @@ def dist_info(world):
         if dist.is_available() and dist.is_initialized():
             info["backend"] = dist.get_backend()
             info["world_size"] = dist.get_world_size()
+        info["all_gathers"] = list(GATHER_LOG)
     except Exception:  # pragma: no cover - informational only
         pass
     try:
@@ -633,21 +639,35 @@ def main(argv=None):
     # rehearsal knobs for one-GPU boxes (several ranks on one card need gloo: RCCL
     # refuses two ranks on one device): MADPOSE_BENCH_DIST_BACKEND, MADPOSE_BENCH_DEVICE
     dev = int(os.environ.get("MADPOSE_BENCH_DEVICE", local_rank)) if gpu else 0
-    if world > 1:
+    # MADPOSE_BENCH_DIST=1: a process group even for one rank, so the result gather runs
+    # through RCCL on a one-GPU box as it does on the 8-GPU node (configs[4]'s collective)
+    force_dist = os.environ.get("MADPOSE_BENCH_DIST") == "1"
+    if world > 1 or force_dist:
         backend = os.environ.get("MADPOSE_BENCH_DIST_BACKEND", "nccl" if gpu else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(dev)
-        dist.init_process_group(backend=backend)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+
+                with socket.socket() as s:
+                    s.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+            dist.init_process_group(backend=backend, rank=0, world_size=1)
+        else:
+            dist.init_process_group(backend=backend)
+    distributed = dist.is_available() and dist.is_initialized()
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier()
         if gpu:
             torch.cuda.synchronize()
 
     if a.workload == "scannet":
         run_scannet(a, wl, world, rank, dev, barrier, eng)
-        if world > 1:
+        if distributed:
             dist.destroy_process_group()
         return 0
 
@@ -696,7 +716,7 @@ def main(argv=None):
         if world == 1 and a.cpu_budget > 0:
             out["cpu_baseline"] = cpu_baseline(wl, pairs[a.warmup], a.cpu_budget, a.cpu_procs)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     return 0
 

@@ -142,6 +142,19 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
                     const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
                     double *errors, int device);
 
+/* mp_debug_score_batch: the estimator's scoring kernel (score_batch) on explicit
+ * model lists -- test hook.  models: num_iterations x M (M = 10 / 16 / 4 for the
+ * calibrated / shared-focal / two-focal variant, problem units), counts[b] of them
+ * used by iteration b.  best: the pre-batch best; flags: 1 the exact early exit
+ * against it, 2 the record skip.  Outputs per iteration: res_best, res_slot (bit 16:
+ * another model within the tie margin), rec_models[b] (the mapped record model,
+ * written when res_best[b] < best + tie); tie: the margin used. */
+int mp_debug_score_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                         const double *d1, const double *cam0, const double *cam1, const mp_ransac_options *options,
+                         const mp_estimator_config *config, int32_t num_iterations, const int32_t *counts,
+                         const mp_model *models, double best, int32_t flags, double *res_best, int32_t *res_slot,
+                         mp_model *rec_models, double *tie, int device);
+
 /* mp_debug_lo_sweep: the same models through the engine's host LO sweep
  * (madpose_amd/csrc/host/lo_sweep.h), the sweep LocalOptimization and
  * UpdateRANSACTerminationCriteria use (src/hybrid_ransac.h:265-349, 383-538): errors
@@ -213,18 +226,17 @@ int mp_relpose_5pt(const double *x1, const double *x2, mp_model *out, int max_ou
 /* mp_debug_pt5_roots: the engine's batched root stage of the calibrated 5-point
  * solver (the part of PoseLib relpose_5pt before pose recovery) over ns samples of
  * five normalized image points (pts0, pts1: ns x 5 x 2, identity intrinsics).
- * impl 0 = one lane per sample, 1 = one 16-lane group per sample (the default in
- * the estimator).  cand: ns x 96 doubles, 9 per essential matrix (ascending roots);
- * ncand: ns counts.  Test hook. */
+ * impl must be 1 (one 16-lane group per sample, the estimator's stage).  cand: ns x 96
+ * doubles, 9 per essential matrix (ascending roots); ncand: ns counts.  Test hook. */
 int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *pts1, double *cand, int32_t *ncand,
                        int device);
-/* mp_debug_pt_roots: the same for variant 0 (calibrated 5-point, as above) or 1
- * (shared-focal 6-point: the root stage of PoseLib relpose_6pt_shared_focal as
- * called at src/hybrid_pose_shared_focal_estimator.cpp:87; pts0/pts1: ns x 6 x 2
- * normalized points; cand per sample: the 3x9 epipolar null-space basis N, then the
- * positive roots u = f^2 of the degree-15 focal polynomial, ascending); for the
- * 6-point, impl 2 = one sample per 64-lane wave with the DFT nodes split over its four
- * groups (MADPOSE_PT6_WAVE=1 in the estimator; default impl 1).  Test hook. */
+/* mp_debug_pt_roots: the same for variant 0 (calibrated 5-point, impl 1, as above) or
+ * 1 (shared-focal 6-point, impl 3: the root stage of PoseLib relpose_6pt_shared_focal
+ * as called at src/hybrid_pose_shared_focal_estimator.cpp:87, by the deflated
+ * eigenproblem the estimator runs; pts0/pts1: ns x 6 x 2 normalized points; cand per
+ * sample: the 3x9 epipolar null-space basis N, then the positive roots u = f^2 of the
+ * degree-15 focal polynomial, ascending).  Other impl values return MP_EINVAL.  Test
+ * hook. */
 int mp_debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
                       int32_t *ncand, int device);
 
@@ -276,6 +288,8 @@ typedef struct mp_kernel_profile {
     uint64_t scored;          /* hypotheses whose score_batch sweep ran (the
                                  record skip drops iterations past a batch's
                                  first new best; `hypotheses` counts them)     */
+    uint64_t tie_checks;      /* iterations whose new-best decision was re-scored
+                                 in the reference's order (near ties)         */
 } mp_kernel_profile;
 int mp_profile_enable(int on);
 int mp_profile_reset(void);

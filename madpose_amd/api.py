@@ -694,6 +694,40 @@ def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_confi
     return (scores[:nm], errors[:nm]) if with_errors else scores[:nm]
 
 
+def debug_score_batch(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, iterations, best,
+                      exit=True, record_skip=True):
+    """The estimator's scoring kernel on explicit per-iteration model lists (test hook,
+    mp_debug_score_batch).  iterations: list of model lists (problem units).  Returns
+    (best scores, slots with the ambiguity bit, record models, tie margin)."""
+    x0 = _pts(x0, "x0")
+    x1 = _pts(x1, "x1")
+    n = x0.shape[0]
+    d0 = _vec(depth0, n, "depth0")
+    d1 = _vec(depth1, n, "depth1")
+    c0 = np.ascontiguousarray(np.asarray(cam0, dtype=np.float64).reshape(-1))
+    c1 = np.ascontiguousarray(np.asarray(cam1, dtype=np.float64).reshape(-1))
+    M = {0: 10, 1: 16, 2: 4, 3: 10}[variant]
+    B = len(iterations)
+    arr = (L.mp_model * (B * M))()
+    counts = np.zeros(B, dtype=np.int32)
+    for b, ms in enumerate(iterations):
+        counts[b] = len(ms)
+        for m, mod in enumerate(ms):
+            arr[b * M + m] = _model_to_c(mod, variant)
+    rb = np.zeros(B)
+    rs = np.zeros(B, dtype=np.int32)
+    rec = (L.mp_model * B)()
+    tie = ctypes.c_double(0.0)
+    o = options._to_c()
+    c = (est_config or EstimatorConfig())._to_c()
+    flags = (1 if exit else 0) | (2 if record_skip else 0)
+    L.check(L.lib().mp_debug_score_batch(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1),
+                                         ctypes.byref(o), ctypes.byref(c), B, counts.ctypes.data_as(L.c_int32_p),
+                                         arr, float(best), flags, _dp(rb), rs.ctypes.data_as(L.c_int32_p), rec,
+                                         ctypes.byref(tie), _DEFAULT_DEVICE))
+    return rb, rs, [_model_from_c(rec[b], variant) for b in range(B)], tie.value
+
+
 def device_count():
     return int(L.lib().mp_device_count())
 

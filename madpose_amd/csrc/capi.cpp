@@ -298,6 +298,27 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
     });
 }
 
+int mp_debug_score_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                         const double *d1, const double *cam0, const double *cam1, const mp_ransac_options *options,
+                         const mp_estimator_config *config, int32_t num_iterations, const int32_t *counts,
+                         const mp_model *models, double best, int32_t flags, double *res_best, int32_t *res_slot,
+                         mp_model *rec_models, double *tie, int device) {
+    return guarded([&]() {
+        if (!options || !counts || !models || !res_best || !res_slot || num_iterations <= 0)
+            throw std::invalid_argument("bad arguments");
+        const double md[2] = {0.0, 0.0};
+        mp::PairInput in = make_input(variant, n, x0, x1, d0, d1, md, cam0, cam1);
+        const int maxm = mp::max_models(variant == 3 ? 0 : variant);
+        std::vector<mp::Model> ms((size_t)num_iterations * maxm), rm(num_iterations);
+        std::memcpy(ms.data(), models, sizeof(mp_model) * ms.size());
+        mp::debug_score_batch(in, to_opts(options), to_cfg(config), num_iterations, counts, ms.data(), best, flags,
+                              res_best, res_slot, rm.data(), tie, device);
+        if (rec_models)
+            for (int b = 0; b < num_iterations; ++b) to_model(rm[b], &rec_models[b]);
+        return MP_OK;
+    });
+}
+
 int mp_debug_lo_sweep(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
                       const double *cam0, const double *cam1, const mp_ransac_options *options,
                       const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
@@ -354,8 +375,12 @@ static int point_direct(int kind, const double *x1, const double *x2, mp_model *
 int mp_debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
                       int32_t *ncand, int device) {
     if (!pts0 || !pts1 || !cand || !ncand) return fail(MP_EINVAL, "null pointer");
+    // impl names the estimator's root stage: 1 for the 5-point (16-lane groups), 3 for
+    // the 6-point (deflated eigenproblem); the round-2 alternates left the library
+    if ((variant == 0 && impl != 1) || (variant == 1 && impl != 3))
+        return fail(MP_EINVAL, "impl must be 1 (5-point group stage) or 3 (6-point eigen stage)");
     return guarded([&] {
-        mp::debug_pt_roots(variant, impl, ns, pts0, pts1, cand, ncand, device);
+        mp::debug_pt_roots(variant, ns, pts0, pts1, cand, ncand, device);
         return MP_OK;
     });
 }
@@ -451,6 +476,7 @@ int mp_profile_read(mp_kernel_profile *out) {
     out->model_trips_full = p.model_trips_full;
     out->accepted = p.accepted;
     out->scored = p.scored;
+    out->tie_checks = p.tie_checks;
     return MP_OK;
 }
 

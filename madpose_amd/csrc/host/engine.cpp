@@ -166,29 +166,28 @@ class Sampler {
 };
 
 // ---------------------------------------------------------------------------
-// Zero-copy LO sweep resources of one issuing thread: errors (3 x n) and the score
-// land in host-coherent pinned memory, completion is a flag raised by the kernel.
-// Two result buffers used alternately: the issuer reads a result in place while the
-// next sweep writes the other buffer, so nothing is copied out.
+// Device resources of one LO lane (the estimator thread or an LO worker): a stream and
+// the staging of the opt-in device LM (MADPOSE_DEVICE_LM).  The LO sweeps themselves
+// run on the lane's own core (host/lo_sweep.h).
 struct SweepSlot {
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    int64_t cap = 0;
-    double *h_out = nullptr, *d_out = nullptr;
-    double *h_out2 = nullptr, *d_out2 = nullptr;
-    int flip = 0;
-    int *h_flag = nullptr, *d_flag = nullptr; // one completion flag per workgroup
-    int seq = 0;
-    // device-LM staging (MADPOSE_DEVICE_LM): job + index lists up, model + status down
+    // device-LM staging: job + index lists up, model + status down
     int64_t lm_cap = 0;
     char *h_lm = nullptr, *d_lm = nullptr;
     hipEvent_t lm_done = nullptr; // blocking-sync event: the waiting thread sleeps
 
     void ensure_lm(int64_t nidx) {
+        if (!stream) {
+            MP_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+            own_stream = true;
+        }
         if (!lm_done) MP_HIP(hipEventCreateWithFlags(&lm_done, hipEventBlockingSync | hipEventDisableTiming));
         if (nidx <= lm_cap) return;
         if (h_lm) hipHostFree(h_lm);
         if (d_lm) hipFree(d_lm);
+        h_lm = d_lm = nullptr;
+        lm_cap = 0;
         const size_t bytes = lm_bytes(nidx);
         MP_HIP(hipHostMalloc(&h_lm, bytes, hipHostMallocDefault));
         MP_HIP(hipMalloc(&d_lm, bytes));
@@ -196,51 +195,6 @@ struct SweepSlot {
     }
     // layout: LmJob | Model out | int status | pad | int idx[nidx]
     static size_t lm_bytes(int64_t nidx) { return 512 + sizeof(int) * (size_t)nidx; }
-
-    void release() {
-        if (h_out) hipHostFree(h_out);
-        if (h_out2) hipHostFree(h_out2);
-        if (h_flag) hipHostFree(h_flag);
-        h_out = d_out = nullptr;
-        h_out2 = d_out2 = nullptr;
-        h_flag = d_flag = nullptr;
-        cap = 0;
-    }
-    // stream: the owner's stream (slot 0) or nullptr for a stream of its own
-    void ensure(int64_t nn, hipStream_t borrowed) {
-        if (!stream) {
-            if (borrowed) {
-                stream = borrowed;
-            } else {
-                // MADPOSE_SWEEP_PRIORITY=1: the device's highest stream priority, so LO
-                // sweeps dispatch ahead of a speculative batch's queued workgroups
-                static const bool prio = [] {
-                    const char *e = std::getenv("MADPOSE_SWEEP_PRIORITY");
-                    return e && e[0] == '1';
-                }();
-                if (prio) {
-                    int lo = 0, hi = 0;
-                    MP_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                    MP_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
-                } else {
-                    MP_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-                }
-                own_stream = true;
-            }
-        }
-        if (nn <= cap) return;
-        release();
-        const int nb = sweep_blocks(nn), np = nb * sweep_waves_per_block();
-        MP_HIP(hipHostMalloc(&h_out, sizeof(double) * (3 * nn + np), hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostMalloc(&h_out2, sizeof(double) * (3 * nn + np), hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostMalloc(&h_flag, sizeof(int) * nb, hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostGetDevicePointer((void **)&d_out, h_out, 0));
-        MP_HIP(hipHostGetDevicePointer((void **)&d_out2, h_out2, 0));
-        MP_HIP(hipHostGetDevicePointer((void **)&d_flag, h_flag, 0));
-        for (int b = 0; b < nb; ++b) h_flag[b] = seq;
-        MP_HIP(hipStreamSynchronize(stream));
-        cap = nn;
-    }
 };
 
 // Worker threads for the parallel LO steps: run(n, f) calls f(job, lane) for jobs
@@ -350,8 +304,7 @@ struct DeviceCtx {
     double *d_pt_cand = nullptr, *d_pt_pen = nullptr;
     int *d_pt_ncand = nullptr, *d_pt_valid = nullptr;
     Model *d_pt_slots = nullptr;
-    // LO sweep issuers: slot 0 on `stream` (the estimator thread), slots 1.. with
-    // streams of their own (parallel LO steps)
+    // device resources of the LO lanes (lane 0: the estimator thread)
     SweepSlot sweep_slot[kLoLanes];
     std::unique_ptr<LoWorkers> lo_workers; // created on first parallel LO
     // pinned host mirrors
@@ -397,7 +350,6 @@ struct DeviceCtx {
         h_rec1 = nullptr;
         h_model1 = nullptr;
         h_recmodel = d_recmodel = nullptr;
-        for (auto &sl : sweep_slot) sl.release();
         cap_n = 0;
         cap_b = cap_m = 0;
     }
@@ -437,8 +389,6 @@ struct DeviceCtx {
         MP_HIP(hipHostMalloc(&h_model1, sizeof(Model) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_recmodel, sizeof(Model) * (size_t)bb, hipHostMallocMapped | hipHostMallocCoherent));
         MP_HIP(hipHostGetDevicePointer((void **)&d_recmodel, h_recmodel, 0));
-        // (a stream of its own: the post-LO batch runs on `stream` while LO sweeps)
-        sweep_slot[0].ensure(nn, nullptr);
         cap_n = nn;
         cap_b = bb;
         cap_m = mm;
@@ -580,7 +530,7 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
         C.loss_scale = 1.0 / (s * s);
         // upper-triangular intrinsics with unit last row: the score kernels' ray form
         auto tri = [](const double *K) { return K[3] == 0.0 && K[6] == 0.0 && K[7] == 0.0 && K[8] == 1.0; };
-        C.kstd = (tri(C.K0) && tri(C.K1) && tri(C.K0i) && tri(C.K1i) && !std::getenv("MADPOSE_SCORE_MATRIX_FORM")) ? 1 : 0;
+        C.kstd = (tri(C.K0) && tri(C.K1) && tri(C.K0i) && tri(C.K1i)) ? 1 : 0;
     } else {
         double scale = 0.0;
         for (int i = 0; i < n; ++i) {
@@ -682,6 +632,10 @@ class Run {
         const char *env3 = std::getenv("MADPOSE_BATCH_GROWTH");
         growth_ = env3 ? std::max(0.01, std::atof(env3)) : 1.0;
         trace_ = std::getenv("MADPOSE_TRACE") != nullptr;
+        double M = 0.0;
+        for (int t = 0; t < 3; ++t) M += P.C.thr[t] * std::fabs(P.C.w[t]);
+        const char *ts = std::getenv("MADPOSE_TIE_SCALE");
+        tie_ = 4e-12 * std::max(n_, 64) * M * (ts ? std::max(1.0, std::atof(ts)) : 1.0);
     }
 
     void run(Model *best, Stats *S);
@@ -698,6 +652,16 @@ class Run {
     int max_batch_, min_batch_;
     double growth_; // batch = growth_ x iterations so far (MADPOSE_BATCH_GROWTH)
     bool trace_ = false;
+    // Tie margin: an absolute bound on |device score_batch sum - reference-order sum| of
+    // one model.  Every MSAC term is min(e, thr_t) w_t with e >= 0, so |term| <=
+    // thr_t |w_t| and a sum has |terms| <= M = n (thr_0 |w_0| + thr_1 |w_1| + thr_2 |w_2|);
+    // either summation order is within gamma_{3n} M ~ 3n eps M of the exact sum and the
+    // two residual forms differ by a few ulp per term, so the margin 4e-12 M holds for
+    // n up to ~5000 with room (it is the bound the early exit, the record skip and the
+    // host's near-tie resolution use).  MADPOSE_TIE_SCALE multiplies it (tests force the
+    // resolution path with a large factor).
+    double tie_ = 0.0;
+    uint64_t tie_checks_ = 0;
     PairData D_;
     Stats *S_ = nullptr;
     IterationStream rs_; // sampler + selection/LO streams
@@ -716,7 +680,7 @@ class Run {
         const double *err = nullptr; // the buffer holding the last result
         std::vector<double> herr;    // host sweeps' errors (3 x n)
         uint64_t count = 0;
-        double t[3] = {0, 0, 0}; // launch / wait / copy seconds (MADPOSE_SWEEP_TIMING)
+        double t[3] = {0, 0, 0}; // -, sweep, - seconds (MADPOSE_SWEEP_TIMING)
     };
     Lane lanes_[kLoLanes]; // lanes_[0]: the estimator thread
     // LO phase seconds (MADPOSE_LO_TIMING): serial prefix, steps phase, LO count, sum of
@@ -726,9 +690,9 @@ class Run {
     double lo_t_[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool lo_parallel_ = true;
 
-    // LO sweeps on the issuing thread's core (host/lo_sweep.h; the default) or through
-    // the device kernel sweep_host (MADPOSE_LO_SWEEP=device, A/B)
-    bool host_sweep_ = true;
+    // LO sweeps run on the issuing thread's core (host/lo_sweep.h): the reference's
+    // residual operations and ScoreModel order, bit-identical to the oracle; a lane
+    // keeps its last result (LO asks for the same model's score and inliers in turn)
     LoSweepData hsw_;
     const double *sweep(Lane &L, const Model &m, double *score) {
         if (L.valid && std::memcmp(&m, &L.model, sizeof(Model)) == 0) {
@@ -736,62 +700,15 @@ class Run {
             return L.err;
         }
         auto t_sw = Clock::now();
-        if (host_sweep_) {
-            if (L.herr.size() < 3 * (size_t)n_) L.herr.resize(3 * (size_t)n_);
-            L.score = lo_sweep(P_.C, hsw_, m, L.herr.data());
-            L.err = L.herr.data();
-            L.model = m;
-            L.valid = true;
-            L.count++;
-            const double dt = secs(t_sw);
-            L.t[1] += dt;
-            if (g_prof_on.load(std::memory_order_relaxed)) {
-                std::lock_guard<std::mutex> lk(g_prof_mu);
-                g_prof.sweeps += 1;
-                g_prof.sweep_wall_ms += 1e3 * dt;
-            }
-            *score = L.score;
-            return L.err;
-        }
-        ScoreRec rec;
-        prepare_score_rec(P_.C, m, rec);
-        SweepSlot &sl = *L.slot;
-        const int seq = ++sl.seq;
-        sl.flip ^= 1;
-        double *d_out = sl.flip ? sl.d_out2 : sl.d_out;
-        const double *h_out = sl.flip ? sl.h_out2 : sl.h_out;
-        MP_HIP(launch_sweep_host(sl.stream, D_, P_.C, rec, d_out, sl.d_flag, seq));
-        const double t_launched = secs(t_sw);
-        // poll the workgroups' completion flags; after 2 s fall back to a stream sync,
-        // which also surfaces any kernel error
-        const int nb = sweep_blocks(n_);
-        for (int b = 0; b < nb; ++b) {
-            for (uint64_t spin = 0; __atomic_load_n(sl.h_flag + b, __ATOMIC_ACQUIRE) != seq; ++spin) {
-                if ((spin & 1023) == 1023 && secs(t_sw) > 2.0) {
-                    MP_HIP(hipStreamSynchronize(sl.stream));
-                    if (__atomic_load_n(sl.h_flag + b, __ATOMIC_ACQUIRE) != seq)
-                        throw std::runtime_error("LO sweep did not signal completion");
-                }
-            }
-        }
-        double total = 0.0; // partial scores: waves in order within a workgroup, workgroups in order
-        const int W = sweep_waves_per_block();
-        for (int b = 0; b < nb; ++b) {
-            double sb = 0.0;
-            for (int w = 0; w < W; ++w) sb += h_out[3 * n_ + W * b + w];
-            total += sb;
-        }
-        const double t_done = secs(t_sw);
-        L.err = h_out;
-        L.t[0] += t_launched;
-        L.t[1] += t_done - t_launched;
-        L.t[2] += secs(t_sw) - t_done;
+        if (L.herr.size() < 3 * (size_t)n_) L.herr.resize(3 * (size_t)n_);
+        L.score = lo_sweep(P_.C, hsw_, m, L.herr.data());
+        L.err = L.herr.data();
         L.model = m;
-        L.score = total;
         L.valid = true;
         L.count++;
+        const double dt = secs(t_sw);
+        L.t[1] += dt;
         if (g_prof_on.load(std::memory_order_relaxed)) {
-            const double dt = secs(t_sw);
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.sweeps += 1;
             g_prof.sweep_wall_ms += 1e3 * dt;
@@ -1219,7 +1136,7 @@ class Run {
         if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
         if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
-        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res, best,
+        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res, best, tie_,
                                   prof ? X_.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
                                   X_.d_models, X_.d_recmodel));
         if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
@@ -1227,20 +1144,41 @@ class Run {
         if (prof) MP_HIP(hipMemcpyAsync(X_.h_work, X_.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     }
 
-    // the model of a new best: score_batch wrote it to the mapped record slot of its
-    // iteration (the batch's stream has been synchronized); MADPOSE_FETCH_MODEL=1 copies
-    // it from the device instead (A/B)
-    Model fetch_model(int b, int slot) {
-        static const bool copy = [] {
-            const char *e = std::getenv("MADPOSE_FETCH_MODEL");
-            return e && e[0] == '1';
-        }();
-        if (!copy) return X_.h_recmodel[b];
-        MP_HIP(hipMemcpyAsync(X_.h_model1, X_.d_models + (size_t)b * maxm_ + slot, sizeof(Model),
+    // Reference-order score of a model (host/lo_sweep.h), on lane 0: the LO that follows
+    // a new best starts with a sweep of the same model and finds it cached.
+    double exact_score(const Model &m) { return score(lanes_[0], m); }
+
+    // Iteration j of the last batch could hold a new best but its device best is within
+    // the tie margin of best_min_score, or another of its models is within the margin of
+    // its best: re-score the contenders in the reference's order and take the first
+    // minimum (GetBestEstimatedModelId, src/hybrid_ransac.h:245-263).  Models whose
+    // device score is more than the margin above the device best cannot be the exact
+    // winner.  Rare (tests/test_engine_gpu.py::test_tie_margin_inflated forces it).
+    void resolve_tie(uint32_t j, Model *out, double *out_score) {
+        const int nm = X_.h_res[j].count;
+        const double bl = X_.h_res[j].best;
+        std::vector<double> dsc(nm);
+        std::vector<Model> ms(nm);
+        MP_HIP(hipMemcpyAsync(dsc.data(), X_.d_scores + (size_t)j * maxm_, sizeof(double) * nm,
                               hipMemcpyDeviceToHost, X_.stream));
+        MP_HIP(hipMemcpyAsync(ms.data(), X_.d_models + (size_t)j * maxm_, sizeof(Model) * nm, hipMemcpyDeviceToHost,
+                              X_.stream));
         MP_HIP(hipStreamSynchronize(X_.stream));
-        return X_.h_model1[0];
+        *out_score = kMax;
+        for (int m = 0; m < nm; ++m) {
+            if (!(dsc[m] < kMax) || !(dsc[m] <= bl + tie_)) continue;
+            const double e = exact_score(ms[m]);
+            if (e < *out_score) { // strict '<': the first minimum wins
+                *out_score = e;
+                *out = ms[m];
+            }
+        }
+        ++tie_checks_;
     }
+
+    // the model of a new best: score_batch wrote it to the mapped record slot of its
+    // iteration (the batch's stream has been synchronized)
+    Model fetch_model(int b, int /*slot*/) { return X_.h_recmodel[b]; }
 };
 
 void Run::run(Model *best, Stats *S) {
@@ -1272,19 +1210,14 @@ void Run::run(Model *best, Stats *S) {
         lo_parallel_ = !(e && e[0] == '0') && o_.num_lo_steps > 1;
         const char *d = std::getenv("MADPOSE_DEVICE_LM");
         device_lm_ = d && d[0] == '1';
-        const char *hs = std::getenv("MADPOSE_LO_SWEEP");
-        host_sweep_ = !(hs && std::strcmp(hs, "device") == 0);
     }
     if (lo_parallel_) {
         const int nl = lo_lanes_setting();
         if (!X_.lo_workers || X_.lo_workers->lanes() != nl) X_.lo_workers.reset(new LoWorkers(nl));
-        for (int l = 1; l < nl; ++l) {
-            X_.sweep_slot[l].ensure(X_.cap_n, nullptr);
-            lanes_[l].slot = &X_.sweep_slot[l];
-        }
+        for (int l = 1; l < nl; ++l) lanes_[l].slot = &X_.sweep_slot[l];
     }
     upload_pair(X_, P_, &D_);
-    if (host_sweep_) lo_sweep_prepare(P_.C, P_.H.x0.data(), P_.H.x1.data(), P_.H.d0.data(), P_.H.d1.data(), &hsw_);
+    lo_sweep_prepare(P_.C, P_.H.x0.data(), P_.H.x1.data(), P_.H.d0.data(), P_.H.d1.data(), &hsw_);
     rs_.n = n_;
     rs_.seed(o_.random_seed);
 
@@ -1412,13 +1345,33 @@ void Run::run(Model *best, Stats *S) {
             S->num_hypotheses += (uint64_t)nm;
             bool lo_here = false;
             if (nm > 0) {
+                // The device sums screen; the decision is taken on reference-order sums
+                // (exact_score) -- see tie_margin.  `maybe`: the iteration could hold a new
+                // best; `certain`: it does, and its best model is unambiguous.
                 const double bl = X_.h_res[j].best;
-                if (bl < best_min_score || iter == lo_start) {
-                    const bool new_best = bl < best_min_score;
+                const int raw = X_.h_res[j].slot;
+                const bool maybe = best_min_score == kMax ? bl < kMax : bl < best_min_score + tie_;
+                if (maybe || iter == lo_start) {
+                    bool new_best = false;
+                    if (maybe) {
+                        const bool certain = best_min_score == kMax || bl < best_min_score - tie_;
+                        Model m;
+                        double e = kMax;
+                        if (certain && !(raw & kSlotAmbiguous)) {
+                            m = fetch_model((int)j, raw & kSlotMask);
+                            e = exact_score(m);
+                        } else {
+                            resolve_tie(j, &m, &e);
+                        }
+                        if (e < best_min_score) {
+                            new_best = true;
+                            best_min = m;
+                            best_min_score = e;
+                        }
+                    }
                     if (new_best) {
-                        if (trace_) std::fprintf(stderr, "[engine] it=%u new best %.17g (solver %d, %d models)\n", iter, bl, st, nm);
-                        best_min_score = bl;
-                        best_min = fetch_model((int)j, X_.h_res[j].slot);
+                        if (trace_) std::fprintf(stderr, "[engine] it=%u new best %.17g (device %.17g, solver %d, %d models)\n",
+                                                 iter, best_min_score, bl, st, nm);
                         update_best(best_min_score, best_min, st, &S->best_model_score, best, &S->best_solver_type);
                     }
                     const bool run_lo = iter >= lo_start && best_min_score < kMax;
@@ -1534,15 +1487,15 @@ void Run::run(Model *best, Stats *S) {
                      1e6 * lo_t_[8] / lo_t_[2], 1e6 * lo_t_[9] / lo_t_[2], 1e6 * lo_t_[10] / lo_t_[2],
                      1e6 * lo_t_[11] / lo_t_[2], 1e6 * lo_t_[12] / lo_t_[2], lo_t_[13] / lo_t_[2]);
     if (std::getenv("MADPOSE_SWEEP_TIMING") && S->num_lo_sweeps > 0)
-        std::fprintf(stderr, "[engine] %llu sweeps: launch %.2f us, wait %.2f us, copy %.2f us (avg)\n",
-                     (unsigned long long)S->num_lo_sweeps, 1e6 * tsum[0] / S->num_lo_sweeps,
-                     1e6 * tsum[1] / S->num_lo_sweeps, 1e6 * tsum[2] / S->num_lo_sweeps);
+        std::fprintf(stderr, "[engine] %llu host sweeps: %.2f us (avg)\n", (unsigned long long)S->num_lo_sweeps,
+                     1e6 * tsum[1] / S->num_lo_sweeps);
     if (g_prof_on.load(std::memory_order_relaxed)) {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof.sample_wall_ms += 1e3 * sample_s_;
         g_prof.wait_wall_ms += 1e3 * S->seconds_gpu_wait;
         g_prof.run_wall_ms += 1e3 * S->seconds_total;
         g_prof.accepted += S->num_hypotheses;
+        g_prof.tie_checks += tie_checks_;
     }
 }
 
@@ -1635,6 +1588,56 @@ void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const Estim
         scores[m] = lo_sweep(P.C, D, models[m], err.data());
         if (errors) std::memcpy(errors + (size_t)m * 3 * in.n, err.data(), sizeof(double) * 3 * in.n);
     }
+}
+
+// score_batch on explicit per-iteration model lists (mp_debug_score_batch, test hook):
+// the estimator's launch with the pre-batch best `best`, its tie margin, and the exact
+// early exit / record skip as flags allow; results and record models back
+void debug_score_batch(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nb,
+                       const int *counts, const Model *models, double best, int flags, double *res_best,
+                       int *res_slot, Model *rec_models, double *tie_out, int device) {
+    validate(in, opts);
+    const int v = in.variant == kScaleOnly ? kCal : in.variant;
+    const int maxm = max_models(v);
+    if (nb <= 0 || nb > (1 << 20)) throw std::invalid_argument("bad iteration count");
+    for (int b = 0; b < nb; ++b)
+        if (counts[b] < 0 || counts[b] > maxm) throw std::invalid_argument("model count out of range");
+    CtxLease lease(device);
+    DeviceCtx &X = *lease.c;
+    Problem P = make_problem(in, opts, cfg);
+    X.ensure(in.n, nb, maxm);
+    PairData D;
+    upload_pair(X, P, &D);
+    std::vector<ScoreRec> recs((size_t)nb * maxm);
+    std::vector<Model> ms((size_t)nb * maxm);
+    std::memset(ms.data(), 0, sizeof(Model) * ms.size());
+    std::memset(recs.data(), 0, sizeof(ScoreRec) * recs.size());
+    for (int b = 0; b < nb; ++b)
+        for (int m = 0; m < counts[b]; ++m) {
+            ms[(size_t)b * maxm + m] = models[(size_t)b * maxm + m];
+            prepare_score_rec(P.C, ms[(size_t)b * maxm + m], recs[(size_t)b * maxm + m]);
+        }
+    double M = 0.0;
+    for (int t = 0; t < 3; ++t) M += P.C.thr[t] * std::fabs(P.C.w[t]);
+    const double tie = 4e-12 * std::max<int64_t>(in.n, 64) * M;
+    if (tie_out) *tie_out = tie;
+    MP_HIP(hipMemcpyAsync(X.d_recs, recs.data(), sizeof(ScoreRec) * recs.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemcpyAsync(X.d_models, ms.data(), sizeof(Model) * ms.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemcpyAsync(X.d_counts, counts, sizeof(int) * nb, hipMemcpyHostToDevice, X.stream));
+    std::memset(X.h_recmodel, 0, sizeof(Model) * nb);
+    const bool exit = (flags & 1) != 0, skip = (flags & 2) != 0;
+    const unsigned epoch_hi = ~(++X.epoch);
+    MP_HIP(launch_score_batch(X.stream, D, P.C, X.d_recs, X.d_counts, nb, maxm, X.d_scores, X.d_res,
+                              exit ? best : DBL_MAX, tie, nullptr, skip ? X.d_recword : nullptr, epoch_hi, X.d_models,
+                              X.d_recmodel));
+    std::vector<IterResult> res(nb);
+    MP_HIP(hipMemcpyAsync(res.data(), X.d_res, sizeof(IterResult) * nb, hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipStreamSynchronize(X.stream));
+    for (int b = 0; b < nb; ++b) {
+        res_best[b] = res[b].best;
+        res_slot[b] = res[b].slot;
+    }
+    if (rec_models) std::memcpy(rec_models, X.h_recmodel, sizeof(Model) * nb);
 }
 
 namespace {
@@ -1747,26 +1750,18 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
     std::memcpy(in.data() + 3 * k, y, sizeof(double) * 3 * k);
     std::memcpy(in.data() + 6 * k, dx, sizeof(double) * k);
     std::memcpy(in.data() + 7 * k, dy, sizeof(double) * k);
-    double *d_in, *d_sols;
-    int *d_n;
-    Model *d_poses;
-    MP_HIP(hipMalloc(&d_in, sizeof(double) * in.size()));
-    MP_HIP(hipMalloc(&d_sols, sizeof(double) * 8 * 6));
-    MP_HIP(hipMalloc(&d_n, sizeof(int) * 2));
-    MP_HIP(hipMalloc(&d_poses, sizeof(Model) * 8));
-    MP_HIP(hipMemcpyAsync(d_in, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, X.stream));
-    MP_HIP(launch_md_direct(X.stream, variant, alt, d_in, d_sols, d_n, d_poses, d_n + 1));
+    DevArray<double> d_in(in.size()), d_sols(8 * 6);
+    DevArray<int> d_n(2);
+    DevArray<Model> d_poses(8);
+    MP_HIP(hipMemcpyAsync(d_in.p, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_md_direct(X.stream, variant, alt, d_in.p, d_sols.p, d_n.p, d_poses.p, d_n.p + 1));
     double hs[48];
     int hn[2];
     Model hp[8];
-    MP_HIP(hipMemcpyAsync(hs, d_sols, sizeof(hs), hipMemcpyDeviceToHost, X.stream));
-    MP_HIP(hipMemcpyAsync(hn, d_n, sizeof(hn), hipMemcpyDeviceToHost, X.stream));
-    MP_HIP(hipMemcpyAsync(hp, d_poses, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(hs, d_sols.p, sizeof(hs), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(hn, d_n.p, sizeof(hn), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(hp, d_poses.p, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));
-    hipFree(d_in);
-    hipFree(d_sols);
-    hipFree(d_n);
-    hipFree(d_poses);
     const int w = variant == kCal ? 4 : (variant == kSF ? 5 : 6);
     for (int i = 0; i < std::min(hn[0], max_sols); ++i)
         for (int c = 0; c < w; ++c) sols[i * w + c] = hs[i * w + c];
@@ -1777,12 +1772,12 @@ int solve_md_direct(int variant, const double *x, const double *y, const double 
 
 int solve_point_direct(int kind, const double *x1, const double *x2, Model *poses, int max_poses, int device) {
     if (kind < 0 || kind > 2) throw std::invalid_argument("point solver kind must be 0, 1 or 2");
-    if (kind == 1 && !pt6_dft()) {
+    if (kind == 1) {
         // the estimator's root stage (deflated eigenproblem) on this one sample, then
         // its poses
         double cand[kPtCandStride];
         int nc = 0;
-        debug_pt_roots(kSF, 3, 1, x1, x2, cand, &nc, device);
+        debug_pt_roots(kSF, 1, x1, x2, cand, &nc, device);
         CtxLease lease(device);
         DeviceCtx &X = *lease.c;
         double in[24];
@@ -1806,35 +1801,27 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
     }
     CtxLease lease(device);
     DeviceCtx &X = *lease.c;
-    const int per = kind == 0 ? 15 : (kind == 1 ? 12 : 14);
+    const int per = kind == 0 ? 15 : 14;
     double in[30];
     std::memcpy(in, x1, sizeof(double) * per);
     std::memcpy(in + per, x2, sizeof(double) * per);
-    double *d_in;
-    int *d_n;
-    Model *d_poses;
     constexpr int kCap = 16;
-    MP_HIP(hipMalloc(&d_in, sizeof(in)));
-    MP_HIP(hipMalloc(&d_n, sizeof(int)));
-    MP_HIP(hipMalloc(&d_poses, sizeof(Model) * kCap));
-    MP_HIP(hipMemcpyAsync(d_in, in, sizeof(in), hipMemcpyHostToDevice, X.stream));
-    MP_HIP(launch_point_direct(X.stream, kind, d_in, d_poses, d_n));
+    DevArray<double> d_in(30);
+    DevArray<int> d_n(1);
+    DevArray<Model> d_poses(kCap);
+    MP_HIP(hipMemcpyAsync(d_in.p, in, sizeof(in), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_point_direct(X.stream, kind, d_in.p, d_poses.p, d_n.p));
     int hn = 0;
     Model hp[kCap];
-    MP_HIP(hipMemcpyAsync(&hn, d_n, sizeof(int), hipMemcpyDeviceToHost, X.stream));
-    MP_HIP(hipMemcpyAsync(hp, d_poses, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(&hn, d_n.p, sizeof(int), hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(hp, d_poses.p, sizeof(hp), hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));
-    hipFree(d_in);
-    hipFree(d_n);
-    hipFree(d_poses);
     for (int i = 0; i < std::min(std::min(hn, kCap), max_poses); ++i) poses[i] = hp[i];
     return hn;
 }
 
-void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
-                    int *ncand, int device) {
-    if (impl < 0 || impl > (variant == 1 ? 3 : 1))
-        throw std::invalid_argument("impl must be 0 (lane), 1 (group) or, for the 6-point, 2 (wave) or 3 (eigen)");
+void debug_pt_roots(int variant, int64_t ns, const double *pts0, const double *pts1, double *cand, int *ncand,
+                    int device) {
     if (variant != kCal && variant != kSF) throw std::invalid_argument("variant must be 0 (5pt) or 1 (6pt)");
     if (ns <= 0 || ns > (1 << 22)) throw std::invalid_argument("bad number of samples");
     CtxLease lease(device);
@@ -1857,13 +1844,10 @@ void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const
         list[s] = (int)s;
         for (int j = 0; j < K; ++j) smp[8 * s + j] = (int)(K * s + j);
     }
-    double *d_pair, *d_cand;
-    int *d_smp, *d_list, *d_n;
-    MP_HIP(hipMalloc(&d_pair, sizeof(double) * host.size()));
-    MP_HIP(hipMalloc(&d_cand, sizeof(double) * kPtCandStride * (size_t)ns));
-    MP_HIP(hipMalloc(&d_smp, sizeof(int) * smp.size()));
-    MP_HIP(hipMalloc(&d_list, sizeof(int) * list.size()));
-    MP_HIP(hipMalloc(&d_n, sizeof(int) * (size_t)ns));
+    DevArray<double> d_pair_a(host.size()), d_cand_a(kPtCandStride * (size_t)ns);
+    DevArray<int> d_smp_a(smp.size()), d_list_a(list.size()), d_n_a((size_t)ns);
+    double *d_pair = d_pair_a.p, *d_cand = d_cand_a.p;
+    int *d_smp = d_smp_a.p, *d_list = d_list_a.p, *d_n = d_n_a.p;
     MP_HIP(hipMemcpyAsync(d_pair, host.data(), sizeof(double) * host.size(), hipMemcpyHostToDevice, X.stream));
     MP_HIP(hipMemcpyAsync(d_smp, smp.data(), sizeof(int) * smp.size(), hipMemcpyHostToDevice, X.stream));
     MP_HIP(hipMemcpyAsync(d_list, list.data(), sizeof(int) * list.size(), hipMemcpyHostToDevice, X.stream));
@@ -1874,27 +1858,22 @@ void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const
     C.variant = variant;
     C.n = (int)np;
     for (int k = 0; k < 9; ++k) C.K0[k] = C.K1[k] = C.K0i[k] = C.K1i[k] = (k % 4 == 0) ? 1.0 : 0.0;
-    DevArray<double> d_pen(impl == 3 ? (size_t)ns * kPtPenStride : 1);
-    MP_HIP(launch_pt_roots(X.stream, D, C, d_list, (int)ns, d_smp, d_cand, d_n, impl, d_pen.p));
+    DevArray<double> d_pen(variant == kSF ? (size_t)ns * kPtPenStride : 1);
+    MP_HIP(launch_pt_roots(X.stream, D, C, d_list, (int)ns, d_smp, d_cand, d_n, d_pen.p));
     MP_HIP(hipMemcpyAsync(cand, d_cand, sizeof(double) * kPtCandStride * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipMemcpyAsync(ncand, d_n, sizeof(int) * (size_t)ns, hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));
-    for (void *p : {(void *)d_pair, (void *)d_cand, (void *)d_smp, (void *)d_list, (void *)d_n}) hipFree(p);
 }
 
 void bougnoux_batch(int64_t k, const double *F, double *out, int device) {
     if (k <= 0) return;
     CtxLease lease(device);
     hipStream_t s = lease.c->stream;
-    double *d_F, *d_out;
-    MP_HIP(hipMalloc(&d_F, sizeof(double) * 9 * (size_t)k));
-    MP_HIP(hipMalloc(&d_out, sizeof(double) * 2 * (size_t)k));
-    MP_HIP(hipMemcpyAsync(d_F, F, sizeof(double) * 9 * (size_t)k, hipMemcpyHostToDevice, s));
-    MP_HIP(launch_bougnoux(s, d_F, k, d_out));
-    MP_HIP(hipMemcpyAsync(out, d_out, sizeof(double) * 2 * (size_t)k, hipMemcpyDeviceToHost, s));
+    DevArray<double> d_F(9 * (size_t)k), d_out(2 * (size_t)k);
+    MP_HIP(hipMemcpyAsync(d_F.p, F, sizeof(double) * 9 * (size_t)k, hipMemcpyHostToDevice, s));
+    MP_HIP(launch_bougnoux(s, d_F.p, k, d_out.p));
+    MP_HIP(hipMemcpyAsync(out, d_out.p, sizeof(double) * 2 * (size_t)k, hipMemcpyDeviceToHost, s));
     MP_HIP(hipStreamSynchronize(s));
-    MP_HIP(hipFree(d_F));
-    MP_HIP(hipFree(d_out));
 }
 
 void pose_eval_batch(int64_t k, const double *R, const double *t, const double *T, double t_thres, double *err_t,
@@ -1911,8 +1890,8 @@ void pose_eval_batch(int64_t k, const double *R, const double *t, const double *
     std::memcpy(host.data(), R, sizeof(double) * 9 * k);
     std::memcpy(host.data() + 9 * k, t, sizeof(double) * 3 * k);
     std::memcpy(host.data() + 12 * k, T, sizeof(double) * 16 * k);
-    double *d;
-    MP_HIP(hipMalloc(&d, sizeof(double) * tot));
+    DevArray<double> d_all(tot);
+    double *d = d_all.p;
     double *d_et = d + in, *d_eR = d_et + k, *d_max = d_eR + k, *d_sorted = d_max + k, *d_thr = d_sorted + k,
            *d_auc = d_thr + nthr;
     MP_HIP(hipMemcpyAsync(d, host.data(), sizeof(double) * in, hipMemcpyHostToDevice, s));
@@ -1923,7 +1902,6 @@ void pose_eval_batch(int64_t k, const double *R, const double *t, const double *
     MP_HIP(hipMemcpyAsync(err_R, d_eR, sizeof(double) * k, hipMemcpyDeviceToHost, s));
     if (nthr > 0) MP_HIP(hipMemcpyAsync(aucs, d_auc, sizeof(double) * nthr, hipMemcpyDeviceToHost, s));
     MP_HIP(hipStreamSynchronize(s));
-    MP_HIP(hipFree(d));
 }
 
 void pose_auc_batch(int64_t k, const double *errors, int nthr, const double *thr, double *aucs, int device) {
@@ -1934,15 +1912,14 @@ void pose_auc_batch(int64_t k, const double *errors, int nthr, const double *thr
     }
     CtxLease lease(device);
     hipStream_t s = lease.c->stream;
-    double *d; // errors (k) | sorted (k) | thresholds, aucs (2 nthr)
-    MP_HIP(hipMalloc(&d, sizeof(double) * (2 * (size_t)k + 2 * (size_t)nthr)));
+    DevArray<double> d_all(2 * (size_t)k + 2 * (size_t)nthr); // errors (k) | sorted (k) | thresholds, aucs
+    double *d = d_all.p;
     double *d_sorted = d + k, *d_thr = d_sorted + k, *d_auc = d_thr + nthr;
     MP_HIP(hipMemcpyAsync(d, errors, sizeof(double) * k, hipMemcpyHostToDevice, s));
     MP_HIP(hipMemcpyAsync(d_thr, thr, sizeof(double) * nthr, hipMemcpyHostToDevice, s));
     MP_HIP(launch_pose_auc(s, k, d, d_sorted, nthr, d_thr, d_auc));
     MP_HIP(hipMemcpyAsync(aucs, d_auc, sizeof(double) * nthr, hipMemcpyDeviceToHost, s));
     MP_HIP(hipStreamSynchronize(s));
-    MP_HIP(hipFree(d));
 }
 
 void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *dims, const int64_t *pt_off,
@@ -1966,16 +1943,12 @@ void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *d
     const int64_t total = pt_off[num], cells = map_off[num];
     CtxLease lease(device);
     hipStream_t s = lease.c->stream;
-    char *d_maps, *d_out;
-    int64_t *d_map_off, *d_hw, *d_pt_off;
-    double *d_fac, *d_pts;
-    MP_HIP(hipMalloc(&d_maps, es * (size_t)std::max<int64_t>(cells, 1)));
-    MP_HIP(hipMalloc(&d_out, es * (size_t)std::max<int64_t>(total, 1)));
-    MP_HIP(hipMalloc(&d_map_off, sizeof(int64_t) * (num + 1)));
-    MP_HIP(hipMalloc(&d_hw, sizeof(int64_t) * 2 * num));
-    MP_HIP(hipMalloc(&d_pt_off, sizeof(int64_t) * (num + 1)));
-    MP_HIP(hipMalloc(&d_fac, sizeof(double) * 2 * num));
-    MP_HIP(hipMalloc(&d_pts, sizeof(double) * 2 * (size_t)std::max<int64_t>(total, 1)));
+    DevArray<char> d_maps_a(es * (size_t)std::max<int64_t>(cells, 1)), d_out_a(es * (size_t)std::max<int64_t>(total, 1));
+    DevArray<int64_t> d_map_off_a(num + 1), d_hw_a(2 * (size_t)num), d_pt_off_a(num + 1);
+    DevArray<double> d_fac_a(2 * (size_t)num), d_pts_a(2 * (size_t)std::max<int64_t>(total, 1));
+    char *d_maps = d_maps_a.p, *d_out = d_out_a.p;
+    int64_t *d_map_off = d_map_off_a.p, *d_hw = d_hw_a.p, *d_pt_off = d_pt_off_a.p;
+    double *d_fac = d_fac_a.p, *d_pts = d_pts_a.p;
     MP_HIP(hipMemcpyAsync(d_maps, maps, es * (size_t)cells, hipMemcpyHostToDevice, s));
     MP_HIP(hipMemcpyAsync(d_map_off, map_off.data(), sizeof(int64_t) * (num + 1), hipMemcpyHostToDevice, s));
     MP_HIP(hipMemcpyAsync(d_hw, hw.data(), sizeof(int64_t) * 2 * num, hipMemcpyHostToDevice, s));
@@ -1985,9 +1958,6 @@ void get_depths_batch(int dtype, int32_t num, const void *maps, const int64_t *d
     MP_HIP(launch_get_depths(s, dtype, d_maps, d_map_off, d_hw, d_fac, d_pt_off, num, total, d_pts, d_out));
     if (total > 0) MP_HIP(hipMemcpyAsync(out, d_out, es * (size_t)total, hipMemcpyDeviceToHost, s));
     MP_HIP(hipStreamSynchronize(s));
-    for (void *p : {(void *)d_maps, (void *)d_out, (void *)d_map_off, (void *)d_hw, (void *)d_pt_off, (void *)d_fac,
-                    (void *)d_pts})
-        hipFree(p);
 }
 
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device) {
@@ -1997,16 +1967,12 @@ void scale_and_pose_direct(const double *X, const double *Y, const double *W, in
     std::memcpy(in.data(), X, sizeof(double) * 3 * n);
     std::memcpy(in.data() + 3 * n, Y, sizeof(double) * 3 * n);
     std::memcpy(in.data() + 6 * n, W, sizeof(double) * n);
-    double *d_in;
-    Model *d_out;
-    MP_HIP(hipMalloc(&d_in, sizeof(double) * in.size()));
-    MP_HIP(hipMalloc(&d_out, sizeof(Model)));
-    MP_HIP(hipMemcpyAsync(d_in, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, C.stream));
-    MP_HIP(launch_scale_and_pose(C.stream, d_in, n, d_out));
-    MP_HIP(hipMemcpyAsync(out, d_out, sizeof(Model), hipMemcpyDeviceToHost, C.stream));
+    DevArray<double> d_in(in.size());
+    DevArray<Model> d_out(1);
+    MP_HIP(hipMemcpyAsync(d_in.p, in.data(), sizeof(double) * in.size(), hipMemcpyHostToDevice, C.stream));
+    MP_HIP(launch_scale_and_pose(C.stream, d_in.p, n, d_out.p));
+    MP_HIP(hipMemcpyAsync(out, d_out.p, sizeof(Model), hipMemcpyDeviceToHost, C.stream));
     MP_HIP(hipStreamSynchronize(C.stream));
-    hipFree(d_in);
-    hipFree(d_out);
 }
 
 int device_count() {

@@ -66,6 +66,13 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
 void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
                      int nm, double *scores, double *errors);
 
+// score_batch over explicit models (mp_debug_score_batch; test hook).  models: nb x
+// max_models(variant) (problem units), counts[b] of them used per iteration.  flags: 1
+// exact early exit against `best`, 2 record skip.  res_slot keeps kSlotAmbiguous.
+void debug_score_batch(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nb,
+                       const int *counts, const Model *models, double best, int flags, double *res_best,
+                       int *res_slot, Model *rec_models, double *tie_out, int device);
+
 // Batched device LM (mp_lm_refine_batch): problem j refines models[j] (problem units)
 // over the residual blocks idx[offsets[3j] .. offsets[3j+1]) (reproj 0->1),
 // [offsets[3j+1] .. offsets[3j+2]) (1->0), [offsets[3j+2] .. offsets[3j+3]) (Sampson),
@@ -89,8 +96,8 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
 // root stage of the calibrated 5-point (variant 0) or shared-focal 6-point (variant 1)
 // solver over ns samples of K = 5 / 6 normalized image points each (pts*: ns x K x 2);
 // candidates into cand (ns x 96), counts into ncand
-void debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
-                    int *ncand, int device);
+void debug_pt_roots(int variant, int64_t ns, const double *pts0, const double *pts1, double *cand, int *ncand,
+                    int device);
 
 // estimate_scale_and_pose (src/solver.cpp:5-33) on the device; X, Y point-major n x 3
 void scale_and_pose_direct(const double *X, const double *Y, const double *W, int64_t n, Model *out, int device);
@@ -132,6 +139,7 @@ struct KernelProfile {
     uint64_t model_trips_full = 0; // ... and without the early exit (models x trips)
     uint64_t accepted = 0;         // hypotheses of the iterations the estimator consumed
     uint64_t scored = 0;           // hypotheses whose score_batch sweep ran (not record-skipped)
+    uint64_t tie_checks = 0;       // iterations whose new-best decision needed reference-order re-scoring
 };
 constexpr size_t kBigLM = 1024;
 void profile_enable(bool on);

@@ -75,8 +75,10 @@ struct PairData {
 // record, so a batch's results come back in one copy.
 struct IterResult {
     double best;
-    int slot, count;
+    int slot, count; // slot | kSlotAmbiguous: another model within the tie margin (score_batch)
 };
+constexpr int kSlotAmbiguous = 1 << 16;
+constexpr int kSlotMask = kSlotAmbiguous - 1;
 
 // One least-squares problem of the batched device LM (kernels/lm_device.h): residual
 // blocks idx[off0 .. off0+n0) (reprojection 0->1), idx[off1 ..) (1->0), idx[off2 ..)

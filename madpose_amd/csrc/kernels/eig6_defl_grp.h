@@ -24,10 +24,14 @@
 // hess = true: the 15 x 15 Hessenberg block row-major in pen[0, 225), pen[225] = 1
 // (0: M0 singular, no roots).
 #pragma once
-#include "eig6_grp.h"
+#include "eig6.h"
 
 namespace mp {
 namespace {
+
+// value of v at lane `src` (0..15) of the caller's group (src group-uniform)
+__device__ inline double e6g_at(double v, int src) { return __shfl(v, (int)(threadIdx.x & ~15u) + src, 64); }
+
 
 // all-reduce sum over the 16-lane group (identical in every lane: each step adds a
 // pair of partial sums, and IEEE addition commutes)

@@ -31,36 +31,30 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                            int maxm);
 // scoring sweep: one workgroup per iteration, every model of the iteration scored
 // over all correspondences; per-iteration argmin (first minimum wins) into res[b].
-// best: the best minimal-model score before the batch (DBL_MAX: none yet); a model
-// whose partial MSAC sum exceeds it cannot win and is dropped early (exact early
-// exit, kernels.hip ScoreBound), reporting DBL_MAX.  work (nullable): per iteration
-// the (model, 256-correspondence trip) pairs evaluated.  rec (nullable): the record
-// word of a batch that is cut at its first new best (kernels.hip ScoreBound), with
-// epoch_hi = ~epoch, a value unique to the batch.  rec_out (nullable, device-mapped
-// host memory, nb Models): iterations whose best beats `best` write that model (from
-// models, nb x maxm) to rec_out[b].
+// best: the best minimal-model score before the batch (DBL_MAX: none yet), tie: the
+// absolute margin between this kernel's sums and the reference-order sums (engine.cpp
+// tie_margin); a model whose partial MSAC sum exceeds best + tie cannot win and is
+// dropped early (exact early exit, kernels.hip ScoreBound; only with non-negative
+// weights), reporting DBL_MAX.  An iteration whose second-best model is within tie of
+// its best reports slot | kSlotAmbiguous.  work (nullable): per iteration the (model,
+// 256-correspondence trip) pairs evaluated.  rec (nullable): the record word of a
+// batch that is cut at its first new best (kernels.hip ScoreBound), with epoch_hi =
+// ~epoch, a value unique to the batch; published below best - tie.  rec_out (nullable,
+// device-mapped host memory, nb Models): iterations whose best is below best + tie
+// write that model (from models, nb x maxm) to rec_out[b].
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
-                              int *work, unsigned long long *rec = nullptr, unsigned epoch_hi = 0,
+                              double tie, int *work, unsigned long long *rec = nullptr, unsigned epoch_hi = 0,
                               const Model *models = nullptr, Model *rec_out = nullptr);
 // single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);
-// point-solver root stage alone, C.variant kCal (5pt) or kSF (6pt); impl 0: lane
-// per sample, 1: 16-lane groups, (6pt) 2: DFT nodes over a wave, 3: deflated
-// eigenproblem (the estimator default, eig6.h).  cand: kPtCandStride doubles per sample (cal: 9 per
-// essential matrix; sf: null-space basis N (27), then the positive roots u)
+// the estimator's point-solver root stage alone, C.variant kCal (5pt, 16-lane groups)
+// or kSF (6pt, deflated eigenproblem, eig6.h; pen: kPtPenStride doubles per sample).
+// cand: kPtCandStride doubles per sample (cal: 9 per essential matrix; sf: null-space
+// basis N (27), then the positive roots u)
 hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                           const int *samples, double *cand, int *ncand, int impl, double *pen = nullptr);
-// the single-model sweep writing straight to host-mapped memory: out[0, 3n) the errors,
-// out[3n + W b + w] the partial score of wave w of workgroup b (W =
-// sweep_waves_per_block()), flags[b] = seq (system scope) once workgroup b is done,
-// for b < sweep_blocks(n); the score is the sum over workgroups in order of each
-// workgroup's wave partials summed in wave order
-int sweep_blocks(int64_t n);
-int sweep_waves_per_block();
-hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
-                            int *flags, int seq);
+                           const int *samples, double *cand, int *ncand, double *pen = nullptr);
 // scores of many explicit models (one workgroup per model) -- used by mp_score_models
 hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
                                double *scores);
@@ -73,9 +67,6 @@ hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model 
 // sample, ncand: root count); in: the 6 + 6 normalized 2-D points
 hipError_t launch_point_direct_6pt(hipStream_t s, const double *in, const double *cand, const int *ncand,
                                    Model *poses, int *nposes);
-// MADPOSE_PT6_DFT=1: the shared-focal root stage by DFT + Sturm (A/B) instead of the
-// deflated eigenproblem
-bool pt6_dft();
 
 // batched device LM: one workgroup per job; out[j] the refined model, status[j] 1
 // refined, 0 no residuals, 2 infeasible constant block (unchanged)

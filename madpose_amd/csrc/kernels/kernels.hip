@@ -13,8 +13,8 @@
 //                     through the scalar cache; MSAC sums reduced in-wave (DPP shuffles)
 //                     and across the 4 waves in LDS in a fixed order (deterministic);
 //                     the workgroup also performs GetBestEstimatedModelId's argmin.
-//  sweep_host<V>      LO sweep: one model, all points, errors + partial scores straight
-//                     to pinned host memory, one completion flag per workgroup
+//  sweep<V>           one model, all points (the C ABI's explicit sweeps; LO sweeps
+//                     run on the host, host/lo_sweep.h)
 #include <cfloat>
 #include <cstdlib>
 #include <cstring>
@@ -23,10 +23,8 @@
 #include "../include/mp_md_alt.h"
 #include "../include/mp_score.h"
 #include "group_5pt.h"
-#include "group_6pt.h"
 #include "group_tail.h"
 #include "eig6.h"
-#include "eig6_grp.h"
 #include "eig6_defl_grp.h"
 #include "lm_device.h"
 #include "kernels.h"
@@ -332,146 +330,25 @@ template <> struct PtTraits<kTF> {
     static constexpr int kRoots = 3, kPosesPerRoot = 1, K = 7;
 };
 
-// calibrated bearings / 2-D points of a point sample (src/hybrid_pose_estimator.cpp:121-133)
-__device__ inline void load_cal_sample(const PairData &D, const PairConst &C, const int *s, double (&b1)[5][3],
-                                       double (&b2)[5][3], double (&p0)[5][2], double (&p1)[5][2], double (&dd0)[5],
-                                       double (&dd1)[5]) {
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const int i = s[j];
-        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
-        double a[3], c[3];
-        matvec3(C.K0i, xa, a);
-        matvec3(C.K1i, xb, c);
-        const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            b1[j][q] = a[q] * na;
-            b2[j][q] = c[q] * nc;
-        }
-        p0[j][0] = a[0];
-        p0[j][1] = a[1];
-        p1[j][0] = c[0];
-        p1[j][1] = c[1];
-        dd0[j] = D.d0[i];
-        dd1[j] = D.d1[i];
-    }
-}
-
-template <int V>
-__global__ void __launch_bounds__(64) pt_roots_kernel(PairData D, PairConst C, const int *list, int nlist,
-                                                      const int *samples, double *cand, int *ncand) {
+// two-focal root stage, one lane per sample: the 7-point fundamental matrices
+// (PoseLib relpose_7pt: cubic by multilinear expansion, Sturm roots)
+__global__ void __launch_bounds__(64) pt_roots7_kernel(PairData D, const int *list, int nlist, const int *samples,
+                                                       double *cand, int *ncand) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= nlist) return;
     const int *s = samples + (size_t)list[idx] * kSampleStride;
     double *out = cand + (size_t)idx * kCandStride;
-    int n = 0;
-    if (V == kCal) {
-        double b1[5][3], b2[5][3], p0[5][2], p1[5][2], dd0[5], dd1[5];
-        load_cal_sample(D, C, s, b1, b2, p0, p1, dd0, dd1);
-        FivePtSys S;
-        if (fivept_system(b1, b2, S)) {
-            double roots[10];
-            const int nr = sturm_real_roots<10>(S.d10, roots);
-            for (int r = 0; r < nr; ++r) {
-                double E[9];
-                if (!fivept_E_for_root(S, roots[r], E)) continue;
+    double b0[7][3], b1[7][3], p0[7][2], p1[7][2], dd0[7], dd1[7];
+    load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
+    double F[3][9];
+    const int n = relpose_7pt_F(b0, b1, F);
+    static_for<3>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if (k < n)
 #pragma unroll
-                for (int e = 0; e < 9; ++e) out[9 * n + e] = E[e];
-                ++n;
-            }
-        }
-    } else if (V == kSF) {
-        double b0[6][3], b1[6][3], p0[6][2], p1[6][2], dd0[6], dd1[6];
-        load_uncal_sample<6>(D, s, b0, b1, p0, p1, dd0, dd1);
-        double Q[6][9], N[3][9];
-        epipolar_rows<6>(b0, b1, Q);
-        nullspace_kx9<6>(Q, N);
-        double M[3][10][10];
-        sixpt_matrices(N, M);
-        double roots[15];
-        n = sixpt_roots(M, roots);
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int e = 0; e < 9; ++e) out[9 * a + e] = N[a][e];
-        for (int k = 0; k < n; ++k) out[27 + k] = roots[k];
-    } else {
-        double b0[7][3], b1[7][3], p0[7][2], p1[7][2], dd0[7], dd1[7];
-        load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
-        double F[3][9];
-        n = relpose_7pt_F(b0, b1, F);
-        static_for<3>([&](auto K) {
-            constexpr int k = decltype(K)::value;
-            if (k < n)
-#pragma unroll
-                for (int e = 0; e < 9; ++e) out[9 * k + e] = F[k][e];
-        });
-    }
+            for (int e = 0; e < 9; ++e) out[9 * k + e] = F[k][e];
+    });
     ncand[idx] = n;
-}
-
-template <int V>
-__global__ void __launch_bounds__(64) pt_tail_kernel(PairData D, PairConst C, const int *list, int nlist,
-                                                     const int *samples, const double *cand, const int *ncand,
-                                                     Model *slots, int *valid) {
-    using T = PtTraits<V>;
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int k = gid / nlist, idx = gid - k * nlist;
-    if (k >= T::kRoots || k >= ncand[idx]) return;
-    const int *s = samples + (size_t)list[idx] * kSampleStride;
-    const double *cd = cand + (size_t)idx * kCandStride;
-    Model *sl = slots + (size_t)idx * kSlotStride + T::kPosesPerRoot * k;
-    int *vl = valid + (size_t)idx * kSlotStride + T::kPosesPerRoot * k;
-    const bool shift = C.use_shift != 0 && !C.scale_only, mdc = C.min_depth_constraint != 0;
-    if (V == kCal) {
-        // src/hybrid_pose_estimator.cpp:134-182
-        double b1[5][3], b2[5][3], p0[5][2], p1[5][2], dd0[5], dd1[5];
-        load_cal_sample(D, C, s, b1, b2, p0, p1, dd0, dd1);
-        Model poses[2];
-        const int np = motion_from_essential<5>(cd + 9 * k, b1, b2, poses, 0, 2);
-        for (int j = 0; j < 2; ++j) {
-            bool ok = false;
-            if (j < np) {
-                Model m = poses[j];
-                ok = point_model_tail<5>(p0, p1, dd0, dd1, 1.0, 1.0, shift, mdc, C.min_depth, m);
-                if (ok) sl[j] = m;
-            }
-            vl[j] = ok ? 1 : 0;
-        }
-    } else if (V == kSF) {
-        // src/hybrid_pose_shared_focal_estimator.cpp:87-126
-        double b0[6][3], b1[6][3], p0[6][2], p1[6][2], dd0[6], dd1[6];
-        load_uncal_sample<6>(D, s, b0, b1, p0, p1, dd0, dd1);
-        double N[3][9];
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int e = 0; e < 9; ++e) N[a][e] = cd[9 * a + e];
-        double M[3][10][10];
-        sixpt_matrices(N, M);
-        Model poses[2];
-        const int np = sixpt_poses_for_root(M, N, cd[27 + k], b0, b1, poses, 0, 2);
-        for (int j = 0; j < 2; ++j) {
-            bool ok = false;
-            if (j < np) {
-                Model m = poses[j];
-                const double f = m.focal0;
-                ok = point_model_tail<6>(p0, p1, dd0, dd1, f, f, shift, mdc, C.min_depth, m);
-                if (ok) sl[j] = m;
-            }
-            vl[j] = ok ? 1 : 0;
-        }
-    } else {
-        // src/hybrid_pose_two_focal_estimator.cpp:118-181
-        double b0[7][3], b1[7][3], p0[7][2], p1[7][2], dd0[7], dd1[7];
-        load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
-        Model m;
-        twofocal_pose_from_F<7>(cd + 9 * k, p0, p1, m);
-        const bool ok = point_model_tail<7>(p0, p1, dd0, dd1, m.focal0, m.focal1, shift, mdc, C.min_depth, m);
-        if (ok) sl[0] = m;
-        vl[0] = ok ? 1 : 0;
-    }
 }
 
 // Compaction of a point sample's valid tail slots into its model slots, in slot
@@ -546,16 +423,25 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
 // are always scored in full, so the host's walk never reads a skipped one.  The word
 // carries an epoch in its high half (complemented, so a new batch's first record
 // always wins the minimum) and needs no reset between batches.
+//
+// Near ties.  The host decides every new best on reference-order sums
+// (host/lo_sweep.h); this kernel's sums only screen, with a proven margin `tie` (an
+// absolute bound on |device sum - reference-order sum|): a record is published (and
+// the iterations behind it skipped) only when the best is below the pre-batch best by
+// more than the margin (rec_lo), the model is handed to the host whenever it could be a
+// new best (rec_hi), and an iteration whose second-best model is within the margin of
+// its best is flagged (kSlotAmbiguous in its result's slot) for the host to resolve.
 struct ScoreBound {
     double cut;          // +inf: no early exit
     int first, every;    // first check after `first` trips, then every `every` trips
     int *work;           // per iteration: (model, trip) pairs evaluated (profiling)
     unsigned long long *rec; // nullptr: no record skip
     unsigned epoch_hi;       // ~epoch of this batch
-    double best;             // the pre-batch best (exact)
-    // record models (nullable): an iteration whose best beats `best` writes that model
+    double rec_lo, rec_hi;   // pre-batch best -/+ tie
+    double tie;              // the margin
+    // record models (nullable): an iteration whose best is below rec_hi writes that model
     // to rec_out[b] (mapped host memory), so the host reads a new best's model without
-    // a copy round trip (every new best of a batch beats the pre-batch best)
+    // a copy round trip (every new best of a batch is below the pre-batch best)
     const Model *models;
     Model *rec_out;
 };
@@ -673,7 +559,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double bs = DBL_MAX;
+        double bs = DBL_MAX, s2 = DBL_MAX; // best and second-best score
         int bi = 0;
         for (int m = 0; m < nm; ++m) {
             double v = DBL_MAX; // killed: cannot win
@@ -684,16 +570,20 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
             }
             scores[(size_t)b * MAXM + m] = v;
             if (v < bs) { // strict '<': first minimum wins (src/hybrid_ransac.h:258)
+                s2 = bs;
                 bs = v;
                 bi = m;
+            } else if (v < s2) {
+                s2 = v;
             }
         }
-        res[b] = skipped ? IterResult{DBL_MAX, 0, nm} : IterResult{bs, bi, nm};
+        const int amb = (bs < DBL_MAX && s2 - bs <= sb.tie) ? kSlotAmbiguous : 0;
+        res[b] = skipped ? IterResult{DBL_MAX, 0, nm} : IterResult{bs, bi | amb, nm};
         // (a record-skipped iteration reports its trips negated: profiling only)
         if (sb.work) sb.work[b] = skipped ? -work : work;
-        if (sb.rec && !skipped && bs < sb.best)
+        if (sb.rec && !skipped && bs < sb.rec_lo)
             atomicMin(sb.rec, ((unsigned long long)sb.epoch_hi << 32) | (unsigned long long)(unsigned)b);
-        if (sb.rec_out && !skipped && bs < sb.best) {
+        if (sb.rec_out && !skipped && bs < sb.rec_hi) {
             const double *src = (const double *)(sb.models + (size_t)b * MAXM + bi);
             double *dst = (double *)(sb.rec_out + b);
 #pragma unroll
@@ -727,41 +617,6 @@ __global__ void __launch_bounds__(1024) sweep_kernel(PairData D, PairConst C, co
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
         *score = s;
     }
-}
-
-// LO sweep straight into pinned host memory: errors (3 x n) and the per-workgroup
-// partial scores land in host-visible memory, and every workgroup raises its own
-// completion flag (flags[blockIdx.x] = seq, system scope) after a system-scope fence,
-// so the host polls a few words instead of issuing a copy and a stream sync, and no
-// cross-workgroup counter or last-workgroup reduction sits on the latency path
-// (tools/sweep_lat.hip: 13.6 -> 12.1 us round trip at N = 2000).  One correspondence
-// per lane over ceil(n / kSweepBlock) workgroups (the sweep is latency-bound: one
-// evaluation deep instead of n / 1024).  The host sums the partials in workgroup
-// order -- deterministic.
-constexpr int kSweepBlock = 256;
-template <int V>
-__global__ void __launch_bounds__(kSweepBlock) sweep_host_kernel(PairData D, PairConst C, ScoreRec r, double *out,
-                                                                 int *flags, int seq) {
-    double acc = 0.0;
-    const bool gate_md = C.score_type == 1, gate_epi = C.score_type == 2;
-    for (int i = blockIdx.x * kSweepBlock + threadIdx.x; i < C.n; i += gridDim.x * kSweepBlock) {
-        const Corr p = load_corr(C, D, i, V == kCal);
-        double e0, e1, e2;
-        eval_corr<V>(C, r, p, false, e0, e1, e2);
-        out[i] = e0;
-        out[C.n + i] = e1;
-        out[2 * C.n + i] = e2;
-        acc += gate_md ? C.thr[0] * C.w[0] + C.thr[1] * C.w[1] : msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]);
-        acc += gate_epi ? C.thr[2] * C.w[2] : msac(e2, C.thr[2], C.w[2]);
-    }
-    // each wave's partial score goes to host memory beside the error rows, so one
-    // system-scope fence per thread covers both before the workgroup's flag
-    const double v = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) out[3 * C.n + (kSweepBlock / 64) * blockIdx.x + (threadIdx.x >> 6)] = v;
-    __threadfence_system(); // this thread's error rows and partial reach host memory
-    __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <int V>
@@ -867,9 +722,10 @@ __global__ void md_direct_kernel(int variant, int alt, const double *in, double 
 }
 
 // standalone point solvers (test hooks): kind 0 = 5pt on unit bearings (5 + 5 x 3
-// doubles); kind 1 = shared-focal 6pt, kind 2 = two-focal 7pt + Bougnoux +
-// recoverPose, both on normalized 2-D points (K + K x 2 doubles) turned into
-// bearings exactly as the estimator does.  Models are returned before the depth fit.
+// doubles); kind 2 = two-focal 7pt + Bougnoux + recoverPose on normalized 2-D points
+// (K + K x 2 doubles) turned into bearings exactly as the estimator does (the
+// shared-focal 6pt runs the estimator's staged root stage, engine.cpp
+// solve_point_direct).  Models are returned before the depth fit.
 __global__ void point_direct_kernel(int kind, const double *in, Model *poses, int *nposes) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     if (kind == 0) {
@@ -880,17 +736,6 @@ __global__ void point_direct_kernel(int kind, const double *in, Model *poses, in
                 b2[j][c] = in[15 + 3 * j + c];
             }
         *nposes = relpose_5pt(b1, b2, poses, kMaxModelsCal);
-    } else if (kind == 1) {
-        double b0[6][3], b1[6][3];
-        for (int j = 0; j < 6; ++j) {
-            const double a[3] = {in[2 * j], in[2 * j + 1], 1.0}, c[3] = {in[12 + 2 * j], in[12 + 2 * j + 1], 1.0};
-            const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
-            for (int q = 0; q < 3; ++q) {
-                b0[j][q] = a[q] * na;
-                b1[j][q] = c[q] * nc;
-            }
-        }
-        *nposes = relpose_6pt_sf(b0, b1, poses, kMaxModelsSF);
     } else {
         double b0[7][3], b1[7][3], p0[7][2], p1[7][2];
         for (int j = 0; j < 7; ++j) {
@@ -1006,10 +851,9 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
     });
 }
 
-// the shared-focal root stage by the deflated eigenproblem: the pencil, its
-// deflation + balanced Hessenberg form (one sample per wave), then the lockstep QR
-// (one sample per lane, eig6.h / eig15_gen.h); MADPOSE_PT6_EIG=wave: hqr with one
-// sample per wave instead (A/B)
+// the shared-focal root stage by the deflated eigenproblem: the pencil (16-lane groups,
+// eig6.h), its deflation + balance + Hessenberg form (16-lane groups, eig6_defl_grp.h),
+// then the lockstep Francis QR (one sample per lane, eig6.h / eig15_gen.h)
 // samples per wave of the lockstep QR: about one wave per SIMD (1024 on MI355X;
 // MADPOSE_EIG_WAVES overrides, MADPOSE_EIG_WAVES=16 packs 64 samples per wave at 1024)
 int eig_spw(int nlist) {
@@ -1022,107 +866,40 @@ int eig_spw(int nlist) {
 
 static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int nlist, const int *samples,
                           double *cand, int *ncand, double *pen) {
-    static const bool wave = [] {
-        const char *e = std::getenv("MADPOSE_PT6_EIG");
-        return e && e[0] == 'w';
-    }();
     pt_pencil6_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, list, nlist, samples, cand, kCandStride,
                                                                          pen);
-    if (wave) {
-        pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, false);
-        pt_eig6_kernel<<<nlist, 64, 0, s>>>(pen, cand, ncand, kCandStride);
-    } else {
-        // deflation + balance + Hessenberg on 16-lane groups (eig6_defl_grp.h);
-        // MADPOSE_DEFL_WAVE=1: one sample per wave (pt_defl6_kernel, A/B)
-        static const bool defl_wave = [] {
-            const char *e = std::getenv("MADPOSE_DEFL_WAVE");
-            return e && e[0] == '1';
-        }();
-        if (defl_wave)
-            pt_defl6_kernel<<<nlist, 64, 0, s>>>(pen, true);
-        else
-            pt_defl6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist);
-        // MADPOSE_EIG_GRP_MAX=n: the 16-lane group QR (eig6_grp.h, bit-identical
-        // eigenvalues) for batches of up to n samples.  Off by default: measured no faster
-        // than one sample per lane even at 512 samples (293 vs 282-368 us), 1.5x slower
-        // at 16384 (613 vs 388 us), profiles/r03/s4
-        static const int grp_max = [] {
-            const char *e = std::getenv("MADPOSE_EIG_GRP_MAX");
-            return e ? std::atoi(e) : 0;
-        }();
-        if (nlist <= grp_max) {
-            pt_eig6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist, cand, ncand, kCandStride);
-        } else {
-            const int spw = eig_spw(nlist);
-            pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride);
-        }
-    }
-}
-
-bool pt6_dft() {
-    static const bool v = [] {
-        const char *e = std::getenv("MADPOSE_PT6_DFT");
-        return e && e[0] == '1';
-    }();
-    return v;
+    pt_defl6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist);
+    const int spw = eig_spw(nlist);
+    pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride);
 }
 
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
                            int maxm) {
     if (nlist <= 0) return hipSuccess;
-    const int grid = (nlist + 63) / 64;
     return by_variant(C.variant, [&](auto V) {
         constexpr int v = decltype(V)::value;
-        // calibrated / shared focal: one 16-lane group per sample (group_5pt.h,
-        // group_6pt.h); MADPOSE_PT5_LANE=1 / MADPOSE_PT6_LANE=1 select the
-        // one-lane-per-sample kernels (A/B measurements)
-        static const bool lane5 = std::getenv("MADPOSE_PT5_LANE") != nullptr;
-        static const bool lane6 = std::getenv("MADPOSE_PT6_LANE") != nullptr;
-        // MADPOSE_PT6_WAVE=1: one sample per wave, DFT nodes over the four groups
-        // (pt_roots6_wave_kernel, A/B: 399 vs 291 us per launch for the group kernel at
-        // the shared-focal batch sizes -- four times the waves, throughput-bound)
-        static const bool wave6 = std::getenv("MADPOSE_PT6_WAVE") != nullptr;
-        // shared focal default: the deflated eigenproblem (eig6.h); MADPOSE_PT6_DFT=1
-        // keeps the DFT + Sturm kernels above (A/B; they lose roots)
-        static const bool dft6 = pt6_dft();
-        if (v == kSF && !dft6)
+        // root stage: calibrated 5pt on 16-lane groups (group_5pt.h), shared-focal 6pt by
+        // the deflated eigenproblem, two-focal 7pt one lane per sample
+        if (v == kSF)
             launch_sf_eig(s, D, list, nlist, samples, W.cand, W.ncand, W.pen);
-        else if (v == kCal && !lane5)
+        else if (v == kCal)
             pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
                                                                           kCandStride);
-        else if (v == kSF && !lane6 && wave6)
-            pt_roots6_wave_kernel<<<nlist, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand, kCandStride);
-        else if (v == kSF && !lane6)
-            pt_roots6_group_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, C, list, nlist, samples,
-                                                                                      W.cand, W.ncand, kCandStride);
         else
-            pt_roots_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand);
-        // point-solver tails on lane groups per (root, sample) (group_tail.h: 8 lanes
-        // for cal / tf, 16 for sf); MADPOSE_TAIL_LANE=1 selects the one-lane kernels
-        static const bool lane_tail = std::getenv("MADPOSE_TAIL_LANE") != nullptr;
+            pt_roots7_kernel<<<(nlist + 63) / 64, 64, 0, s>>>(D, list, nlist, samples, W.cand, W.ncand);
+        // tails on lane groups per (root, sample) (group_tail.h: 8 lanes for cal / tf, 16
+        // for sf), root-major so that waves of high root indices are empty and retire
         const long lanes = (long)nlist * PtTraits<v>::kRoots;
         const int tgrid = (int)((lanes * kTail + 63) / 64);
-        // two-focal: 8 lanes per (root, sample); MADPOSE_TAIL7_LANES=32 runs the four
-        // recoverPose candidates on four subgroups (measured slower: DESIGN.md §8)
-        static const int tail7 = [] {
-            const char *e = std::getenv("MADPOSE_TAIL7_LANES");
-            return (e && e[0] == '3') ? 32 : 8;
-        }();
-        if (v == kTF && !lane_tail && tail7 == 32)
-            pt_tail7_group_kernel<32><<<(int)((lanes * 32 + 63) / 64), 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand,
-                                                                                   samples, W.slots, W.valid);
-        else if (v == kTF && !lane_tail)
+        if (v == kTF)
             pt_tail7_group_kernel<8><<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots,
                                                           W.valid);
-        else if (v == kCal && !lane_tail)
+        else if (v == kCal)
             pt_tail5_group_kernel<<<tgrid, 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand, samples, W.slots, W.valid);
-        else if (v == kSF && !lane_tail)
+        else
             pt_tail6_group_kernel<<<(int)((lanes * kGrp + 63) / 64), 64, 0, s>>>(D, C, list, nlist, W.cand, W.ncand,
                                                                                 samples, W.slots, W.valid);
-        else
-            pt_tail_kernel<v><<<(int)((lanes + 63) / 64), 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,
-                                                                      W.slots, W.valid);
         constexpr int kCompactG = PtTraits<v>::kPosesPerRoot * PtTraits<v>::kRoots <= 4 ? 4 : 32;
         pt_compact_kernel<v><<<(int)(((size_t)nlist * kCompactG + 63) / 64), 64, 0, s>>>(
             C, list, nlist, W.ncand, W.slots, W.valid, models, recs, counts, maxm);
@@ -1132,8 +909,9 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
 
 // Early-exit schedule (MADPOSE_SCORE_EXIT=0 turns the exit off; MADPOSE_SCORE_CHECK
 // "first,every" in trips of 256 correspondences overrides the schedule).
-static ScoreBound score_bound(double best, int n, int *work, unsigned long long *rec, unsigned epoch_hi,
-                              const Model *models, Model *rec_out) {
+static ScoreBound score_bound(const PairConst &C, double best, double tie, int *work, unsigned long long *rec,
+                              unsigned epoch_hi, const Model *models, Model *rec_out) {
+    const int n = C.n;
     static const int mode = [] {
         const char *e = std::getenv("MADPOSE_SCORE_EXIT");
         return (e && e[0] == '0') ? 0 : 1;
@@ -1148,8 +926,13 @@ static ScoreBound score_bound(double best, int n, int *work, unsigned long long 
                                      return c ? std::max(1, std::atoi(c + 1)) : 1;
                                  }()};
     ScoreBound sb;
-    const bool on = mode != 0 && best < DBL_MAX && best >= 0.0;
-    sb.cut = on ? best * (1.0 + 1e-12) : __builtin_inf();
+    // the exit and the record skip rest on every MSAC term being >= 0 (a partial sum is
+    // then a lower bound of the total): errors are squares or DBL_MAX, thresholds are
+    // positive (validate()), so it takes non-negative weights; the reference accepts any
+    // weights, and with a negative one every iteration is scored in full
+    const bool nonneg = C.w[0] >= 0.0 && C.w[1] >= 0.0 && C.w[2] >= 0.0;
+    const bool on = mode != 0 && best < DBL_MAX && nonneg;
+    sb.cut = on ? best + tie : __builtin_inf();
     const int ntrip = (n + kBlock - 1) / kBlock;
     // default: a check every quarter of the trips, at most every two trips (512
     // correspondences; each check costs a wave reduction per live model and a barrier).
@@ -1165,9 +948,11 @@ static ScoreBound score_bound(double best, int n, int *work, unsigned long long 
         const char *e = std::getenv("MADPOSE_RECORD_SKIP");
         return !(e && e[0] == '0');
     }();
-    sb.rec = skip ? rec : nullptr;
+    sb.rec = (skip && on) ? rec : nullptr;
     sb.epoch_hi = epoch_hi;
-    sb.best = best;
+    sb.rec_lo = best < DBL_MAX ? best - tie : DBL_MAX;
+    sb.rec_hi = best < DBL_MAX ? best + tie : DBL_MAX;
+    sb.tie = tie;
     sb.models = models;
     sb.rec_out = rec_out;
     return sb;
@@ -1175,12 +960,12 @@ static ScoreBound score_bound(double best, int n, int *work, unsigned long long 
 
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
-                              int *work, unsigned long long *rec, unsigned epoch_hi, const Model *models,
+                              double tie, int *work, unsigned long long *rec, unsigned epoch_hi, const Model *models,
                               Model *rec_out) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
     const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
-    const ScoreBound sb = score_bound(best, C.n, work, rec, epoch_hi, models, rec_out);
+    const ScoreBound sb = score_bound(C, best, tie, work, rec, epoch_hi, models, rec_out);
     const bool exit = sb.cut < __builtin_inf();
     auto go = [&](auto V, auto M, auto F) {
         constexpr int kV = decltype(V)::value, kM = decltype(M)::value;
@@ -1212,40 +997,16 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
 }
 
 hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
-                           const int *samples, double *cand, int *ncand, int impl, double *pen) {
+                           const int *samples, double *cand, int *ncand, double *pen) {
     if (nlist <= 0) return hipSuccess;
-    const int ggrid = (nlist + kGrpPerWg - 1) / kGrpPerWg, lgrid = (nlist + 63) / 64;
-    if (C.variant == kCal) {
-        if (impl == 1)
-            pt_roots5_group_kernel<<<ggrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
-        else
-            pt_roots_kernel<kCal><<<lgrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
-    } else if (C.variant == kSF) {
-        if (impl == 1)
-            pt_roots6_group_kernel<<<ggrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
-        else if (impl == 2)
-            pt_roots6_wave_kernel<<<nlist, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand, kCandStride);
-        else if (impl == 3 && pen)
-            launch_sf_eig(s, D, list, nlist, samples, cand, ncand, pen);
-        else if (impl == 3)
-            return hipErrorInvalidValue;
-        else
-            pt_roots_kernel<kSF><<<lgrid, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand);
-    } else {
+    if (C.variant == kCal)
+        pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, cand, ncand,
+                                                                      kCandStride);
+    else if (C.variant == kSF && pen)
+        launch_sf_eig(s, D, list, nlist, samples, cand, ncand, pen);
+    else
         return hipErrorInvalidValue;
-    }
     return hipGetLastError();
-}
-
-int sweep_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kSweepBlock - 1) / kSweepBlock); }
-int sweep_waves_per_block() { return kSweepBlock / 64; }
-
-hipError_t launch_sweep_host(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec &rec, double *out,
-                            int *flags, int seq) {
-    return by_variant(C.variant, [&](auto V) {
-        sweep_host_kernel<decltype(V)::value><<<sweep_blocks(C.n), kSweepBlock, 0, s>>>(D, C, rec, out, flags, seq);
-        return hipGetLastError();
-    });
 }
 
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,

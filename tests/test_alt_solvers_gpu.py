@@ -75,6 +75,7 @@ def _parity(variant, o, c, p):
     om, ost, oinl = oracle.estimate(variant, p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], cam0, cam1,
                                     oracle_opts(o), oracle_cfg(c))
     assert st.num_iterations_total == ost.num_iterations_total
+    assert st.num_hypotheses == ost.num_hypotheses, (st.num_hypotheses, ost.num_hypotheses)
     assert st.num_iterations_per_solver == list(ost.num_iterations_per_solver)
     assert st.number_lo_iterations == ost.number_lo_iterations
     for t in range(3):

@@ -97,13 +97,14 @@ def test_scannet_summary_and_gathered_errors():
     assert [res["pose_auc"][k] for k in ("5", "10", "20")] == ref
 
 
-def _run_bench(args, timeout=600):
+def _run_bench(args, timeout=600, env_extra=None):
     import json
     import subprocess
 
     env = dict(os.environ)
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "MADPOSE_BENCH_DIST"):
         env.pop(k, None)
+    env.update(env_extra or {})
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -177,3 +178,15 @@ def test_single_rank_in_flight_leg_and_records():
     assert res["results"]["records"] == 4
     # the stub returns R = I, t = (1, 0, 0): its pose errors come from compute_pose_error
     assert res["results"]["median_pose_err_deg"] >= 0.0
+
+
+def test_forced_one_rank_group_gathers_through_the_collective():
+    """MADPOSE_BENCH_DIST=1 (the one-GPU rehearsal of the RCCL gather): one rank still
+    creates a process group (gloo here) and its counters and records go through
+    dist.all_gather."""
+    res = _run_bench(["--steps", "2", "--warmup", "1", "--cpu-budget", "0", "--in-flight", "1", "--engine-module",
+                      "tests.bench_stub_engine"], env_extra={"MADPOSE_BENCH_DIST": "1"})
+    d = res["dist"]
+    assert d["backend"] == "gloo" and d["world_size"] == 1
+    assert len(d["all_gathers"]) == 2
+    assert res["results"]["records"] == 2

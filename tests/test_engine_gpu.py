@@ -215,6 +215,9 @@ def _run_both(p, o, c, variant=0):
 
 def _assert_parity(pose, st, om, ost, oinl):
     assert st.num_iterations_total == ost.num_iterations_total
+    # the headline's unit: models scored by the minimal-sample iterations the estimator
+    # consumed (src/hybrid_ransac.h:120-123 GetBestEstimatedModelId over num_models)
+    assert st.num_hypotheses == ost.num_hypotheses, (st.num_hypotheses, ost.num_hypotheses)
     assert st.num_iterations_per_solver == list(ost.num_iterations_per_solver)
     assert st.number_lo_iterations == ost.number_lo_iterations
     assert st.best_solver_type == ost.best_solver_type
@@ -394,37 +397,27 @@ def _five_point_samples(rng, ns, noise_free):
     return p0, p1, Es
 
 
-def test_group_5pt_kernel_matches_lane_kernel():
-    """The 16-lane-group 5-point root kernel (the estimator's default) against the
-    one-lane-per-sample kernel on the same samples: the same number of essential
-    matrices per sample and the same matrices (they perform the same operations per
-    value up to FMA contraction, so only ill-conditioned samples may drift), and on
-    noise-free samples both find the ground-truth essential matrix."""
+def test_group_5pt_root_stage_finds_ground_truth():
+    """The estimator's 5-point root stage (one 16-lane group per sample): on noise-free
+    samples the ground-truth essential matrix is among its candidates (99.5 % at 1e-6;
+    the rest are ill-conditioned samples).  (The one-lane-per-sample kernel it was once
+    compared with left the library in round 4; test_5pt_matches_oracle_and_ground_truth
+    checks the solver against the oracle.)"""
     rng = np.random.default_rng(5)
     p0, p1, Es = _five_point_samples(rng, 2000, noise_free=True)
-    for impl in (0, 1):
-        cand, ncand = _pt5_roots(impl, p0, p1)
-        found = 0
-        for s in range(len(Es)):
-            best = 1.0
-            for k in range(ncand[s]):
-                E = cand[s, 9 * k: 9 * k + 9].reshape(3, 3)
-                E = E / np.linalg.norm(E)
-                best = min(best, np.abs(E - Es[s]).max(), np.abs(E + Es[s]).max())
-            found += best < 1e-6
-        assert found >= 0.995 * len(Es), (impl, found)
-    # noisy samples: compare the two kernels directly
-    p0, p1, _ = _five_point_samples(rng, 4000, noise_free=False)
-    c0, n0 = _pt5_roots(0, p0, p1)
-    c1, n1 = _pt5_roots(1, p0, p1)
-    same = n0 == n1
-    assert same.mean() >= 0.995, same.mean()
-    close = 0
-    for s in np.flatnonzero(same):
-        a, b = c0[s, : 9 * n0[s]], c1[s, : 9 * n0[s]]
-        close += np.abs(a - b).max(initial=0.0) <= 1e-6
-    assert close >= 0.98 * same.sum(), (close, same.sum())
-
+    cand, ncand = _pt5_roots(1, p0, p1)
+    found = 0
+    for s in range(len(Es)):
+        best = 1.0
+        for k in range(ncand[s]):
+            E = cand[s, 9 * k: 9 * k + 9].reshape(3, 3)
+            E = E / np.linalg.norm(E)
+            best = min(best, np.abs(E - Es[s]).max(), np.abs(E + Es[s]).max())
+        found += best < 1e-6
+    assert found >= 0.995 * len(Es), found
+    # impl values other than the estimator's stage are refused
+    with pytest.raises(ValueError):
+        _pt5_roots(0, p0[:4], p1[:4])
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
 def test_parallel_lo_steps_match_serial(monkeypatch, variant):

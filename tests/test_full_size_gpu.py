@@ -37,6 +37,7 @@ def test_full_size_config_parity(name, seed):
     pose, st = fn(*args, o, c)
     om, ost, oinl = oracle.estimate(variant, *args, oracle_opts(o), oracle_cfg(c))
     assert st.num_iterations_total == ost.num_iterations_total == iters
+    assert st.num_hypotheses == ost.num_hypotheses, (st.num_hypotheses, ost.num_hypotheses)  # the headline's unit
     assert st.num_iterations_per_solver == list(ost.num_iterations_per_solver)
     assert st.number_lo_iterations == ost.number_lo_iterations
     assert st.best_solver_type == ost.best_solver_type

@@ -44,6 +44,7 @@ def test_scale_only_estimator_parity(seed, solver):
                                     oracle_opts(o), oracle_cfg(c))
     assert isinstance(pose, madpose.PoseAndScale)
     assert st.num_iterations_total == ost.num_iterations_total
+    assert st.num_hypotheses == ost.num_hypotheses, (st.num_hypotheses, ost.num_hypotheses)
     assert st.num_iterations_per_solver == list(ost.num_iterations_per_solver)
     assert st.number_lo_iterations == ost.number_lo_iterations
     for t in range(3):

@@ -29,6 +29,7 @@ def test_batch_pose_auc_matches_oracle():
         ref, rst, inl = oracle.estimate(1, p["x0"], p["x1"], p["depth0"], p["depth1"], p["min_depth"], p["pp0"],
                                         p["pp1"], oracle_opts(o), oracle_cfg(c))
         assert st.num_iterations_total == rst.num_iterations_total
+        assert st.num_hypotheses == rst.num_hypotheses, (st.num_hypotheses, rst.num_hypotheses)
         assert rot_angle_deg(m.R(), ref["R"]) <= 1e-6
         for t in range(3):
             assert np.array_equal(np.sort(st.inlier_indices[t]), np.sort(inl[t]))

@@ -19,8 +19,8 @@
 // Per value the operations are those of det_pencil10 / pencil_poly15 /
 // sturm_real_roots, so both kernels agree up to FMA contraction.
 #pragma once
-#include "../include/mp_pt67.h"
-#include "group_sturm.h"
+#include "../../madpose_amd/csrc/include/mp_pt67.h"
+#include "../../madpose_amd/csrc/kernels/group_sturm.h"
 
 namespace mp {
 namespace {

@@ -8,6 +8,8 @@
 //   tools/eig6_bench [samples]
 #define MP_EIG6_PROFILE 1
 #include "../madpose_amd/csrc/kernels/kernels.hip"
+#include "ab/group_6pt.h"
+#include "ab/eig6_ab.h"
 
 #include <cstdio>
 #include <random>
