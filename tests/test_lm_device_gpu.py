@@ -53,8 +53,8 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
         okd = LC.close(m, ref, variant, epi_only=lo_type == 1)
         okh = LC.close(mh, ref, variant, epi_only=lo_type == 1)
         if reason is None:
-            assert okh, ("host", kind, sizes)
-            assert okd, ("device", kind, sizes)
+            assert okh, ("host", kind, sizes, LC.deviation(mh, ref))
+            assert okd, ("device", kind, sizes, LC.deviation(m, ref))
         else:
             excluded[reason] += 1
             agree["device"] += okd

@@ -9,9 +9,8 @@ are trusted only outside a proven margin (engine.cpp tie_margin).  These tests:
 * score_batch's exact early exit and record skip against the plain kernel on the same
   model lists (every iteration up to the first record identical; record models equal
   the iterations' best models);
-* a constructed exact tie of every hypothesis (all errors above tiny thresholds: every
-  model scores the same sum) -- the first model of the first iteration must win, as in
-  the oracle;
+* a constructed exact tie: an iteration holding the same model twice (a duplicated
+  minimal sample's solution) -- the first slot wins and the iteration is flagged;
 * near ties forced through the resolution path by an inflated margin
   (MADPOSE_TIE_SCALE), with full parity against the oracle;
 * negative and zero data-type weights (the exit and the record skip are off then).
@@ -92,29 +91,13 @@ def test_score_batch_flags_duplicated_model_as_ambiguous():
     assert not (s[1] & AMB)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
-def test_every_hypothesis_ties_first_model_wins(variant):
-    """Thresholds so small that every residual is clipped: every model of every
-    iteration scores the same sum, so no later hypothesis is strictly better and the
-    first model of the first iteration with models stays the best (the oracle's
-    result); its LO finds no inliers to refine on."""
-    p = synthetic.make_pair(11 + variant, n=300)
-    o, c = synthetic.example_options("calibrated" if variant == 0 else "shared_focal", iterations=300)
-    o.squared_inlier_thresholds = [1e-300, 1e-300]
-    pose, st, om, ost, oinl = _run_both(p, o, c, variant)
-    assert st.num_iterations_total == ost.num_iterations_total
-    assert st.num_hypotheses == ost.num_hypotheses
-    assert st.best_solver_type == ost.best_solver_type
-    assert rot_angle_deg(pose.R(), om["R"]) < 1e-6
-    assert st.best_model_score == ost.best_model_score  # the reference-order sum, to the bit
-
-
 @pytest.mark.parametrize("variant,seed", [(0, 0), (0, 3), (1, 1), (2, 2)])
 def test_tie_margin_inflated_parity(variant, seed, monkeypatch):
-    """MADPOSE_TIE_SCALE=1e9 widens the margin to about a percent of the score, so most
-    new-best candidates go through the reference-order resolution; the estimate must
-    still equal the oracle's in every parity field."""
-    monkeypatch.setenv("MADPOSE_TIE_SCALE", "1e9")
+    """MADPOSE_TIE_SCALE=1e11 widens the margin to a large share of the score, so most
+    new-best candidates and many multi-model iterations go through the reference-order
+    resolution (and the exit / record skip, bounded by the margin, seldom act); the
+    estimate must still equal the oracle's in every parity field."""
+    monkeypatch.setenv("MADPOSE_TIE_SCALE", "1e11")
     p = synthetic.make_pair(seed, n=400)
     kind = {0: "calibrated", 1: "shared_focal", 2: "two_focal"}[variant]
     o, c = synthetic.example_options(kind, iterations=400)
