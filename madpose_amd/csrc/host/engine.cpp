@@ -662,6 +662,9 @@ class Run {
     // resolution path with a large factor).
     double tie_ = 0.0;
     uint64_t tie_checks_ = 0;
+    // MADPOSE_COUNT_DUMP=<file>: one line per walked iteration (iteration, solver type,
+    // model count, the solver's sample) -- a diagnostic (tools/diag_counts.py)
+    FILE *count_dump_ = nullptr;
     PairData D_;
     Stats *S_ = nullptr;
     IterationStream rs_; // sampler + selection/LO streams
@@ -1183,6 +1186,9 @@ class Run {
 
 void Run::run(Model *best, Stats *S) {
     auto t_start = Clock::now();
+    const char *dump_path = std::getenv("MADPOSE_COUNT_DUMP");
+    std::unique_ptr<FILE, int (*)(FILE *)> dump(dump_path ? std::fopen(dump_path, "w") : nullptr, &std::fclose);
+    count_dump_ = dump.get();
     S_ = S;
     *S = Stats();
     S->best_model_score = kMax;
@@ -1343,6 +1349,12 @@ void Run::run(Model *best, Stats *S) {
             S->num_iterations_per_solver[st] += 1;
             const int nm = X_.h_res[j].count;
             S->num_hypotheses += (uint64_t)nm;
+            if (count_dump_) {
+                const int *smp = slot_ptr(g.slot) + 8 * (size_t)j;
+                std::fprintf(count_dump_, "%u %d %d", iter, st, nm);
+                for (int q = 0; q < (st == 0 ? ss_[0][0] : ss_[1][2]); ++q) std::fprintf(count_dump_, " %d", smp[q]);
+                std::fprintf(count_dump_, "\n");
+            }
             bool lo_here = false;
             if (nm > 0) {
                 // The device sums screen; the decision is taken on reference-order sums
@@ -1374,7 +1386,10 @@ void Run::run(Model *best, Stats *S) {
                                                  iter, best_min_score, bl, st, nm);
                         update_best(best_min_score, best_min, st, &S->best_model_score, best, &S->best_solver_type);
                     }
-                    const bool run_lo = iter >= lo_start && best_min_score < kMax;
+                    // the reference enters this block only on a new best or at
+                    // lo_starting_iterations (src/hybrid_ransac.h:123-124); a `maybe` that
+                    // the exact sums reject is no entry
+                    const bool run_lo = (new_best || iter == lo_start) && iter >= lo_start && best_min_score < kMax;
                     if (new_best || run_lo) {
                         if (run_lo) {
                             // rewind both streams to the end of iteration `iter`

@@ -227,6 +227,16 @@ struct Engine {
         std::mt19937 rng;
         rng.seed(o.random_seed);
         const uint32_t lo_start = (uint32_t)o.lo_starting_iterations;
+        // ORACLE_COUNT_DUMP=<file>: one line per iteration (iteration, solver type, model
+        // count, the solver's sample) -- a diagnostic (tools/diag_counts.py)
+        const char *dump_path = std::getenv("ORACLE_COUNT_DUMP");
+        FILE *dump = dump_path ? std::fopen(dump_path, "w") : nullptr;
+        struct Closer {
+            FILE *f;
+            ~Closer() {
+                if (f) std::fclose(f);
+            }
+        } closer{dump};
 
         for (S->num_iterations_total = 0; S->num_iterations_total < max_total; ++S->num_iterations_total) {
             const uint32_t it = S->num_iterations_total;
@@ -254,6 +264,11 @@ struct Engine {
             for (int t = 0; t < 3; ++t) sampler.draw(ss[st][t], &sample[t]);
             const int nm = minimal_solver(P, sample, st, &models);
             S->num_hypotheses += nm;
+            if (dump) {
+                std::fprintf(dump, "%u %d %d", it, st, nm);
+                for (int i : sample[st == 0 ? 0 : 2]) std::fprintf(dump, " %d", i);
+                std::fprintf(dump, "\n");
+            }
             if (nm > 0) {
                 double bl = kDMax;
                 int bid = 0;

@@ -193,6 +193,17 @@ def lm_cost(variant, args, o, c, model, lists, norm_scale=1.0):
     return float(cost)
 
 
+def epi_only_equivalent(m, ref, cost_m, cost_ref):
+    """EPI_ONLY agreement by cost: Ceres stops once a step lowers the cost by less than
+    function_tolerance (1e-6, src/estimator_config.h:27) of it, and along the valley of
+    the unobserved |t| that leaves the rotation free to ~sqrt(1e-6) relative -- measured
+    up to 1.4e-3 deg between the device LM and the oracle (profiles/r04/s4).  Equivalent:
+    both stop within twice that tolerance of each other's cost, rotation within 1e-2 deg
+    and t direction within 1e-3."""
+    rot, tdir = deviation(m, ref)
+    return bool(abs(cost_m - cost_ref) <= 2e-6 * cost_ref and rot < 1e-2 and tdir < 1e-3)
+
+
 def deviation(m, ref):
     """(rotation deg, t-direction max abs) of m from a reference dict, for messages."""
     tn = lambda v: np.asarray(v) / np.linalg.norm(v)

@@ -52,6 +52,15 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
             assert cm <= c0 * (1 + 1e-9) + 1e-12, (who, kind, sizes, cm, c0)
         okd = LC.close(m, ref, variant, epi_only=lo_type == 1)
         okh = LC.close(mh, ref, variant, epi_only=lo_type == 1)
+        if lo_type == 1 and reason is None and not (okd and okh):
+            # EPI_ONLY: agreement by cost within Ceres' function tolerance (lm_cases.py)
+            cref = LC.lm_cost(variant, args, o, c, LC.model_of(ref, variant), lists, norm_scale)
+            for who, mm, ok0 in (("device", m, okd), ("host", mh, okh)):
+                if not ok0:
+                    cm = LC.lm_cost(variant, args, o, c, mm, lists, norm_scale)
+                    ok = LC.epi_only_equivalent(mm, ref, cm, cref)
+                    assert ok, (who, kind, sizes, LC.deviation(mm, ref), cm, cref)
+            okd = okh = True
         if reason is None:
             assert okh, ("host", kind, sizes, LC.deviation(mh, ref))
             assert okd, ("device", kind, sizes, LC.deviation(m, ref))
