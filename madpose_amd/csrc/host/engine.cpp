@@ -493,6 +493,9 @@ LmJob make_lm_job(const Problem &P, const EstimatorConfig &cfg, const int *sizes
 }
 
 Problem make_problem(const PairInput &in, const RansacOptions &o, const EstimatorConfig &cfg) {
+    // no FMA contraction: the normalization scale (and with it every normalized
+    // coordinate the MD solvers see) is the oracle's to the bit (estimator.cpp:88-103)
+#pragma clang fp contract(off)
     Problem P;
     const int n = (int)in.n;
     PairConst &C = P.C;

@@ -479,6 +479,9 @@ MP_HD int md_sols_tf(const double (&x0)[4][3], const double (&y0)[4][3], const d
 template <int K>
 MP_HD bool md_pose_from_sol(const double (&x)[K][3], const double (&y)[K][3], const double *dx, const double *dy,
                             const double *sol, double fx, double fy, Model &m, bool check_positive = true) {
+    // no FMA contraction: the positivity test of d2 = dy a2 + b2 a2 decides whether a
+    // solution becomes a model, and must see the oracle's (md.cpp:400-404) doubles
+#pragma clang fp contract(off)
     double X[K][3], Y[K][3], cx[3] = {0, 0, 0}, cy[3] = {0, 0, 0};
     bool ok = true;
 #pragma unroll

@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "../include/mp_md_alt.h"
+#include "../include/mp_md_exact.h"
 #include "../include/mp_score.h"
 #include "group_5pt.h"
 #include "group_tail.h"
@@ -284,6 +285,55 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kC
         if (keep && pos < maxm) put_model(C, m, b, pos, maxm, models, recs);
         if (r == 0) counts[b] = total < maxm ? total : maxm;
     }
+}
+
+// The shared- and two-focal MD solvers with the oracle's arithmetic (mp_md_exact.h):
+// one sample per lane on the first SPW lanes of a wave, the lane's scratch its column
+// of an LDS block (SPW x NS doubles); accepted models go to their slots in root order,
+// as md_solve_group's.  The per-sample work is a long serial chain with divergent
+// trip counts (hqr iterations, roots), so a wave carries few samples and the launch
+// spreads them over every SIMD.
+template <int V, int SPW>
+__global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                      const int *samples, Model *models, ScoreRec *recs, int *counts,
+                                                      int maxm) {
+    static_assert(V == kSF || V == kTF, "md_exact_kernel: shared / two focal");
+    constexpr int NS = V == kSF ? kMdxScratchSF : kMdxScratchTF;
+    __shared__ double scr[NS * SPW];
+    if (threadIdx.x >= SPW) return;
+    const int idx = blockIdx.x * SPW + threadIdx.x;
+    if (idx >= nlist) return;
+    const int b = list[idx];
+    const int *s = samples + (size_t)b * kSampleStride;
+    double x[4][3], y[4][3], dx[4], dy[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = s[j];
+        x[j][0] = D.x0u[i];
+        x[j][1] = D.x0v[i];
+        x[j][2] = 1.0;
+        y[j][0] = D.x1u[i];
+        y[j][1] = D.x1v[i];
+        y[j][2] = 1.0;
+        dx[j] = D.d0[i];
+        dy[j] = D.d1[i];
+    }
+    int n = 0;
+    auto pose = [&](const double (&sol)[6]) {
+        Model m;
+        m.focal0 = sol[4];
+        m.focal1 = sol[5];
+        if (md_pose_from_sol<4>(x, y, dx, dy, sol, sol[4], sol[5], m) && md_accept(C, m)) {
+            if (n < maxm) put_model(C, m, b, n, maxm, models, recs);
+            ++n;
+        }
+    };
+    const LaneScratch W{scr + threadIdx.x, SPW};
+    if (V == kSF)
+        mdx_sols_sf(W, x, y, dx, dy, pose);
+    else
+        mdx_sols_tf(W, x, y, dx, dy, pose);
+    counts[b] = n < maxm ? n : maxm;
 }
 
 template <int K>
@@ -704,9 +754,17 @@ __global__ void md_direct_kernel(int variant, int alt, const double *in, double 
         dx[j] = in[24 + j];
         dy[j] = in[28 + j];
     }
-    double sols[8][6];
-    const int ns = (variant == kSF) ? md_sols_sf(x, y, dx, dy, sols)
-                                    : md_sols_tf(x, y, dx, dy, *reinterpret_cast<double(*)[4][6]>(&sols[0][0]));
+    double sols[8][6], scr[kMdxScratchSF];
+    int ns = 0;
+    auto keep = [&](const double (&sol)[6]) {
+        for (int c = 0; c < 6; ++c) sols[ns][c] = sol[c];
+        ++ns;
+    };
+    const LaneScratch W{scr, 1};
+    if (variant == kSF)
+        mdx_sols_sf(W, x, y, dx, dy, keep);
+    else
+        mdx_sols_tf(W, x, y, dx, dy, keep);
     const int w = (variant == kSF) ? 5 : 6;
     int np = 0;
     for (int k = 0; k < ns; ++k) {
@@ -836,6 +894,26 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
         // default solvers on 16-lane groups (MADPOSE_MD_LANE: one sample per lane)
         static const bool lane_md = std::getenv("MADPOSE_MD_LANE") != nullptr;
         const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
+        if constexpr (v != kCal) {
+            if (plain) {
+                static const int spw = [] {
+                    const char *e = std::getenv("MADPOSE_MDX_SPW");
+                    return e ? std::atoi(e) : 16;
+                }();
+                if (spw == 64)
+                    md_exact_kernel<v, 64><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+                else if (spw == 8)
+                    md_exact_kernel<v, 8><<<(nlist + 7) / 8, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                         counts, maxm);
+                else if (spw == 4)
+                    md_exact_kernel<v, 4><<<(nlist + 3) / 4, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                         counts, maxm);
+                else
+                    md_exact_kernel<v, 16><<<(nlist + 15) / 16, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                            counts, maxm);
+                return hipGetLastError();
+            }
+        }
         if (plain && !lane_md) {
             md_solve_group_kernel<v><<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, C, list, nlist, samples,
                                                                                      models, recs, counts, maxm);

@@ -1,0 +1,103 @@
+"""The shared-/two-focal (and calibrated) MD solvers of mp_md_exact.h against the oracle,
+bit for bit, on the CPU: the header is compiled for the host by clang with FMA
+available (-march=x86-64-v3) and contraction off by the header's own pragmas, behind
+the C ABI of tests/md_exact_check.cpp.  Equal solution lists (count, order, every
+double) for random samples, for samples whose resultant's roots span several orders
+of magnitude (the class on which the former Sturm isolation lost or invented roots,
+profiles/r04/s6/diag_sf0.log), and for the full-size estimator samples where it did.
+The device build of the same header is checked against the oracle in
+tests/test_md_exact_gpu.py."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from madpose_amd import synthetic
+from tests.helpers import oracle_cfg, oracle_opts
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLANG = "/opt/rocm/llvm/bin/clang++"
+_dp = ctypes.POINTER(ctypes.c_double)
+
+# (case, seed, iteration sample) of the estimator MD samples whose device solutions
+# differed from the oracle's before this solver (profiles/r04/s6/diag_{sf,tf}0.log)
+DIAG = [("sf", 0, [824, 451, 1708, 1394]), ("sf", 0, [414, 799, 267, 1502]), ("sf", 0, [1366, 1645, 1374, 1587]),
+        ("sf", 0, [236, 1756, 1009, 623]), ("sf", 0, [508, 746, 1379, 36]), ("sf", 0, [200, 1495, 1982, 991]),
+        ("sf", 0, [704, 971, 594, 851]), ("tf", 0, [2871, 920, 2581, 2674])]
+
+
+@pytest.fixture(scope="module")
+def mdx(tmp_path_factory):
+    if not os.path.exists(CLANG):
+        pytest.fail(f"{CLANG} missing: the host build of mp_md_exact.h needs ROCm's clang")
+    so = str(tmp_path_factory.mktemp("mdx") / "mdx_check.so")
+    cmd = [CLANG, "-O3", "-std=c++17", "-march=x86-64-v3", "-fPIC", "-shared", "-I",
+           os.path.join(ROOT, "madpose_amd", "csrc", "include"), os.path.join(ROOT, "tests", "md_exact_check.cpp"),
+           "-o", so]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lib = ctypes.CDLL(so)
+    lib.mdx_check_solve.restype = ctypes.c_int
+
+    def solve(v, x, y, dx, dy):
+        a = [np.ascontiguousarray(t, dtype=np.float64) for t in (x, y, dx, dy)]
+        out = np.zeros(48)
+        n = lib.mdx_check_solve(v, *[t.ctypes.data_as(_dp) for t in a], out.ctypes.data_as(_dp))
+        return out[:6 * n].reshape(n, 6)[:, :[4, 5, 6][v]]
+    return solve
+
+
+def _oracle(v, x, y, dx, dy):
+    s = np.asarray(oracle.md_scale_shift(v, x, y, dx, dy), dtype=np.float64)
+    return s.reshape(-1, [4, 5, 6][v])
+
+
+def _check(mdx, v, x, y, dx, dy):
+    a, b = mdx(v, x, y, dx, dy), _oracle(v, x, y, dx, dy)
+    assert a.shape == b.shape and np.array_equal(a, b), (v, a, b)
+    return len(a)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_random_samples_bit_exact(mdx, variant):
+    rng = np.random.default_rng(40 + variant)
+    k = 3 if variant == 0 else 4
+    total = 0
+    for _ in range(3000):
+        x = np.c_[rng.standard_normal((k, 2)), np.ones(k)]
+        y = np.c_[rng.standard_normal((k, 2)), np.ones(k)]
+        total += _check(mdx, variant, x, y, rng.uniform(0.5, 5, k), rng.uniform(0.5, 5, k))
+    assert total > 1000  # solutions were found and compared
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_wide_root_range_bit_exact(mdx, variant):
+    """Depths spread over several orders of magnitude and nearly collinear points: the
+    resultant's roots then span many decades (the Sturm chain's failure class)."""
+    rng = np.random.default_rng(50 + variant)
+    for _ in range(3000):
+        x = np.c_[rng.standard_normal((4, 2)) * 10.0 ** rng.uniform(-3, 1), np.ones(4)]
+        y = np.c_[x[:, :2] + rng.standard_normal((4, 2)) * 10.0 ** rng.uniform(-4, 0), np.ones(4)]
+        dx = 10.0 ** rng.uniform(-2, 3, 4)
+        dy = 10.0 ** rng.uniform(-2, 3, 4)
+        _check(mdx, variant, x, y, dx, dy)
+
+
+def test_estimator_diag_samples_bit_exact(mdx):
+    from tests.test_full_size_gpu import CASES
+    for name, seed, idx in DIAG:
+        variant, kind, cfg, iters = CASES[name]
+        p = synthetic.config_pair(cfg, seed=seed)
+        o, c = synthetic.throughput_options(kind, iterations=iters)
+        cam0, cam1 = p["pp0"], p["pp1"]
+        _, _, ns = oracle.score_models(variant, p["x0"], p["x1"], p["depth0"], p["depth1"], cam0, cam1,
+                                       oracle_opts(o), oracle_cfg(c), [])
+        a0 = (np.asarray(p["x0"], float) - np.asarray(cam0, float).reshape(2)) / ns
+        a1 = (np.asarray(p["x1"], float) - np.asarray(cam1, float).reshape(2)) / ns
+        idx = np.asarray(idx)
+        x = np.c_[a0[idx], np.ones(4)]
+        y = np.c_[a1[idx], np.ones(4)]
+        _check(mdx, variant, x, y, np.asarray(p["depth0"], float)[idx], np.asarray(p["depth1"], float)[idx])
