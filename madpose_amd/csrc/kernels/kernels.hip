@@ -288,20 +288,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kC
 }
 
 // The shared- and two-focal MD solvers with the oracle's arithmetic (mp_md_exact.h):
-// one sample per lane on the first SPW lanes of a wave, the lane's scratch its column
-// of an LDS block (SPW x NS doubles); accepted models go to their slots in root order,
-// as md_solve_group's.  The per-sample work is a long serial chain with divergent
-// trip counts (hqr iterations, roots), so a wave carries few samples and the launch
-// spreads them over every SIMD.
-template <int V, int SPW>
+// one sample per lane, register-resident (only the sorted root list goes to the lane's
+// column of an LDS block); accepted models go to their slots in root order, as
+// md_solve_group's.  The kernel is issue-bound (the predicated, fully unrolled QR), so
+// full waves pay best: 64 / 16 / 8 / 4 samples per wave gave sf 12.9 / 13.4 / 15.0 /
+// 16.3 ms per pair on one box (profiles/r04/mdx/).
+template <int V>
 __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                       const int *samples, Model *models, ScoreRec *recs, int *counts,
                                                       int maxm) {
     static_assert(V == kSF || V == kTF, "md_exact_kernel: shared / two focal");
     constexpr int NS = V == kSF ? kMdxScratchSF : kMdxScratchTF;
-    __shared__ double scr[NS * SPW];
-    if (threadIdx.x >= SPW) return;
-    const int idx = blockIdx.x * SPW + threadIdx.x;
+    __shared__ double scr[NS * 64];
+    const int idx = blockIdx.x * 64 + threadIdx.x;
     if (idx >= nlist) return;
     const int b = list[idx];
     const int *s = samples + (size_t)b * kSampleStride;
@@ -328,7 +327,7 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
             ++n;
         }
     };
-    const LaneScratch W{scr + threadIdx.x, SPW};
+    const LaneScratch W{scr + threadIdx.x, 64};
     if (V == kSF)
         mdx_sols_sf(W, x, y, dx, dy, pose);
     else
@@ -896,21 +895,7 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
         const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
         if constexpr (v != kCal) {
             if (plain) {
-                static const int spw = [] {
-                    const char *e = std::getenv("MADPOSE_MDX_SPW");
-                    return e ? std::atoi(e) : 16;
-                }();
-                if (spw == 64)
-                    md_exact_kernel<v, 64><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
-                else if (spw == 8)
-                    md_exact_kernel<v, 8><<<(nlist + 7) / 8, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
-                                                                         counts, maxm);
-                else if (spw == 4)
-                    md_exact_kernel<v, 4><<<(nlist + 3) / 4, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
-                                                                         counts, maxm);
-                else
-                    md_exact_kernel<v, 16><<<(nlist + 15) / 16, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
-                                                                            counts, maxm);
+                md_exact_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
                 return hipGetLastError();
             }
         }

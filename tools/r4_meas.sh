@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-4 measurement set on the current tree: the GPU suite, smoke(), the default
+# bench line (cal, CPU baselines), sf / tf / ScanNet lines, rocprofv3 kernel statistics
+# of short cal and sf runs.  Output under gpurun_out/$1 (default r4m).
+out=gpurun_out/${1:-r4m}
+mkdir -p "$out"
+export TMPDIR=/tmp
+step() { # seconds log command...
+  local secs=$1 log=$2; shift 2
+  echo "== $log"
+  timeout -k 10 "$secs" "$@" > "$out/$log" 2>&1
+  local rc=$?
+  tail -3 "$out/$log"
+  case $rc in 0|1) ;; *) echo "fatal rc=$rc"; exit $rc ;; esac
+  return 0
+}
+step 700 pytest_gpu.log python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider
+step 200 smoke.log python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step 240 bench_cal.log python -u bench.py
+step 200 bench_sf.log python -u bench.py --workload sf --cpu-budget 0
+step 200 bench_tf.log python -u bench.py --workload tf --cpu-budget 0
+step 200 bench_scannet.log python -u bench.py --workload scannet --cpu-budget 0
+step 240 prof_cal.log rocprofv3 --kernel-trace --stats -d "$out/prof_cal" -o cal -- python3 bench.py --cpu-budget 0 --in-flight 1
+step 60 cal_summary.log python tools/prof_summary.py "$out/prof_cal" "$out/cal_kernel_stats.csv"
+step 240 prof_sf.log rocprofv3 --kernel-trace --stats -d "$out/prof_sf" -o sf -- python3 bench.py --workload sf --cpu-budget 0 --in-flight 1
+step 60 sf_summary.log python tools/prof_summary.py "$out/prof_sf" "$out/sf_kernel_stats.csv"
+exit 0
