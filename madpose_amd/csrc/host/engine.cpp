@@ -1115,6 +1115,8 @@ class Run {
     // per-iteration best scores / slots / model counts back to pinned host memory.
     // best: best_min_model_score when the batch starts (the scoring's early exit).
     bool batch_prof_ = false;
+    double launch_s_ = 0.0; // main-thread time in launch_batch (MADPOSE_LO_TIMING)
+    int launch_n_ = 0;
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
     // best runs LO and cuts it; score_batch then skips the iterations behind a record
     void launch_batch(const Batch &g, double best, bool cut_on_record) {
@@ -1302,7 +1304,12 @@ void Run::run(Model *best, Stats *S) {
         auto t_batch = Clock::now();
         const Batch &g = gen[cur];
         const uint32_t B = g.B;
-        if (!launched) launch_batch(g, best_min_score, it >= lo_start);
+        if (!launched) {
+            auto tl = Clock::now();
+            launch_batch(g, best_min_score, it >= lo_start);
+            launch_s_ += secs(tl);
+            ++launch_n_;
+        }
         launched = false;
         const bool prof = batch_prof_;
         // While the batch is in flight, the sampler thread draws the next one into the
@@ -1496,6 +1503,11 @@ void Run::run(Model *best, Stats *S) {
         S->num_lo_sweeps += L.count;
         for (int k = 0; k < 3; ++k) tsum[k] += L.t[k];
     }
+    if (std::getenv("MADPOSE_LO_TIMING"))
+        std::fprintf(stderr, "[engine] pair: %.1f us total, %d batches (%d launched by the estimator thread, %.1f us "
+                     "each), gpu wait %.1f us, sampling %.1f us, LO %.1f us\n", 1e6 * S->seconds_total,
+                     (int)S->num_batches, launch_n_, launch_n_ ? 1e6 * launch_s_ / launch_n_ : 0.0,
+                     1e6 * S->seconds_gpu_wait, 1e6 * sample_s_, 1e6 * S->seconds_lo);
     if (std::getenv("MADPOSE_LO_TIMING") && lo_t_[2] > 0)
         std::fprintf(stderr, "[engine] %d LO: prefix %.1f us, steps %.1f us, step sum %.1f us, step0 %.1f us, longest "
                      "step %.1f us, step0 fit %.1f us, step0 score %.1f us, other fit %.1f us, step0 lsq %.1f us, "
