@@ -438,6 +438,9 @@ struct CtxLease {
 
 // ---------------------------------------------------------------------------
 void inv3(const double *K, double *Ki) {
+    // no FMA contraction: the calibrated rays K^-1 x the MD solvers see are the oracle's
+    // (oracle/src/estimator.cpp inv3, mv3) to the bit
+#pragma clang fp contract(off)
     const double d = K[0] * (K[4] * K[8] - K[5] * K[7]) - K[1] * (K[3] * K[8] - K[5] * K[6]) +
                      K[2] * (K[3] * K[7] - K[4] * K[6]);
     Ki[0] = (K[4] * K[8] - K[5] * K[7]) / d;

@@ -628,6 +628,12 @@ template <int K, class FJ> MP_HD void newton_polish(double (&z)[5], FJ fj) {
     }
 }
 
+// o = M v, each row (M0 v0 + M1 v1) + M2 v2 (oracle/src/estimator.cpp mv3)
+MP_HD void mv3_exact(const double *M, const double *v, double *o) {
+#pragma clang fp contract(off)
+    for (int r = 0; r < 3; ++r) o[r] = M[3 * r] * v[0] + M[3 * r + 1] * v[1] + M[3 * r + 2] * v[2];
+}
+
 // prescale x / f (md.cpp:202-217)
 MP_HD double mean_abs_xy(const double (&x)[4][3]) {
 #pragma clang fp contract(off)

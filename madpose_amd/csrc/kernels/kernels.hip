@@ -290,7 +290,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kC
 // The shared- and two-focal MD solvers with the oracle's arithmetic (mp_md_exact.h):
 // one sample per lane, register-resident (only the sorted root list goes to the lane's
 // column of an LDS block); accepted models go to their slots in root order, as
-// md_solve_group's.  The kernel is issue-bound (the predicated, fully unrolled QR), so
+// md_solve_group's.  (The calibrated MD solver keeps md_solve_group: the exact form
+// of it ran 152 us per cal launch against 57 us, on the critical path of the 95 us
+// point chain -- cal 6.0-6.6 -> 6.9-7.3 ms per pair, profiles/r04/calx/.)  The kernel is issue-bound (the predicated, fully unrolled QR), so
 // full waves pay best: 64 / 16 / 8 / 4 samples per wave gave sf 12.9 / 13.4 / 15.0 /
 // 16.3 ms per pair on one box (profiles/r04/mdx/).
 template <int V>
@@ -304,6 +306,8 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
     if (idx >= nlist) return;
     const int b = list[idx];
     const int *s = samples + (size_t)b * kSampleStride;
+    const LaneScratch W{scr + threadIdx.x, 64};
+    int n = 0;
     double x[4][3], y[4][3], dx[4], dy[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -317,7 +321,6 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
         dx[j] = D.d0[i];
         dy[j] = D.d1[i];
     }
-    int n = 0;
     auto pose = [&](const double (&sol)[6]) {
         Model m;
         m.focal0 = sol[4];
@@ -327,7 +330,6 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
             ++n;
         }
     };
-    const LaneScratch W{scr + threadIdx.x, 64};
     if (V == kSF)
         mdx_sols_sf(W, x, y, dx, dy, pose);
     else
