@@ -644,42 +644,51 @@ MP_HD double mean_abs_xy(const double (&x)[4][3]) {
 
 } // namespace mdx
 
-// solve_scale_and_shift (calibrated, md.cpp:161-200): rays x, y (3 x 3); emit(sol)
-// per solution in ascending b1, sol = (1, b1, a2, b2 * a2, 1, 1).  Scratch >= 4.
-template <class Emit>
-MP_HD int mdx_sols_cal(LaneScratch W, const double (&x3)[3][3], const double (&y3)[3][3], const double *dx,
-                       const double *dy, Emit &&emit) {
-#pragma clang fp contract(off)
-    double x[4][3], y[4][3];
-    for (int i = 0; i < 3; ++i)
-        for (int c = 0; c < 3; ++c) {
-            x[i][c] = x3[i][c];
-            y[i][c] = y3[i][c];
-        }
-    for (int c = 0; c < 3; ++c) x[3][c] = y[3][c] = 0.0;
-    const int pr[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+// The solvers in two parts, as the oracle's loop over roots: setup() builds the
+// sample's system and returns the ascending real roots of its resultant; root() turns
+// one root into a solution, false when the oracle's filters reject it.  The
+// estimator's kernel runs root() on one lane per root (kernels.hip md_exact); the
+// mdx_sols_* loops run them in one lane (the direct solver entries, the host check).
+
+// solve_scale_and_shift (calibrated, md.cpp:161-200): rays x, y (3 x 3); solutions in
+// ascending b1, sol = (1, b1, a2, b2 * a2, 1, 1).
+struct MdxCal {
+    static constexpr int NR = 4;
     PairTerms T[3];
-    for (int k = 0; k < 3; ++k) T[k] = mdx::pair_terms<false>(x, y, dx, dy, pr[k][0], pr[k][1]);
-    double Q[3][3], Pm[3][3], L[3][3];
-    for (int k = 0; k < 3; ++k)
+    double l1[3], l2[3];
+    MP_HD int setup(const double (&x3)[3][3], const double (&y3)[3][3], const double *dx, const double *dy,
+                    double (&roots)[NR]) {
+#pragma clang fp contract(off)
+        double x[4][3], y[4][3];
+        for (int i = 0; i < 3; ++i)
+            for (int c = 0; c < 3; ++c) {
+                x[i][c] = x3[i][c];
+                y[i][c] = y3[i][c];
+            }
+        for (int c = 0; c < 3; ++c) x[3][c] = y[3][c] = 0.0;
+        for (int k = 0; k < NR; ++k) roots[k] = 0.0;
+        const int pr[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+        for (int k = 0; k < 3; ++k) T[k] = mdx::pair_terms<false>(x, y, dx, dy, pr[k][0], pr[k][1]);
+        double Q[3][3], Pm[3][3], L[3][3];
+        for (int k = 0; k < 3; ++k)
+            for (int c = 0; c < 3; ++c) {
+                Q[k][c] = T[k].B[c];
+                Pm[k][c] = T[k].A[c];
+            }
+        if (!mdx::qr_solve<3, 3>(Q, Pm, L)) return 0;
+        const double l0[3] = {L[0][2], L[0][1], L[0][0]};
         for (int c = 0; c < 3; ++c) {
-            Q[k][c] = T[k].B[c];
-            Pm[k][c] = T[k].A[c];
+            l1[c] = L[1][2 - c];
+            l2[c] = L[2][2 - c];
         }
-    constexpr int NR = 4;
-    if (!mdx::qr_solve<3, 3>(Q, Pm, L)) return 0;
-    const double l0[3] = {L[0][2], L[0][1], L[0][0]}, l1[3] = {L[1][2], L[1][1], L[1][0]},
-                 l2[3] = {L[2][2], L[2][1], L[2][0]};
-    double a[5], b[5], quart[5];
-    mdx::pmul(l1, l1, a);
-    mdx::pmul(l0, l2, b);
-    mdx::psub(a, b, quart);
-    double roots[4];
-    const int nr = mdx::real_roots(quart, roots);
-    for (int k = 0; k < NR; ++k) W[k] = roots[k];
-    int nsol = 0;
-    for (int q = 0; q < nr; ++q) {
-        const double b1 = W[q];
+        double a[5], b[5], quart[5];
+        mdx::pmul(l1, l1, a);
+        mdx::pmul(l0, l2, b);
+        mdx::psub(a, b, quart);
+        return mdx::real_roots(quart, roots);
+    }
+    MP_HD bool root(double b1, double (&sol)[6]) const {
+#pragma clang fp contract(off)
         const double s = mdx::peval(l2, b1);
         const double beta = mdx::peval(l1, b1) / s;
         double z[5] = {b1, beta, s, 0.0, 0.0};
@@ -696,80 +705,81 @@ MP_HD int mdx_sols_cal(LaneScratch W, const double (&x3)[3][3], const double (&y
                 J[k][2] = -vb;
             }
         });
-        if (!(z[2] > 0)) continue;
+        if (!(z[2] > 0)) return false;
         const double a2 = sqrt(z[2]);
-        double sol[6] = {1.0, z[0], a2, z[1] * a2, 1.0, 1.0};
-        emit(sol);
-        ++nsol;
+        sol[0] = 1.0;
+        sol[1] = z[0];
+        sol[2] = a2;
+        sol[3] = z[1] * a2;
+        sol[4] = sol[5] = 1.0;
+        return true;
     }
-    return nsol;
-}
+};
 
 // solve_scale_and_shift_shared_focal (md.cpp:219-284): x0, y0 pp-centred normalized
-// points (homogeneous, 4 x 3); sol = (1, b1, a2, b2 * a2, f, f).  Scratch >= 8.
-template <class Emit>
-MP_HD int mdx_sols_sf(LaneScratch W, const double (&x0)[4][3], const double (&y0)[4][3], const double *dx,
-                      const double *dy, Emit &&emit) {
-#pragma clang fp contract(off)
-    const double f0 = 0.5 * (mdx::mean_abs_xy(x0) + mdx::mean_abs_xy(y0));
-    double x[4][3], y[4][3];
-    for (int i = 0; i < 4; ++i) {
-        x[i][0] = x0[i][0] / f0;
-        x[i][1] = x0[i][1] / f0;
-        x[i][2] = x0[i][2];
-        y[i][0] = y0[i][0] / f0;
-        y[i][1] = y0[i][1] / f0;
-        y[i][2] = y0[i][2];
-    }
-    const int pr[4][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}};
+// points (homogeneous, 4 x 3); sol = (1, b1, a2, b2 * a2, f, f).
+struct MdxSF {
+    static constexpr int NR = 8;
     PairTerms T[4];
-    double M[4][4], Rh[4][4], L[4][4];
-    for (int k = 0; k < 4; ++k) {
-        T[k] = mdx::pair_terms<true>(x, y, dx, dy, pr[k][0], pr[k][1]);
-        M[k][0] = T[k].A[0];
-        M[k][1] = T[k].A[1];
-        M[k][2] = -T[k].B[0];
-        M[k][3] = -T[k].B[1];
-        Rh[k][0] = -T[k].A[2];
-        Rh[k][1] = T[k].B[2];
-        Rh[k][2] = T[k].dz1;
-        Rh[k][3] = -T[k].dz0;
+    double q0[4][2], q1[4][2], X[5], Y[5], f0;
+    MP_HD int setup(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                    double (&roots)[NR]) {
+#pragma clang fp contract(off)
+        for (int k = 0; k < NR; ++k) roots[k] = 0.0;
+        f0 = 0.5 * (mdx::mean_abs_xy(x0) + mdx::mean_abs_xy(y0));
+        double x[4][3], y[4][3];
+        for (int i = 0; i < 4; ++i) {
+            x[i][0] = x0[i][0] / f0;
+            x[i][1] = x0[i][1] / f0;
+            x[i][2] = x0[i][2];
+            y[i][0] = y0[i][0] / f0;
+            y[i][1] = y0[i][1] / f0;
+            y[i][2] = y0[i][2];
+        }
+        const int pr[4][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}};
+        double M[4][4], Rh[4][4], L[4][4];
+        for (int k = 0; k < 4; ++k) {
+            T[k] = mdx::pair_terms<true>(x, y, dx, dy, pr[k][0], pr[k][1]);
+            M[k][0] = T[k].A[0];
+            M[k][1] = T[k].A[1];
+            M[k][2] = -T[k].B[0];
+            M[k][3] = -T[k].B[1];
+            Rh[k][0] = -T[k].A[2];
+            Rh[k][1] = T[k].B[2];
+            Rh[k][2] = T[k].dz1;
+            Rh[k][3] = -T[k].dz0;
+        }
+        if (!mdx::qr_solve<4, 4>(M, Rh, L)) return 0;
+        for (int r = 0; r < 4; ++r) {
+            q0[r][0] = L[r][3];
+            q0[r][1] = L[r][0];
+            q1[r][0] = L[r][2];
+            q1[r][1] = L[r][1];
+        }
+        const double Wp[2] = {0.0, 1.0};
+        double t0[3], t1[3], al0[3], al1[3], al2[3], be0[3], be1[3], be2[3];
+        mdx::pmul(q0[1], q0[1], t0);
+        mdx::pmul(q0[0], Wp, t1);
+        mdx::psub(t0, t1, al0);
+        mdx::pmul(q0[1], q1[1], t0);
+        mdx::pscale(t0, 2.0);
+        mdx::pmul(q1[0], Wp, t1);
+        mdx::psub(t0, t1, al1);
+        mdx::pmul(q1[1], q1[1], al2);
+        mdx::pmul(q0[3], q0[3], be0);
+        mdx::pmul(q0[3], q1[3], t0);
+        mdx::pscale(t0, 2.0);
+        mdx::pmul(q0[2], Wp, t1);
+        mdx::psub(t0, t1, be1);
+        mdx::pmul(q1[3], q1[3], t0);
+        mdx::pmul(q1[2], Wp, t1);
+        mdx::psub(t0, t1, be2);
+        double R[9];
+        mdx::quad_resultant<3, 3, 3, 3, 3, 3, 5, 5, 5, 9>(al0, al1, al2, be0, be1, be2, X, Y, R);
+        return mdx::real_roots(R, roots);
     }
-    constexpr int NR = 8;
-    if (!mdx::qr_solve<4, 4>(M, Rh, L)) return 0;
-    double q0[4][2], q1[4][2];
-    for (int r = 0; r < 4; ++r) {
-        q0[r][0] = L[r][3];
-        q0[r][1] = L[r][0];
-        q1[r][0] = L[r][2];
-        q1[r][1] = L[r][1];
-    }
-    const double Wp[2] = {0.0, 1.0};
-    double t0[3], t1[3], al0[3], al1[3], al2[3], be0[3], be1[3], be2[3];
-    mdx::pmul(q0[1], q0[1], t0);
-    mdx::pmul(q0[0], Wp, t1);
-    mdx::psub(t0, t1, al0);
-    mdx::pmul(q0[1], q1[1], t0);
-    mdx::pscale(t0, 2.0);
-    mdx::pmul(q1[0], Wp, t1);
-    mdx::psub(t0, t1, al1);
-    mdx::pmul(q1[1], q1[1], al2);
-    mdx::pmul(q0[3], q0[3], be0);
-    mdx::pmul(q0[3], q1[3], t0);
-    mdx::pscale(t0, 2.0);
-    mdx::pmul(q0[2], Wp, t1);
-    mdx::psub(t0, t1, be1);
-    mdx::pmul(q1[3], q1[3], t0);
-    mdx::pmul(q1[2], Wp, t1);
-    mdx::psub(t0, t1, be2);
-    double X[5], Y[5], R[9];
-    mdx::quad_resultant<3, 3, 3, 3, 3, 3, 5, 5, 5, 9>(al0, al1, al2, be0, be1, be2, X, Y, R);
-    double roots[8];
-    const int nr = mdx::real_roots(R, roots);
-    for (int k = 0; k < NR; ++k) W[k] = roots[k];
-    int nsol = 0;
-    for (int q = 0; q < nr; ++q) {
-        const double w = W[q];
+    MP_HD bool root(double w, double (&sol)[6]) const {
+#pragma clang fp contract(off)
         const double s = -mdx::peval(X, w) / mdx::peval(Y, w);
         const double wb1 = mdx::peval(q0[1], w) + s * mdx::peval(q1[1], w);
         const double tb = mdx::peval(q0[3], w) + s * mdx::peval(q1[3], w);
@@ -788,79 +798,80 @@ MP_HD int mdx_sols_sf(LaneScratch W, const double (&x0)[4][3], const double (&y0
                 J[k][3] = ua - v[2] * vb;
             }
         });
-        if (z[3] < 0) continue; // src/solver.cpp:283
-        if (!(z[2] > 0)) continue;
+        if (z[3] < 0) return false; // src/solver.cpp:283
+        if (!(z[2] > 0)) return false;
         const double a2 = sqrt(z[2]);
         const double f = f0 / sqrt(z[3]);
-        double sol[6] = {1.0, z[0], a2, z[1] * a2, f, f};
-        emit(sol);
-        ++nsol;
+        sol[0] = 1.0;
+        sol[1] = z[0];
+        sol[2] = a2;
+        sol[3] = z[1] * a2;
+        sol[4] = sol[5] = f;
+        return true;
     }
-    return nsol;
-}
+};
 
 // solve_scale_and_shift_two_focal (md.cpp:286-352); sol = (1, b1, a2, b2 * a2, f1, f2).
-// Scratch >= 4.
-template <class Emit>
-MP_HD int mdx_sols_tf(LaneScratch W, const double (&x0)[4][3], const double (&y0)[4][3], const double *dx,
-                      const double *dy, Emit &&emit) {
-#pragma clang fp contract(off)
-    const double f1 = mdx::mean_abs_xy(x0), f2 = mdx::mean_abs_xy(y0);
-    double x[4][3], y[4][3];
-    for (int i = 0; i < 4; ++i) {
-        x[i][0] = x0[i][0] / f1;
-        x[i][1] = x0[i][1] / f1;
-        x[i][2] = x0[i][2];
-        y[i][0] = y0[i][0] / f2;
-        y[i][1] = y0[i][1] / f2;
-        y[i][2] = y0[i][2];
-    }
-    const int pr[5][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}, {1, 3}};
+struct MdxTF {
+    static constexpr int NR = 4;
     PairTerms T[5];
-    double M[5][5], Rh[5][3], L[5][3];
-    for (int k = 0; k < 5; ++k) {
-        T[k] = mdx::pair_terms<true>(x, y, dx, dy, pr[k][0], pr[k][1]);
-        M[k][0] = T[k].A[0];
-        M[k][1] = T[k].A[1];
-        M[k][2] = -T[k].B[0];
-        M[k][3] = -T[k].B[1];
-        M[k][4] = -T[k].dz1;
-        Rh[k][0] = -T[k].A[2];
-        Rh[k][1] = T[k].B[2];
-        Rh[k][2] = -T[k].dz0;
+    double q0[5][2], q1[5][1], X[3], Y[2], f1, f2;
+    MP_HD int setup(const double (&x0)[4][3], const double (&y0)[4][3], const double *dx, const double *dy,
+                    double (&roots)[NR]) {
+#pragma clang fp contract(off)
+        for (int k = 0; k < NR; ++k) roots[k] = 0.0;
+        f1 = mdx::mean_abs_xy(x0);
+        f2 = mdx::mean_abs_xy(y0);
+        double x[4][3], y[4][3];
+        for (int i = 0; i < 4; ++i) {
+            x[i][0] = x0[i][0] / f1;
+            x[i][1] = x0[i][1] / f1;
+            x[i][2] = x0[i][2];
+            y[i][0] = y0[i][0] / f2;
+            y[i][1] = y0[i][1] / f2;
+            y[i][2] = y0[i][2];
+        }
+        const int pr[5][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}, {1, 3}};
+        double M[5][5], Rh[5][3], L[5][3];
+        for (int k = 0; k < 5; ++k) {
+            T[k] = mdx::pair_terms<true>(x, y, dx, dy, pr[k][0], pr[k][1]);
+            M[k][0] = T[k].A[0];
+            M[k][1] = T[k].A[1];
+            M[k][2] = -T[k].B[0];
+            M[k][3] = -T[k].B[1];
+            M[k][4] = -T[k].dz1;
+            Rh[k][0] = -T[k].A[2];
+            Rh[k][1] = T[k].B[2];
+            Rh[k][2] = -T[k].dz0;
+        }
+        if (!mdx::qr_solve<5, 3>(M, Rh, L)) return 0;
+        for (int r = 0; r < 5; ++r) {
+            q0[r][0] = L[r][2];
+            q0[r][1] = L[r][0];
+            q1[r][0] = L[r][1];
+        }
+        const double Wp[2] = {0.0, 1.0};
+        double t0[3], t1[3], s0[2], s1[2], u0[1], al0[3], al1[2], al2[1], be0[3], be1[2], be2[1];
+        mdx::pmul(q0[1], q0[1], t0);
+        mdx::pmul(q0[0], Wp, t1);
+        mdx::psub(t0, t1, al0);
+        mdx::pmul(q0[1], q1[1], s0);
+        mdx::pscale(s0, 2.0);
+        mdx::pmul(q1[0], Wp, s1);
+        mdx::psub(s0, s1, al1);
+        mdx::pmul(q1[1], q1[1], al2);
+        mdx::pmul(q0[3], q0[3], be0);
+        mdx::pmul(q0[3], q1[3], s0);
+        mdx::pscale(s0, 2.0);
+        mdx::psub(s0, q0[2], be1);
+        mdx::pmul(q1[3], q1[3], u0);
+        mdx::psub(u0, q1[2], be2);
+        double R[5];
+        mdx::quad_resultant<3, 2, 1, 3, 2, 1, 3, 2, 4, 5>(al0, al1, al2, be0, be1, be2, X, Y, R);
+        return mdx::real_roots(R, roots);
     }
-    constexpr int NR = 4;
-    if (!mdx::qr_solve<5, 3>(M, Rh, L)) return 0;
-    double q0[5][2], q1[5][1];
-    for (int r = 0; r < 5; ++r) {
-        q0[r][0] = L[r][2];
-        q0[r][1] = L[r][0];
-        q1[r][0] = L[r][1];
-    }
-    const double Wp[2] = {0.0, 1.0};
-    double t0[3], t1[3], s0[2], s1[2], u0[1], al0[3], al1[2], al2[1], be0[3], be1[2], be2[1];
-    mdx::pmul(q0[1], q0[1], t0);
-    mdx::pmul(q0[0], Wp, t1);
-    mdx::psub(t0, t1, al0);
-    mdx::pmul(q0[1], q1[1], s0);
-    mdx::pscale(s0, 2.0);
-    mdx::pmul(q1[0], Wp, s1);
-    mdx::psub(s0, s1, al1);
-    mdx::pmul(q1[1], q1[1], al2);
-    mdx::pmul(q0[3], q0[3], be0);
-    mdx::pmul(q0[3], q1[3], s0);
-    mdx::pscale(s0, 2.0);
-    mdx::psub(s0, q0[2], be1);
-    mdx::pmul(q1[3], q1[3], u0);
-    mdx::psub(u0, q1[2], be2);
-    double X[3], Y[2], R[5];
-    mdx::quad_resultant<3, 2, 1, 3, 2, 1, 3, 2, 4, 5>(al0, al1, al2, be0, be1, be2, X, Y, R);
-    double roots[4];
-    const int nr = mdx::real_roots(R, roots);
-    for (int k = 0; k < NR; ++k) W[k] = roots[k];
-    int nsol = 0;
-    for (int q = 0; q < nr; ++q) {
-        const double w1 = W[q];
+    MP_HD bool root(double w1, double (&sol)[6]) const {
+#pragma clang fp contract(off)
         const double t = -mdx::peval(X, w1) / mdx::peval(Y, w1);
         double m[5];
         for (int r = 0; r < 5; ++r) m[r] = mdx::peval(q0[r], w1) + t * q1[r][0];
@@ -881,14 +892,50 @@ MP_HD int mdx_sols_tf(LaneScratch W, const double (&x0)[4][3], const double (&y0
                 J[k][4] = -v[2] * vb;
             }
         });
-        if (z[3] < 0 || z[4] < 0) continue; // src/solver.cpp:470
-        if (!(z[2] > 0)) continue;
+        if (z[3] < 0 || z[4] < 0) return false; // src/solver.cpp:470
+        if (!(z[2] > 0)) return false;
         const double a2 = sqrt(z[2]);
-        double sol[6] = {1.0, z[0], a2, z[1] * a2, f1 / sqrt(z[3]), f2 / sqrt(z[4])};
-        emit(sol);
-        ++nsol;
+        sol[0] = 1.0;
+        sol[1] = z[0];
+        sol[2] = a2;
+        sol[3] = z[1] * a2;
+        sol[4] = f1 / sqrt(z[3]);
+        sol[5] = f2 / sqrt(z[4]);
+        return true;
     }
-    return nsol;
+};
+
+// One lane, every root in turn (the direct solver entries and the host check): the
+// sorted roots go through the lane's scratch column, read back by a runtime index.
+template <class S, class In, class Emit>
+MP_HD int mdx_sols(LaneScratch W, const In &x, const In &y, const double *dx, const double *dy, Emit &&emit) {
+    S sys;
+    double roots[S::NR];
+    const int nr = sys.setup(x, y, dx, dy, roots);
+    for (int k = 0; k < S::NR; ++k) W[k] = roots[k];
+    int n = 0;
+    for (int q = 0; q < nr; ++q) {
+        double sol[6];
+        if (!sys.root(W[q], sol)) continue;
+        emit(sol);
+        ++n;
+    }
+    return n;
+}
+template <class Emit>
+MP_HD int mdx_sols_cal(LaneScratch W, const double (&x)[3][3], const double (&y)[3][3], const double *dx,
+                       const double *dy, Emit &&emit) {
+    return mdx_sols<MdxCal>(W, x, y, dx, dy, emit);
+}
+template <class Emit>
+MP_HD int mdx_sols_sf(LaneScratch W, const double (&x)[4][3], const double (&y)[4][3], const double *dx,
+                      const double *dy, Emit &&emit) {
+    return mdx_sols<MdxSF>(W, x, y, dx, dy, emit);
+}
+template <class Emit>
+MP_HD int mdx_sols_tf(LaneScratch W, const double (&x)[4][3], const double (&y)[4][3], const double *dx,
+                      const double *dy, Emit &&emit) {
+    return mdx_sols<MdxTF>(W, x, y, dx, dy, emit);
 }
 
 // per-lane scratch doubles of the three solvers (the root list, read back by a

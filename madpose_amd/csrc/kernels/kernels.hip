@@ -287,54 +287,107 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kC
     }
 }
 
-// The shared- and two-focal MD solvers with the oracle's arithmetic (mp_md_exact.h):
-// one sample per lane, register-resident (only the sorted root list goes to the lane's
-// column of an LDS block); accepted models go to their slots in root order, as
-// md_solve_group's.  (The calibrated MD solver keeps md_solve_group: the exact form
-// of it ran 152 us per cal launch against 57 us, on the critical path of the 95 us
-// point chain -- cal 6.0-6.6 -> 6.9-7.3 ms per pair, profiles/r04/calx/.)  The kernel is issue-bound (the predicated, fully unrolled QR), so
-// full waves pay best: 64 / 16 / 8 / 4 samples per wave gave sf 12.9 / 13.4 / 15.0 /
-// 16.3 ms per pair on one box (profiles/r04/mdx/).
-template <int V>
+// The MD solvers with the oracle's arithmetic (mp_md_exact.h: setup() = system +
+// sorted real roots, root() = one root's polish and filters), two layouts:
+//  R = 1: one sample per lane, its roots in turn (shared focal: 8 roots behind an 8 x 8
+//         QR; the kernel is issue-bound there and full waves pay best -- 64 / 16 / 8 / 4
+//         samples per wave gave sf 12.9 / 13.4 / 15.0 / 16.3 ms per pair, profiles/r04/mdx/);
+//  R = 4: four lanes per sample (16 per wave), every lane of a group runs the sample's
+//         setup (the same doubles in each) and lane r the r-th root, the accepted
+//         models compacted in root order by a ballot -- for the two-focal quartic,
+//         whose roots' polish + pose dominate a lane's serial chain (165 -> 91 us per
+//         tf launch, under the 206 us point chain; tf 13.4 -> 12.8 ms per pair,
+//         profiles/r04/mdx4/).
+// Accepted models go to their slots in root order, as md_solve_group's.  The
+// calibrated MD solver keeps md_solve_group (57 us): its exact form, 152 us lane per
+// sample and 106 us lane per root, outlasts the 99 us calibrated point chain (cal
+// 5.6-6.7 -> 5.9-6.7 ms per pair with it, profiles/r04/calx/, mdx4/); its parity at the
+// full sizes holds either way.
+template <int V> struct MdxSys;
+template <> struct MdxSys<kCal> {
+    using S = MdxCal;
+    static constexpr int K = 3;
+};
+template <> struct MdxSys<kSF> {
+    using S = MdxSF;
+    static constexpr int K = 4;
+};
+template <> struct MdxSys<kTF> {
+    using S = MdxTF;
+    static constexpr int K = 4;
+};
+
+template <int V, int R>
 __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                       const int *samples, Model *models, ScoreRec *recs, int *counts,
                                                       int maxm) {
-    static_assert(V == kSF || V == kTF, "md_exact_kernel: shared / two focal");
-    constexpr int NS = V == kSF ? kMdxScratchSF : kMdxScratchTF;
-    __shared__ double scr[NS * 64];
-    const int idx = blockIdx.x * 64 + threadIdx.x;
-    if (idx >= nlist) return;
-    const int b = list[idx];
+    using Sys = typename MdxSys<V>::S;
+    constexpr int K = MdxSys<V>::K, NR = Sys::NR;
+    static_assert(R == 1 || (R == 4 && NR == 4), "one lane per sample, or one lane per root of a quartic");
+    __shared__ double scr[R == 1 ? NR * 64 : 1];
+    const int g = threadIdx.x / R, r = threadIdx.x % R;
+    const int idx = blockIdx.x * (64 / R) + g;
+    const bool active = idx < nlist;
+    if (R == 1 && !active) return;
+    const int b = list[active ? idx : nlist - 1];
     const int *s = samples + (size_t)b * kSampleStride;
-    const LaneScratch W{scr + threadIdx.x, 64};
-    int n = 0;
-    double x[4][3], y[4][3], dx[4], dy[4];
+    double x[K][3], y[K][3], dx[K], dy[K];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < K; ++j) {
         const int i = s[j];
-        x[j][0] = D.x0u[i];
-        x[j][1] = D.x0v[i];
-        x[j][2] = 1.0;
-        y[j][0] = D.x1u[i];
-        y[j][1] = D.x1v[i];
-        y[j][2] = 1.0;
+        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+        if (V == kCal) { // calibrated rays K^-1 x as the oracle forms them (estimator.cpp mv3)
+            mdx::mv3_exact(C.K0i, xa, x[j]);
+            mdx::mv3_exact(C.K1i, xb, y[j]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                x[j][q] = xa[q];
+                y[j][q] = xb[q];
+            }
+        }
         dx[j] = D.d0[i];
         dy[j] = D.d1[i];
     }
-    auto pose = [&](const double (&sol)[6]) {
-        Model m;
+    auto accept = [&](const double (&sol)[6], Model &m) {
         m.focal0 = sol[4];
         m.focal1 = sol[5];
-        if (md_pose_from_sol<4>(x, y, dx, dy, sol, sol[4], sol[5], m) && md_accept(C, m)) {
-            if (n < maxm) put_model(C, m, b, n, maxm, models, recs);
-            ++n;
-        }
+        return md_pose_from_sol<K>(x, y, dx, dy, sol, sol[4], sol[5], m) && md_accept(C, m);
     };
-    if (V == kSF)
-        mdx_sols_sf(W, x, y, dx, dy, pose);
-    else
-        mdx_sols_tf(W, x, y, dx, dy, pose);
-    counts[b] = n < maxm ? n : maxm;
+    if constexpr (R == 1) {
+        int n = 0;
+        mdx_sols<Sys>(LaneScratch{scr + threadIdx.x, 64}, x, y, dx, dy, [&](const double (&sol)[6]) {
+            Model m;
+            if (accept(sol, m)) {
+                if (n < maxm) put_model(C, m, b, n, maxm, models, recs);
+                ++n;
+            }
+        });
+        counts[b] = n < maxm ? n : maxm;
+    } else {
+        Sys sys;
+        double roots[NR];
+        const int nr = sys.setup(x, y, dx, dy, roots);
+        double root = 0.0;
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+            if (q == r) root = opaque(roots[q]);
+        Model m;
+        bool keep = false;
+        if (active && r < nr) {
+            double sol[6];
+            keep = sys.root(root, sol) && accept(sol, m);
+        }
+        const unsigned long long ball = __ballot(keep);
+        const int g0 = (threadIdx.x & 63) & ~(R - 1);
+        const unsigned long long mine = (ball >> g0) & ((1ull << R) - 1);
+        const int pos = __popcll(mine & ((1ull << r) - 1));
+        if (keep && pos < maxm) put_model(C, m, b, pos, maxm, models, recs);
+        if (active && r == 0) {
+            const int n = __popcll(mine);
+            counts[b] = n < maxm ? n : maxm;
+        }
+    }
 }
 
 template <int K>
@@ -895,9 +948,15 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
         // default solvers on 16-lane groups (MADPOSE_MD_LANE: one sample per lane)
         static const bool lane_md = std::getenv("MADPOSE_MD_LANE") != nullptr;
         const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
-        if constexpr (v != kCal) {
+        if constexpr (v == kSF) {
             if (plain) {
-                md_exact_kernel<v><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+                md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+                return hipGetLastError();
+            }
+        } else if constexpr (v == kTF) {
+            if (plain) {
+                md_exact_kernel<v, 4><<<(nlist + 15) / 16, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                       counts, maxm);
                 return hipGetLastError();
             }
         }
