@@ -282,22 +282,39 @@ inline int lo_lanes_setting() {
 
 // ---------------------------------------------------------------------------
 // Device context: stream + cached buffers (one per device and concurrent caller)
+//
+// The per-batch buffers come in two slots (BatchBufs), the slot of a batch being the
+// host sample slot it was drawn into: the continuation batch is launched into the other
+// slot while the host still reads this one's results (early continuation, Run::run).
+struct BatchBufs {
+    int *d_counts = nullptr;
+    IterResult *d_res = nullptr, *h_res = nullptr;
+    int *d_work = nullptr, *h_work = nullptr; // score_batch's evaluated (model, trip) pairs per iteration
+    Model *d_models = nullptr;
+    ScoreRec *d_recs = nullptr;
+    double *d_scores = nullptr;
+    // score_batch writes the models of the iterations that beat the pre-batch best here
+    // (mapped pinned memory, one slot per iteration of the batch)
+    Model *h_recmodel = nullptr, *d_recmodel = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr}; // solve start / score start / score end
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr; // MD side stream fork / join
+    hipEvent_t ev_h2d = nullptr;                    // the batch's samples have been copied
+    hipEvent_t ev_done = nullptr;                   // the batch's results are on the host
+    unsigned epoch_hi = 0;                          // ~epoch of the batch last launched here
+    bool h2d_pending = false;                       // launched, ev_h2d not yet waited for
+};
+
 struct DeviceCtx {
     int device = 0;
     hipStream_t stream = nullptr;
     int64_t cap_n = 0;
     int cap_b = 0, cap_m = 0;
     double *d_pair = nullptr; // 8 arrays of cap_n
-    int *d_samples = nullptr; // a batch's samples + iteration lists (draw_batch layout)
-    int *d_counts = nullptr;
-    IterResult *d_res = nullptr;
-    int *d_work = nullptr; // score_batch's evaluated (model, trip) pairs per iteration
+    int *d_samples = nullptr; // a batch's samples + iteration lists (draw_batch layout; stream-ordered)
     // score_batch's record word (kernels.hip ScoreBound::rec) and the batch epoch
     unsigned long long *d_recword = nullptr;
     uint32_t epoch = 0;
-    Model *d_models = nullptr;
-    ScoreRec *d_recs = nullptr;
-    double *d_scores = nullptr;
+    BatchBufs bb[2];
     ScoreRec *d_rec1 = nullptr;
     double *d_err = nullptr, *d_score1 = nullptr;
     // staged point-solver workspace (kernels.h PtWorkspace)
@@ -309,47 +326,47 @@ struct DeviceCtx {
     std::unique_ptr<LoWorkers> lo_workers; // created on first parallel LO
     // pinned host mirrors
     int *h_samples = nullptr; // two slots of 9 * max_batch ints
-    IterResult *h_res = nullptr;
-    int *h_work = nullptr;
     double *h_err = nullptr, *h_score1 = nullptr;
     ScoreRec *h_rec1 = nullptr;
     Model *h_model1 = nullptr;
-    // score_batch writes the models of the iterations that beat the pre-batch best here
-    // (mapped pinned memory, one slot per iteration of the batch)
-    Model *h_recmodel = nullptr, *d_recmodel = nullptr;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr}; // solve start / score start / score end
-    // the MD solver runs on md_stream, concurrently with the point-solver stages
-    hipStream_t md_stream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // the MD solver runs on md_stream, concurrently with the point-solver stages; host
+    // reads of a finished batch's device data go through copy_stream (the main stream
+    // may already hold the next batch)
+    hipStream_t md_stream = nullptr, copy_stream = nullptr;
     std::unique_ptr<Sampler> sampler;               // created on first use
 
     void free_all() {
         hipSetDevice(device);
-        for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_counts,
-                        (void *)d_res, (void *)d_work, (void *)d_recword, (void *)d_models, (void *)d_recs, (void *)d_scores,
-                        (void *)d_rec1, (void *)d_err, (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_pen, (void *)d_pt_ncand,
-                        (void *)d_pt_valid, (void *)d_pt_slots})
+        for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_recword, (void *)d_rec1, (void *)d_err,
+                        (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_pen, (void *)d_pt_ncand, (void *)d_pt_valid,
+                        (void *)d_pt_slots})
             if (p) hipFree(p);
-        for (void *p : {(void *)h_samples, (void *)h_res, (void *)h_work, (void *)h_err,
-                        (void *)h_score1, (void *)h_rec1, (void *)h_model1, (void *)h_recmodel})
+        for (void *p : {(void *)h_samples, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1})
             if (p) hipHostFree(p);
-        d_pair = d_err = d_scores = d_score1 = nullptr;
-        d_samples = d_counts = nullptr;
-        d_res = nullptr;
-        d_work = nullptr;
+        for (BatchBufs &q : bb) {
+            for (void *p : {(void *)q.d_counts, (void *)q.d_res, (void *)q.d_work, (void *)q.d_models,
+                            (void *)q.d_recs, (void *)q.d_scores})
+                if (p) hipFree(p);
+            for (void *p : {(void *)q.h_res, (void *)q.h_work, (void *)q.h_recmodel})
+                if (p) hipHostFree(p);
+            q.d_counts = q.d_work = q.h_work = nullptr;
+            q.d_res = q.h_res = nullptr;
+            q.d_models = q.h_recmodel = q.d_recmodel = nullptr;
+            q.d_recs = nullptr;
+            q.d_scores = nullptr;
+            q.h2d_pending = false;
+        }
+        d_pair = d_err = d_score1 = nullptr;
+        d_samples = nullptr;
         d_recword = nullptr;
-        d_models = nullptr;
-        d_recs = d_rec1 = nullptr;
+        d_rec1 = nullptr;
         d_pt_cand = d_pt_pen = nullptr;
         d_pt_ncand = d_pt_valid = nullptr;
         d_pt_slots = nullptr;
         h_samples = nullptr;
-        h_res = nullptr;
-        h_work = nullptr;
         h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
         h_model1 = nullptr;
-        h_recmodel = d_recmodel = nullptr;
         cap_n = 0;
         cap_b = cap_m = 0;
     }
@@ -357,40 +374,44 @@ struct DeviceCtx {
     void ensure(int64_t n, int B, int M) {
         if (n <= cap_n && B <= cap_b && M <= cap_m) return;
         const int64_t nn = std::max<int64_t>(std::max<int64_t>(n, cap_n), 64);
-        const int bb = std::max(B, cap_b), mm = std::max(M, cap_m);
-        free_all();
+        const int bb_ = std::max(B, cap_b), mm = std::max(M, cap_m);
         MP_HIP(hipSetDevice(device));
+        MP_HIP(hipDeviceSynchronize()); // (an early continuation may still use the old buffers)
+        free_all();
         MP_HIP(hipMalloc(&d_pair, sizeof(double) * 8 * nn));
         MP_HIP(hipMalloc(&d_err, sizeof(double) * 3 * nn));
-        MP_HIP(hipMalloc(&d_samples, sizeof(int) * 9 * bb));
-        MP_HIP(hipMalloc(&d_counts, sizeof(int) * bb));
-        MP_HIP(hipMalloc(&d_res, sizeof(IterResult) * bb));
-        MP_HIP(hipMalloc(&d_work, sizeof(int) * bb));
+        MP_HIP(hipMalloc(&d_samples, sizeof(int) * 9 * bb_));
         MP_HIP(hipMalloc(&d_recword, sizeof(unsigned long long)));
         MP_HIP(hipMemset(d_recword, 0xff, sizeof(unsigned long long)));
-        MP_HIP(hipMalloc(&d_models, sizeof(Model) * (size_t)bb * mm));
-        MP_HIP(hipMalloc(&d_recs, sizeof(ScoreRec) * (size_t)bb * mm));
-        MP_HIP(hipMalloc(&d_scores, sizeof(double) * (size_t)bb * mm));
+        for (BatchBufs &q : bb) {
+            MP_HIP(hipMalloc(&q.d_counts, sizeof(int) * bb_));
+            MP_HIP(hipMalloc(&q.d_res, sizeof(IterResult) * bb_));
+            MP_HIP(hipMalloc(&q.d_work, sizeof(int) * bb_));
+            MP_HIP(hipMalloc(&q.d_models, sizeof(Model) * (size_t)bb_ * mm));
+            MP_HIP(hipMalloc(&q.d_recs, sizeof(ScoreRec) * (size_t)bb_ * mm));
+            MP_HIP(hipMalloc(&q.d_scores, sizeof(double) * (size_t)bb_ * mm));
+            MP_HIP(hipHostMalloc(&q.h_res, sizeof(IterResult) * bb_, hipHostMallocDefault));
+            MP_HIP(hipHostMalloc(&q.h_work, sizeof(int) * bb_, hipHostMallocDefault));
+            MP_HIP(hipHostMalloc(&q.h_recmodel, sizeof(Model) * (size_t)bb_,
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            MP_HIP(hipHostGetDevicePointer((void **)&q.d_recmodel, q.h_recmodel, 0));
+        }
         MP_HIP(hipMalloc(&d_rec1, sizeof(ScoreRec) * 64));
-        MP_HIP(hipMalloc(&d_pt_cand, sizeof(double) * (size_t)bb * kPtCandStride));
+        MP_HIP(hipMalloc(&d_pt_cand, sizeof(double) * (size_t)bb_ * kPtCandStride));
         // (the pencil workspace of the shared-focal root stage; a stub elsewhere)
-        MP_HIP(hipMalloc(&d_pt_pen, sizeof(double) * (mm == kMaxModelsSF ? (size_t)bb * kPtPenStride : 1)));
-        MP_HIP(hipMalloc(&d_pt_ncand, sizeof(int) * (size_t)bb));
-        MP_HIP(hipMalloc(&d_pt_valid, sizeof(int) * (size_t)bb * kPtSlotStride));
-        MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb * kPtSlotStride));
+        MP_HIP(hipMalloc(&d_pt_pen, sizeof(double) * (mm == kMaxModelsSF ? (size_t)bb_ * kPtPenStride : 1)));
+        MP_HIP(hipMalloc(&d_pt_ncand, sizeof(int) * (size_t)bb_));
+        MP_HIP(hipMalloc(&d_pt_valid, sizeof(int) * (size_t)bb_ * kPtSlotStride));
+        MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb_ * kPtSlotStride));
         MP_HIP(hipMalloc(&d_score1, sizeof(double) * 64));
         // two slots each: the next batch is generated while the current one is in flight
-        MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 9 * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_res, sizeof(IterResult) * bb, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_work, sizeof(int) * bb, hipHostMallocDefault));
+        MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 9 * bb_, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_err, sizeof(double) * 3 * nn, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_score1, sizeof(double) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_rec1, sizeof(ScoreRec) * 64, hipHostMallocDefault));
         MP_HIP(hipHostMalloc(&h_model1, sizeof(Model) * 64, hipHostMallocDefault));
-        MP_HIP(hipHostMalloc(&h_recmodel, sizeof(Model) * (size_t)bb, hipHostMallocMapped | hipHostMallocCoherent));
-        MP_HIP(hipHostGetDevicePointer((void **)&d_recmodel, h_recmodel, 0));
         cap_n = nn;
-        cap_b = bb;
+        cap_b = bb_;
         cap_m = mm;
     }
 };
@@ -424,9 +445,14 @@ struct CtxLease {
             MP_HIP(hipSetDevice(device));
             MP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             MP_HIP(hipStreamCreateWithFlags(&c->md_stream, hipStreamNonBlocking));
-            for (auto &e : c->ev) MP_HIP(hipEventCreate(&e));
-            MP_HIP(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-            MP_HIP(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+            MP_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+            for (BatchBufs &q : c->bb) {
+                for (auto &e : q.ev) MP_HIP(hipEventCreate(&e));
+                MP_HIP(hipEventCreateWithFlags(&q.ev_fork, hipEventDisableTiming));
+                MP_HIP(hipEventCreateWithFlags(&q.ev_join, hipEventDisableTiming));
+                MP_HIP(hipEventCreateWithFlags(&q.ev_h2d, hipEventDisableTiming));
+                MP_HIP(hipEventCreateWithFlags(&q.ev_done, hipEventDisableTiming));
+            }
         }
         MP_HIP(hipSetDevice(device));
     }
@@ -1117,42 +1143,70 @@ class Run {
     // MD solver on the side stream, the point-solver stages, score_batch, and the
     // per-iteration best scores / slots / model counts back to pinned host memory.
     // best: best_min_model_score when the batch starts (the scoring's early exit).
-    bool batch_prof_ = false;
+    bool batch_prof_[2] = {false, false};
     double launch_s_ = 0.0; // main-thread time in launch_batch (MADPOSE_LO_TIMING)
+    // early continuation (MADPOSE_EARLY_CONT=0: launch the continuation after reading
+    // the batch, as before)
+    const bool early_cont_ = [] {
+        const char *e = std::getenv("MADPOSE_EARLY_CONT");
+        return !(e && e[0] == '0');
+    }();
     int launch_n_ = 0;
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
-    // best runs LO and cuts it; score_batch then skips the iterations behind a record
-    void launch_batch(const Batch &g, double best, bool cut_on_record) {
+    // best runs LO and cuts it; score_batch then skips the iterations behind a record.
+    // gate_prev: the batch is launched before the previous one's results were read (an
+    // early continuation); its kernels leave at once if that batch published a record
+    // (kernels.h batch_cancelled), i.e. if the host is bound to discard this one.
+    void launch_batch(const Batch &g, double best, bool cut_on_record, const BatchBufs *gate_prev = nullptr) {
         const uint32_t B = g.B;
         const int nmd = g.nmd, npt = g.npt;
         hipStream_t s = X_.stream;
+        BatchBufs &Q = X_.bb[g.slot];
         const bool prof = g_prof_on.load(std::memory_order_relaxed);
-        batch_prof_ = prof;
+        batch_prof_[g.slot] = prof;
+        PairData D = D_;
+        if (gate_prev) {
+            D.gate = X_.d_recword;
+            D.gate_hi = gate_prev->epoch_hi;
+        }
         // one upload: samples, then the MD list and the (descending) point list
         MP_HIP(hipMemcpyAsync(X_.d_samples, slot_ptr(g.slot), sizeof(int) * 9 * (size_t)B, hipMemcpyHostToDevice, s));
+        MP_HIP(hipEventRecord(Q.ev_h2d, s));
+        Q.h2d_pending = true;
         const int *d_md_list = X_.d_samples + 8 * (size_t)B, *d_pt_list = d_md_list + nmd;
-        if (prof) MP_HIP(hipEventRecord(X_.ev[0], s));
+        if (prof) MP_HIP(hipEventRecord(Q.ev[0], s));
         // MD iterations on the side stream, point iterations on the main one (they
         // write disjoint model slots); scoring waits for both
         if (nmd > 0) {
-            MP_HIP(hipEventRecord(X_.ev_fork, s));
-            MP_HIP(hipStreamWaitEvent(X_.md_stream, X_.ev_fork, 0));
-            MP_HIP(launch_md_solve(X_.md_stream, D_, P_.C, d_md_list, nmd, X_.d_samples, X_.d_models, X_.d_recs,
-                                   X_.d_counts, maxm_));
-            MP_HIP(hipEventRecord(X_.ev_join, X_.md_stream));
+            MP_HIP(hipEventRecord(Q.ev_fork, s));
+            MP_HIP(hipStreamWaitEvent(X_.md_stream, Q.ev_fork, 0));
+            MP_HIP(launch_md_solve(X_.md_stream, D, P_.C, d_md_list, nmd, X_.d_samples, Q.d_models, Q.d_recs,
+                                   Q.d_counts, maxm_));
+            MP_HIP(hipEventRecord(Q.ev_join, X_.md_stream));
         }
         const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen};
-        MP_HIP(launch_pt_solve(s, D_, P_.C, d_pt_list, npt, X_.d_samples, W, X_.d_models, X_.d_recs, X_.d_counts,
+        MP_HIP(launch_pt_solve(s, D, P_.C, d_pt_list, npt, X_.d_samples, W, Q.d_models, Q.d_recs, Q.d_counts,
                                maxm_));
-        if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, X_.ev_join, 0));
-        if (prof) MP_HIP(hipEventRecord(X_.ev[1], s));
+        if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, Q.ev_join, 0));
+        if (prof) MP_HIP(hipEventRecord(Q.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
-        MP_HIP(launch_score_batch(s, D_, P_.C, X_.d_recs, X_.d_counts, (int)B, maxm_, X_.d_scores, X_.d_res, best, tie_,
-                                  prof ? X_.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
-                                  X_.d_models, X_.d_recmodel));
-        if (prof) MP_HIP(hipEventRecord(X_.ev[2], s));
-        MP_HIP(hipMemcpyAsync(X_.h_res, X_.d_res, sizeof(IterResult) * B, hipMemcpyDeviceToHost, s));
-        if (prof) MP_HIP(hipMemcpyAsync(X_.h_work, X_.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        Q.epoch_hi = epoch_hi;
+        MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.d_res, best, tie_,
+                                  prof ? Q.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
+                                  Q.d_models, Q.d_recmodel));
+        if (prof) MP_HIP(hipEventRecord(Q.ev[2], s));
+        MP_HIP(hipMemcpyAsync(Q.h_res, Q.d_res, sizeof(IterResult) * B, hipMemcpyDeviceToHost, s));
+        if (prof) MP_HIP(hipMemcpyAsync(Q.h_work, Q.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        MP_HIP(hipEventRecord(Q.ev_done, s));
+    }
+    // before host sample slot `slot` is redrawn: the last batch launched from it must
+    // have been copied to the device (an early continuation may still be queued)
+    void slot_free(int slot) {
+        BatchBufs &Q = X_.bb[slot];
+        if (Q.h2d_pending) {
+            MP_HIP(hipEventSynchronize(Q.ev_h2d));
+            Q.h2d_pending = false;
+        }
     }
 
     // Reference-order score of a model (host/lo_sweep.h), on lane 0: the LO that follows
@@ -1165,16 +1219,17 @@ class Run {
     // minimum (GetBestEstimatedModelId, src/hybrid_ransac.h:245-263).  Models whose
     // device score is more than the margin above the device best cannot be the exact
     // winner.  Rare (tests/test_engine_gpu.py::test_tie_margin_inflated forces it).
-    void resolve_tie(uint32_t j, Model *out, double *out_score) {
-        const int nm = X_.h_res[j].count;
-        const double bl = X_.h_res[j].best;
+    void resolve_tie(const BatchBufs &Q, uint32_t j, Model *out, double *out_score) {
+        const int nm = Q.h_res[j].count;
+        const double bl = Q.h_res[j].best;
         std::vector<double> dsc(nm);
         std::vector<Model> ms(nm);
-        MP_HIP(hipMemcpyAsync(dsc.data(), X_.d_scores + (size_t)j * maxm_, sizeof(double) * nm,
-                              hipMemcpyDeviceToHost, X_.stream));
-        MP_HIP(hipMemcpyAsync(ms.data(), X_.d_models + (size_t)j * maxm_, sizeof(Model) * nm, hipMemcpyDeviceToHost,
-                              X_.stream));
-        MP_HIP(hipStreamSynchronize(X_.stream));
+        // (the batch is complete; the main stream may already hold the next one)
+        MP_HIP(hipMemcpyAsync(dsc.data(), Q.d_scores + (size_t)j * maxm_, sizeof(double) * nm,
+                              hipMemcpyDeviceToHost, X_.copy_stream));
+        MP_HIP(hipMemcpyAsync(ms.data(), Q.d_models + (size_t)j * maxm_, sizeof(Model) * nm, hipMemcpyDeviceToHost,
+                              X_.copy_stream));
+        MP_HIP(hipStreamSynchronize(X_.copy_stream));
         *out_score = kMax;
         for (int m = 0; m < nm; ++m) {
             if (!(dsc[m] < kMax) || !(dsc[m] <= bl + tie_)) continue;
@@ -1189,7 +1244,7 @@ class Run {
 
     // the model of a new best: score_batch wrote it to the mapped record slot of its
     // iteration (the batch's stream has been synchronized)
-    Model fetch_model(int b, int /*slot*/) { return X_.h_recmodel[b]; }
+    Model fetch_model(const BatchBufs &Q, int b) { return Q.h_recmodel[b]; }
 };
 
 void Run::run(Model *best, Stats *S) {
@@ -1301,6 +1356,7 @@ void Run::run(Model *best, Stats *S) {
         // GPU starts early and the worker draws the big ones)
         if (!have_next) {
             auto t0 = Clock::now();
+            slot_free(cur);
             generate(gen[cur], batch_size(it, sync_batch((uint32_t)bcur)), cur);
             if (gen[cur].B >= 256) draw_s_per_it_ = 0.5 * draw_s_per_it_ + 0.5 * secs(t0) / gen[cur].B;
         }
@@ -1314,31 +1370,53 @@ void Run::run(Model *best, Stats *S) {
             ++launch_n_;
         }
         launched = false;
-        const bool prof = batch_prof_;
+        BatchBufs &Q = X_.bb[g.slot];
+        const bool prof = batch_prof_[g.slot];
         // While the batch is in flight, the sampler thread draws the next one into the
         // other slot.  It is kept if this batch neither triggers LO nor terminates (both
         // rewind the streams); never across lo_start, where an LO runs before the next
-        // batch.
+        // batch.  Early continuation: the sampler launches it as soon as it is drawn,
+        // behind this batch on the stream, instead of after the host has read this one
+        // -- the GPU goes straight on.  A batch at or past lo_start that holds a new best
+        // runs LO and discards the continuation, and a new best that the device could
+        // prove (a published record) makes the continuation's kernels leave at once
+        // (the gate), so a discarded continuation costs almost nothing; its bound is this
+        // batch's pre-batch best, which is its own unless this batch holds a new best,
+        // and then (before lo_start) the bound is conservative and no record skip runs.
         const uint32_t it_next = it + B;
         const uint32_t Bn = (it_next < max_total && it_next != lo_start)
                                 ? batch_size(it_next, grow(it_next))
                                 : 0;
-        if (Bn > 0) X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(cur ^ 1));
+        if (Bn > 0) {
+            slot_free(cur ^ 1);
+            if (early_cont_) {
+                Batch *gn = &gen[cur ^ 1];
+                const double bound = best_min_score;
+                const bool cut_next = it_next >= lo_start;
+                const BatchBufs *prev = it >= lo_start ? &Q : nullptr; // this batch can publish a record
+                X_.sampler->start(rs_, gn, Bn, cur ^ 1, slot_ptr(cur ^ 1), [this, gn, bound, cut_next, prev] {
+                    MP_HIP(hipSetDevice(X_.device));
+                    launch_batch(*gn, bound, cut_next, prev);
+                });
+            } else {
+                X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(cur ^ 1));
+            }
+        }
         auto tw = Clock::now();
-        MP_HIP(hipStreamSynchronize(X_.stream));
+        MP_HIP(hipEventSynchronize(Q.ev_done));
         S->seconds_gpu_wait += secs(tw);
         batch_s_ = 0.5 * batch_s_ + 0.5 * secs(t_batch);
         S->num_batches++;
         if (prof) {
             float ms_solve = 0.f, ms_score = 0.f;
-            MP_HIP(hipEventElapsedTime(&ms_solve, X_.ev[0], X_.ev[1]));
-            MP_HIP(hipEventElapsedTime(&ms_score, X_.ev[1], X_.ev[2]));
+            MP_HIP(hipEventElapsedTime(&ms_solve, Q.ev[0], Q.ev[1]));
+            MP_HIP(hipEventElapsedTime(&ms_score, Q.ev[1], Q.ev[2]));
             uint64_t h = 0, trips = 0, scored = 0;
             for (uint32_t q = 0; q < B; ++q) {
                 // (record-skipped iterations report their partial trips negated)
-                h += (uint64_t)X_.h_res[q].count;
-                trips += (uint64_t)std::abs(X_.h_work[q]);
-                if (X_.h_work[q] > 0) scored += (uint64_t)X_.h_res[q].count;
+                h += (uint64_t)Q.h_res[q].count;
+                trips += (uint64_t)std::abs(Q.h_work[q]);
+                if (Q.h_work[q] > 0) scored += (uint64_t)Q.h_res[q].count;
             }
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.model_trips += trips;
@@ -1360,7 +1438,7 @@ void Run::run(Model *best, Stats *S) {
             const uint32_t iter = it + j;
             const int st = g.types[j];
             S->num_iterations_per_solver[st] += 1;
-            const int nm = X_.h_res[j].count;
+            const int nm = Q.h_res[j].count;
             S->num_hypotheses += (uint64_t)nm;
             if (count_dump_) {
                 const int *smp = slot_ptr(g.slot) + 8 * (size_t)j;
@@ -1373,8 +1451,8 @@ void Run::run(Model *best, Stats *S) {
                 // The device sums screen; the decision is taken on reference-order sums
                 // (exact_score) -- see tie_margin.  `maybe`: the iteration could hold a new
                 // best; `certain`: it does, and its best model is unambiguous.
-                const double bl = X_.h_res[j].best;
-                const int raw = X_.h_res[j].slot;
+                const double bl = Q.h_res[j].best;
+                const int raw = Q.h_res[j].slot;
                 const bool maybe = best_min_score == kMax ? bl < kMax : bl < best_min_score + tie_;
                 if (maybe || iter == lo_start) {
                     bool new_best = false;
@@ -1383,10 +1461,10 @@ void Run::run(Model *best, Stats *S) {
                         Model m;
                         double e = kMax;
                         if (certain && !(raw & kSlotAmbiguous)) {
-                            m = fetch_model((int)j, raw & kSlotMask);
+                            m = fetch_model(Q, (int)j);
                             e = exact_score(m);
                         } else {
-                            resolve_tie(j, &m, &e);
+                            resolve_tie(Q, j, &m, &e);
                         }
                         if (e < best_min_score) {
                             new_best = true;
@@ -1417,6 +1495,7 @@ void Run::run(Model *best, Stats *S) {
                                 from.sel = sel_end;
                                 const uint32_t bc = grow(at);
                                 const int slot = cur ^ 1;
+                                slot_free(slot); // (an early continuation's samples are on the device)
                                 Batch *gs = &gen[slot];
                                 // LO leaves best_min_model_score alone (src/hybrid_ransac.h:149-155)
                                 const double bound = best_min_score;
@@ -1459,7 +1538,10 @@ void Run::run(Model *best, Stats *S) {
                 auto t0 = Clock::now();
                 have_next = X_.sampler->finish(&rs_);
                 sample_s_ += secs(t0);
-                if (have_next) cur ^= 1;
+                if (have_next) {
+                    cur ^= 1;
+                    launched = early_cont_; // (the sampler launched it once drawn)
+                }
             }
             // (otherwise rs_ stands at the end of this batch)
         } else if (spec) {
@@ -1641,6 +1723,7 @@ void debug_score_batch(const PairInput &in, const RansacOptions &opts, const Est
     X.ensure(in.n, nb, maxm);
     PairData D;
     upload_pair(X, P, &D);
+    BatchBufs &Q = X.bb[0];
     std::vector<ScoreRec> recs((size_t)nb * maxm);
     std::vector<Model> ms((size_t)nb * maxm);
     std::memset(ms.data(), 0, sizeof(Model) * ms.size());
@@ -1654,23 +1737,23 @@ void debug_score_batch(const PairInput &in, const RansacOptions &opts, const Est
     for (int t = 0; t < 3; ++t) M += P.C.thr[t] * std::fabs(P.C.w[t]);
     const double tie = 4e-12 * std::max<int64_t>(in.n, 64) * M;
     if (tie_out) *tie_out = tie;
-    MP_HIP(hipMemcpyAsync(X.d_recs, recs.data(), sizeof(ScoreRec) * recs.size(), hipMemcpyHostToDevice, X.stream));
-    MP_HIP(hipMemcpyAsync(X.d_models, ms.data(), sizeof(Model) * ms.size(), hipMemcpyHostToDevice, X.stream));
-    MP_HIP(hipMemcpyAsync(X.d_counts, counts, sizeof(int) * nb, hipMemcpyHostToDevice, X.stream));
-    std::memset(X.h_recmodel, 0, sizeof(Model) * nb);
+    MP_HIP(hipMemcpyAsync(Q.d_recs, recs.data(), sizeof(ScoreRec) * recs.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemcpyAsync(Q.d_models, ms.data(), sizeof(Model) * ms.size(), hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemcpyAsync(Q.d_counts, counts, sizeof(int) * nb, hipMemcpyHostToDevice, X.stream));
+    std::memset(Q.h_recmodel, 0, sizeof(Model) * nb);
     const bool exit = (flags & 1) != 0, skip = (flags & 2) != 0;
     const unsigned epoch_hi = ~(++X.epoch);
-    MP_HIP(launch_score_batch(X.stream, D, P.C, X.d_recs, X.d_counts, nb, maxm, X.d_scores, X.d_res,
-                              exit ? best : DBL_MAX, tie, nullptr, skip ? X.d_recword : nullptr, epoch_hi, X.d_models,
-                              X.d_recmodel));
+    MP_HIP(launch_score_batch(X.stream, D, P.C, Q.d_recs, Q.d_counts, nb, maxm, Q.d_scores, Q.d_res,
+                              exit ? best : DBL_MAX, tie, nullptr, skip ? X.d_recword : nullptr, epoch_hi, Q.d_models,
+                              Q.d_recmodel));
     std::vector<IterResult> res(nb);
-    MP_HIP(hipMemcpyAsync(res.data(), X.d_res, sizeof(IterResult) * nb, hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(res.data(), Q.d_res, sizeof(IterResult) * nb, hipMemcpyDeviceToHost, X.stream));
     MP_HIP(hipStreamSynchronize(X.stream));
     for (int b = 0; b < nb; ++b) {
         res_best[b] = res[b].best;
         res_slot[b] = res[b].slot;
     }
-    if (rec_models) std::memcpy(rec_models, X.h_recmodel, sizeof(Model) * nb);
+    if (rec_models) std::memcpy(rec_models, Q.h_recmodel, sizeof(Model) * nb);
 }
 
 namespace {

@@ -68,6 +68,16 @@ struct PairConst {
 struct PairData {
     const double *x0u, *x0v, *x1u, *x1v, *d0, *d1; // pixels (CAL) or normalized pixels (SF/TF)
     const double *r0, *r1;                          // 1/|K^-1 x| (CAL bearings), else unused
+    // Batch gate (nullable): the kernels of a batch launched before the previous batch's
+    // results were read leave at once when that batch published a record (score_batch's
+    // record word holds ~its epoch, gate_hi), i.e. when the host is bound to run LO and
+    // discard this batch (engine.cpp, early continuation)
+    const unsigned long long *gate = nullptr;
+    unsigned gate_hi = 0;
+};
+struct BatchGate {
+    const unsigned long long *word = nullptr;
+    unsigned hi = 0;
 };
 
 // Per-iteration outcome of a batch (score_batch): the iteration's best score

@@ -69,6 +69,7 @@ constexpr int kPenStride = 300;
 static_assert(kPenStride == kPtPenStride, "the engine sizes the pencil workspace with kPtPenStride (kernels.h)");
 __global__ void __launch_bounds__(64) pt_pencil6_kernel(PairData D, const int *list, int nlist, const int *samples,
                                                         double *cand, int cand_stride, double *pen) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     __shared__ double shN[kGrpPerWg][27];
     const int g = threadIdx.x / kGrp, r = threadIdx.x % kGrp;
     const int idx = blockIdx.x * kGrpPerWg + g;
@@ -148,7 +149,8 @@ namespace {
 // lanes per wave, fewer rounds.  A lane's arithmetic does not depend on the others
 // (its updates are exact no-ops while it waits), so the roots are the same for any spw.
 __global__ void __launch_bounds__(64) pt_eig6_reg_kernel(double *pen, int nlist, int spw, double *cand, int *ncand,
-                                                         int cand_stride) {
+                                                         int cand_stride, BatchGate gate) {
+    if (batch_cancelled(gate.word, gate.hi)) return;
     const int idx = blockIdx.x * spw + threadIdx.x;
     const bool valid = (int)threadIdx.x < spw && idx < nlist;
     const int sidx = valid ? idx : nlist - 1;

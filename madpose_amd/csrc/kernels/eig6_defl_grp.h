@@ -103,7 +103,8 @@ __device__ __forceinline__ void e6g_null(const double (&g)[NC], unsigned cols, i
     });
 }
 
-__global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist) {
+__global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist, BatchGate gate) {
+    if (batch_cancelled(gate.word, gate.hi)) return;
     const int i = threadIdx.x & 15;
     const int idx = blockIdx.x * 4 + (threadIdx.x >> 4);
     const bool valid = idx < nlist;

@@ -159,6 +159,7 @@ struct Group5Shared {
 __global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                              const int *samples, double *cand, int *ncand,
                                                              int cand_stride) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     __shared__ Group5Shared sh;
     const int g = threadIdx.x / kG5, r = threadIdx.x % kG5;
     const int idx = blockIdx.x * kS5 + g;

@@ -44,6 +44,7 @@ template <int G>
 __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                             const double *cand, const int *ncand, const int *samples,
                                                             Model *slots, int *valid) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     static_assert(G == 8 || G == 32, "8 or 32 lanes per (root, sample)");
     constexpr int K = 7;
     const int lane = threadIdx.x % kTail;
@@ -112,6 +113,7 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
 __global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                             const double *cand, const int *ncand, const int *samples,
                                                             Model *slots, int *valid) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     constexpr int K = 5, kRoots = 10, kPoses = 2;
     const int lane = threadIdx.x % kTail;
     const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kTail);
@@ -186,6 +188,7 @@ __device__ inline int gsum16(int v) {
 __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                             const double *cand, const int *ncand, const int *samples,
                                                             Model *slots, int *valid) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     constexpr int K = 6, kRoots = 15, kPoses = 2;
     __shared__ Tail6Shared sh;
     const int g = threadIdx.x / kGrp, r = threadIdx.x % kGrp;

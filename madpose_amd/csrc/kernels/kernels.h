@@ -8,6 +8,14 @@ namespace mp {
 
 constexpr int kSampleStride = 8; // sample indices per iteration slot (max minimal sample = 7)
 
+// The batch gate of PairData: true when the record word holds the previous batch's
+// epoch, i.e. that batch published a record (and the host will discard this one).
+// Every lane of a workgroup reads the same word, so the exit is uniform.
+__device__ inline bool batch_cancelled(const unsigned long long *word, unsigned hi) {
+    return word != nullptr &&
+           (unsigned)(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == hi;
+}
+
 // r0/r1 = 1 / |K^-1 x| for the calibrated bearings
 hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1);
 

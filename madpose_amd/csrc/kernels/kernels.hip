@@ -107,6 +107,7 @@ template <int V, bool ALT>
 __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                       const int *samples, Model *models, ScoreRec *recs, int *counts,
                                                       int maxm) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= nlist) return;
     const int b = list[idx];
@@ -217,6 +218,7 @@ template <int V>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kCal ? 3 : 2))) md_solve_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                             const int *samples, Model *models, ScoreRec *recs,
                                                             int *counts, int maxm) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     using G = MdGroup<V>;
     constexpr int NR = G::NR, K = G::K;
     __shared__ GroupSturm<NR> st[kGrpPerWg];
@@ -321,6 +323,7 @@ template <int V, int R>
 __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                       const int *samples, Model *models, ScoreRec *recs, int *counts,
                                                       int maxm) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     using Sys = typename MdxSys<V>::S;
     constexpr int K = MdxSys<V>::K, NR = Sys::NR;
     static_assert(R == 1 || (R == 4 && NR == 4), "one lane per sample, or one lane per root of a quartic");
@@ -438,6 +441,7 @@ template <> struct PtTraits<kTF> {
 // (PoseLib relpose_7pt: cubic by multilinear expansion, Sturm roots)
 __global__ void __launch_bounds__(64) pt_roots7_kernel(PairData D, const int *list, int nlist, const int *samples,
                                                        double *cand, int *ncand) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= nlist) return;
     const int *s = samples + (size_t)list[idx] * kSampleStride;
@@ -465,7 +469,8 @@ __global__ void __launch_bounds__(64) pt_roots7_kernel(PairData D, const int *li
 template <int V>
 __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *list, int nlist, const int *ncand,
                                                         const Model *slots, const int *valid, Model *models,
-                                                        ScoreRec *recs, int *counts, int maxm) {
+                                                        ScoreRec *recs, int *counts, int maxm, BatchGate gate) {
+    if (batch_cancelled(gate.word, gate.hi)) return;
     using T = PtTraits<V>;
     constexpr int kSlots = T::kPosesPerRoot * T::kRoots;
     constexpr int G = kSlots <= 4 ? 4 : 32;
@@ -557,6 +562,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                                                              const ScoreRec *__restrict__ recs,
                                                              const int *__restrict__ counts, double *scores,
                                                              IterResult *res, ScoreBound sb) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     const int b = blockIdx.x;
     const int nm = counts[b];
     if (nm == 0) {
@@ -992,9 +998,10 @@ static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int
                           double *cand, int *ncand, double *pen) {
     pt_pencil6_kernel<<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, list, nlist, samples, cand, kCandStride,
                                                                          pen);
-    pt_defl6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist);
+    const BatchGate gate{D.gate, D.gate_hi};
+    pt_defl6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist, gate);
     const int spw = eig_spw(nlist);
-    pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride);
+    pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride, gate);
 }
 
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
@@ -1026,7 +1033,7 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                                                                                 samples, W.slots, W.valid);
         constexpr int kCompactG = PtTraits<v>::kPosesPerRoot * PtTraits<v>::kRoots <= 4 ? 4 : 32;
         pt_compact_kernel<v><<<(int)(((size_t)nlist * kCompactG + 63) / 64), 64, 0, s>>>(
-            C, list, nlist, W.ncand, W.slots, W.valid, models, recs, counts, maxm);
+            C, list, nlist, W.ncand, W.slots, W.valid, models, recs, counts, maxm, BatchGate{D.gate, D.gate_hi});
         return hipGetLastError();
     });
 }

@@ -111,7 +111,7 @@ int main(int argc, char **argv) {
         CHECK(hipEventRecord(ev[5]));
         pt_defl6_kernel<<<ns, 64>>>(d_pen2, true); // (the Hessenberg form for the lockstep kernel)
         CHECK(hipEventRecord(ev[6]));
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c4, d_n4, kCandStride);
+        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c4, d_n4, kCandStride, BatchGate{});
         CHECK(hipEventRecord(ev[7]));
         CHECK(hipEventSynchronize(ev[7]));
         if (timed)
@@ -221,7 +221,7 @@ int main(int argc, char **argv) {
             float t = 0.f, tt = 0.f;
             for (int r = 0; r < 4; ++r) {
                 CHECK(hipEventRecord(ev[0]));
-                pt_eig6_reg_kernel<<<(ns + spw - 1) / spw, 64>>>(d_pen2, ns, spw, d_c3, d_n3, kCandStride);
+                pt_eig6_reg_kernel<<<(ns + spw - 1) / spw, 64>>>(d_pen2, ns, spw, d_c3, d_n3, kCandStride, BatchGate{});
                 CHECK(hipEventRecord(ev[1]));
                 CHECK(hipEventSynchronize(ev[1]));
                 CHECK(hipEventElapsedTime(&t, ev[0], ev[1]));
@@ -255,7 +255,7 @@ int main(int argc, char **argv) {
             CHECK(hipEventRecord(ev[0]));
             pt_defl6_kernel<<<ns, 64>>>(d_pen2, true);
             CHECK(hipEventRecord(ev[1]));
-            pt_defl6_grp_kernel<<<(ns + 3) / 4, 64>>>(d_pen3, ns);
+            pt_defl6_grp_kernel<<<(ns + 3) / 4, 64>>>(d_pen3, ns, BatchGate{});
             CHECK(hipEventRecord(ev[2]));
             CHECK(hipEventSynchronize(ev[2]));
             CHECK(hipEventElapsedTime(&t, ev[0], ev[1]));
@@ -263,8 +263,8 @@ int main(int argc, char **argv) {
             CHECK(hipEventElapsedTime(&t, ev[1], ev[2]));
             if (r > 0) tg += t / 3;
         }
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c3, d_n3, kCandStride);
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen3, ns, 64, d_c4, d_n4, kCandStride);
+        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c3, d_n3, kCandStride, BatchGate{});
+        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen3, ns, 64, d_c4, d_n4, kCandStride, BatchGate{});
         CHECK(hipDeviceSynchronize());
         std::vector<int> na(ns), nb(ns);
         std::vector<double> ca((size_t)ns * kCandStride), cb((size_t)ns * kCandStride);
