@@ -148,11 +148,14 @@ namespace {
 // spreads the samples over about one wave per SIMD (kernels.hip launch_sf_eig): fewer
 // lanes per wave, fewer rounds.  A lane's arithmetic does not depend on the others
 // (its updates are exact no-ops while it waits), so the roots are the same for any spw.
+// U (spw == 1): every lane runs the wave's one sample, which makes the QR's window
+// wave-uniform (e15_hqr<true>: scalar branches instead of select chains); lane 0 writes.
+template <bool U>
 __global__ void __launch_bounds__(64) pt_eig6_reg_kernel(double *pen, int nlist, int spw, double *cand, int *ncand,
                                                          int cand_stride, BatchGate gate) {
     if (batch_cancelled(gate.word, gate.hi)) return;
-    const int idx = blockIdx.x * spw + threadIdx.x;
-    const bool valid = (int)threadIdx.x < spw && idx < nlist;
+    const int idx = U ? (int)blockIdx.x : (int)(blockIdx.x * spw + threadIdx.x);
+    const bool valid = (U || (int)threadIdx.x < spw) && idx < nlist;
     const int sidx = valid ? idx : nlist - 1;
     double *P = pen + (size_t)sidx * kPenStride;
     const bool active = valid && P[225] != 0.0;
@@ -161,11 +164,11 @@ __global__ void __launch_bounds__(64) pt_eig6_reg_kernel(double *pen, int nlist,
 #ifdef MP_EIG6_PROFILE
     const unsigned long long t_hqr0 = wall_clock64();
 #endif
-    const bool conv = e15_hqr(P, active, wr, wi);
+    const bool conv = e15_hqr<U>(P, active, wr, wi);
 #ifdef MP_EIG6_PROFILE
     if (threadIdx.x == 0) atomicAdd(&e6_prof[6], wall_clock64() - t_hqr0);
 #endif
-    if (!valid) return;
+    if (!valid || (U && threadIdx.x != 0)) return;
     int cnt = 0;
     if (conv) {
         double *out = cand + (size_t)idx * cand_stride + 27;

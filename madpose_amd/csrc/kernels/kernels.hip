@@ -326,7 +326,8 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
     if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     using Sys = typename MdxSys<V>::S;
     constexpr int K = MdxSys<V>::K, NR = Sys::NR;
-    static_assert(R == 1 || (R == 4 && NR == 4), "one lane per sample, or one lane per root of a quartic");
+    static_assert(R == 1 || R == 2 || R == 4 || R == 8, "1, 2, 4 or 8 lanes per sample");
+    static_assert(NR % R == 0, "a sample's lanes take its roots in equal turns");
     __shared__ double scr[R == 1 ? NR * 64 : 1];
     const int g = threadIdx.x / R, r = threadIdx.x % R;
     const int idx = blockIdx.x * (64 / R) + g;
@@ -371,25 +372,29 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
         Sys sys;
         double roots[NR];
         const int nr = sys.setup(x, y, dx, dy, roots);
-        double root = 0.0;
-#pragma unroll
-        for (int q = 0; q < NR; ++q)
-            if (q == r) root = opaque(roots[q]);
-        Model m;
-        bool keep = false;
-        if (active && r < nr) {
-            double sol[6];
-            keep = sys.root(root, sol) && accept(sol, m);
-        }
-        const unsigned long long ball = __ballot(keep);
         const int g0 = (threadIdx.x & 63) & ~(R - 1);
-        const unsigned long long mine = (ball >> g0) & ((1ull << R) - 1);
-        const int pos = __popcll(mine & ((1ull << r) - 1));
-        if (keep && pos < maxm) put_model(C, m, b, pos, maxm, models, recs);
-        if (active && r == 0) {
-            const int n = __popcll(mine);
-            counts[b] = n < maxm ? n : maxm;
+        int n = 0; // the sample's accepted models so far (root order: turn j, then lane r)
+#pragma unroll
+        for (int j = 0; j < NR / R; ++j) {
+            const int q = j * R + r;
+            double root = 0.0;
+#pragma unroll
+            for (int c = 0; c < R; ++c)
+                if (c == r) root = opaque(roots[j * R + c]);
+            Model m;
+            bool keep = false;
+            if (active && q < nr) {
+                double sol[6];
+                keep = sys.root(root, sol) && accept(sol, m);
+            }
+            const unsigned long long ball = __ballot(keep);
+            const unsigned long long mine = (ball >> g0) & ((1ull << R) - 1);
+            const int pos = n + __popcll(mine & ((1ull << r) - 1));
+            if (keep && pos < maxm) put_model(C, m, b, pos, maxm, models, recs);
+            n += __popcll(mine);
+            if (!__any(active && (j + 1) * R < nr)) break; // (uniform) no sample of the wave has more roots
         }
+        if (active && r == 0) counts[b] = n < maxm ? n : maxm;
     }
 }
 
@@ -956,7 +961,22 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
         const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
         if constexpr (v == kSF) {
             if (plain) {
-                md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+                static const int rps = [] { // lanes per sample (MADPOSE_MDX_R, A/B)
+                    const char *e = std::getenv("MADPOSE_MDX_R");
+                    const int r = e ? std::atoi(e) : 1;
+                    return r == 2 || r == 4 || r == 8 ? r : 1;
+                }();
+                if (rps == 1)
+                    md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+                else if (rps == 2)
+                    md_exact_kernel<v, 2><<<(nlist + 31) / 32, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                           counts, maxm);
+                else if (rps == 4)
+                    md_exact_kernel<v, 4><<<(nlist + 15) / 16, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                           counts, maxm);
+                else
+                    md_exact_kernel<v, 8><<<(nlist + 7) / 8, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                         counts, maxm);
                 return hipGetLastError();
             }
         } else if constexpr (v == kTF) {
@@ -1001,7 +1021,11 @@ static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int
     const BatchGate gate{D.gate, D.gate_hi};
     pt_defl6_grp_kernel<<<(nlist + 3) / 4, 64, 0, s>>>(pen, nlist, gate);
     const int spw = eig_spw(nlist);
-    pt_eig6_reg_kernel<<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride, gate);
+    if (spw == 1)
+        pt_eig6_reg_kernel<true><<<nlist, 64, 0, s>>>(pen, nlist, 1, cand, ncand, kCandStride, gate);
+    else
+        pt_eig6_reg_kernel<false><<<(nlist + spw - 1) / spw, 64, 0, s>>>(pen, nlist, spw, cand, ncand, kCandStride,
+                                                                         gate);
 }
 
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,

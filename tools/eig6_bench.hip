@@ -111,7 +111,7 @@ int main(int argc, char **argv) {
         CHECK(hipEventRecord(ev[5]));
         pt_defl6_kernel<<<ns, 64>>>(d_pen2, true); // (the Hessenberg form for the lockstep kernel)
         CHECK(hipEventRecord(ev[6]));
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c4, d_n4, kCandStride, BatchGate{});
+        pt_eig6_reg_kernel<false><<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c4, d_n4, kCandStride, BatchGate{});
         CHECK(hipEventRecord(ev[7]));
         CHECK(hipEventSynchronize(ev[7]));
         if (timed)
@@ -217,11 +217,14 @@ int main(int argc, char **argv) {
             std::printf("group QR (4 samples per wave, %d waves): %.1f us, %ld of %d root sets bit-identical to the lane kernel\n",
                         (ns + 3) / 4, 1e3 * tt, same, ns);
         }
-        for (int spw : {64, 16, 2, eig_spw(ns)}) {
+        for (int spw : {64, 16, 8, 2, 1}) {
             float t = 0.f, tt = 0.f;
             for (int r = 0; r < 4; ++r) {
                 CHECK(hipEventRecord(ev[0]));
-                pt_eig6_reg_kernel<<<(ns + spw - 1) / spw, 64>>>(d_pen2, ns, spw, d_c3, d_n3, kCandStride, BatchGate{});
+                if (spw == 1)
+                    pt_eig6_reg_kernel<true><<<ns, 64>>>(d_pen2, ns, 1, d_c3, d_n3, kCandStride, BatchGate{});
+                else
+                    pt_eig6_reg_kernel<false><<<(ns + spw - 1) / spw, 64>>>(d_pen2, ns, spw, d_c3, d_n3, kCandStride, BatchGate{});
                 CHECK(hipEventRecord(ev[1]));
                 CHECK(hipEventSynchronize(ev[1]));
                 CHECK(hipEventElapsedTime(&t, ev[0], ev[1]));
@@ -263,8 +266,8 @@ int main(int argc, char **argv) {
             CHECK(hipEventElapsedTime(&t, ev[1], ev[2]));
             if (r > 0) tg += t / 3;
         }
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c3, d_n3, kCandStride, BatchGate{});
-        pt_eig6_reg_kernel<<<(ns + 63) / 64, 64>>>(d_pen3, ns, 64, d_c4, d_n4, kCandStride, BatchGate{});
+        pt_eig6_reg_kernel<false><<<(ns + 63) / 64, 64>>>(d_pen2, ns, 64, d_c3, d_n3, kCandStride, BatchGate{});
+        pt_eig6_reg_kernel<false><<<(ns + 63) / 64, 64>>>(d_pen3, ns, 64, d_c4, d_n4, kCandStride, BatchGate{});
         CHECK(hipDeviceSynchronize());
         std::vector<int> na(ns), nb(ns);
         std::vector<double> ca((size_t)ns * kCandStride), cb((size_t)ns * kCandStride);
