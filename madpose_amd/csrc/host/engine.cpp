@@ -423,6 +423,14 @@ std::atomic<bool> g_prof_on{false};
 std::mutex g_prof_mu;
 KernelProfile g_prof;
 
+// estimators running on each device (leases held): the early continuation is
+// speculative GPU work that pays only while one estimator has the device to itself
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_active_runs[kMaxDevices];
+int active_runs(int device) {
+    return device >= 0 && device < kMaxDevices ? g_active_runs[device].load(std::memory_order_relaxed) : 1;
+}
+
 struct CtxLease {
     DeviceCtx *c = nullptr;
     explicit CtxLease(int device) {
@@ -455,8 +463,10 @@ struct CtxLease {
             }
         }
         MP_HIP(hipSetDevice(device));
+        if (device < kMaxDevices) g_active_runs[device].fetch_add(1, std::memory_order_relaxed);
     }
     ~CtxLease() {
+        if (c->device < kMaxDevices) g_active_runs[c->device].fetch_sub(1, std::memory_order_relaxed);
         std::lock_guard<std::mutex> lk(g_pool_mu);
         g_pool.push_back(c);
     }
@@ -1146,11 +1156,15 @@ class Run {
     bool batch_prof_[2] = {false, false};
     double launch_s_ = 0.0; // main-thread time in launch_batch (MADPOSE_LO_TIMING)
     // early continuation (MADPOSE_EARLY_CONT=0: launch the continuation after reading
-    // the batch, as before)
-    const bool early_cont_ = [] {
+    // the batch, as before; =1: also with other estimators on the device).  By default
+    // only while this estimator is alone on its device: with 8 shared-focal pairs in
+    // flight the discarded continuations took GPU time from the other pairs (ScanNet
+    // stand-in 747 -> 1064 pairs/s without them, profiles/r04/scab/)
+    const int early_mode_ = [] {
         const char *e = std::getenv("MADPOSE_EARLY_CONT");
-        return !(e && e[0] == '0');
+        return e ? (e[0] == '0' ? 0 : 2) : 1;
     }();
+    bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
     int launch_n_ = 0;
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
     // best runs LO and cuts it; score_batch then skips the iterations behind a record.
@@ -1387,9 +1401,10 @@ void Run::run(Model *best, Stats *S) {
         const uint32_t Bn = (it_next < max_total && it_next != lo_start)
                                 ? batch_size(it_next, grow(it_next))
                                 : 0;
+        const bool early = Bn > 0 && early_now();
         if (Bn > 0) {
             slot_free(cur ^ 1);
-            if (early_cont_) {
+            if (early) {
                 Batch *gn = &gen[cur ^ 1];
                 const double bound = best_min_score;
                 const bool cut_next = it_next >= lo_start;
@@ -1540,7 +1555,7 @@ void Run::run(Model *best, Stats *S) {
                 sample_s_ += secs(t0);
                 if (have_next) {
                     cur ^= 1;
-                    launched = early_cont_; // (the sampler launched it once drawn)
+                    launched = early; // (the sampler launched it once drawn)
                 }
             }
             // (otherwise rs_ stands at the end of this batch)

@@ -291,15 +291,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kC
 
 // The MD solvers with the oracle's arithmetic (mp_md_exact.h: setup() = system +
 // sorted real roots, root() = one root's polish and filters), two layouts:
-//  R = 1: one sample per lane, its roots in turn (shared focal: 8 roots behind an 8 x 8
-//         QR; the kernel is issue-bound there and full waves pay best -- 64 / 16 / 8 / 4
-//         samples per wave gave sf 12.9 / 13.4 / 15.0 / 16.3 ms per pair, profiles/r04/mdx/);
-//  R = 4: four lanes per sample (16 per wave), every lane of a group runs the sample's
-//         setup (the same doubles in each) and lane r the r-th root, the accepted
-//         models compacted in root order by a ballot -- for the two-focal quartic,
-//         whose roots' polish + pose dominate a lane's serial chain (165 -> 91 us per
-//         tf launch, under the 206 us point chain; tf 13.4 -> 12.8 ms per pair,
-//         profiles/r04/mdx4/).
+//  R = 1: one sample per lane, its roots in turn (the kernel is issue-bound, and full
+//         waves paid best: 64 / 16 / 8 / 4 samples per wave gave sf 12.9 / 13.4 / 15.0 /
+//         16.3 ms per pair, profiles/r04/mdx/);
+//  R > 1: R lanes per sample (64 / R per wave), every lane of a group runs the sample's
+//         setup (the same doubles in each) and lane r the roots r, r + R, ..., the
+//         accepted models compacted in root order by a ballot per turn -- R = 4 for the
+//         two-focal quartic, whose roots' polish + pose dominate a lane's serial chain
+//         (165 -> 91 us per tf launch, under the 206 us point chain; tf 13.4 -> 12.8 ms
+//         per pair, profiles/r04/mdx4/), R = 2 for the shared-focal octic (below).
 // Accepted models go to their slots in root order, as md_solve_group's.  The
 // calibrated MD solver keeps md_solve_group (57 us): its exact form, 152 us lane per
 // sample and 106 us lane per root, outlasts the 99 us calibrated point chain (cal
@@ -961,10 +961,14 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
         const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
         if constexpr (v == kSF) {
             if (plain) {
-                static const int rps = [] { // lanes per sample (MADPOSE_MDX_R, A/B)
+                // lanes per sample (MADPOSE_MDX_R, A/B): 2 -- the kernel 267 -> 212 us per
+                // launch, sf gpu_solve 8.17 -> 7.74 ms per pair; 4 and 8 shorten it further
+                // (190 / 230 us) but their extra waves slow the point chain beside it
+                // (pt_defl6_grp 80 -> 105 / 124 us), profiles/r04/mdxr/
+                static const int rps = [] {
                     const char *e = std::getenv("MADPOSE_MDX_R");
-                    const int r = e ? std::atoi(e) : 1;
-                    return r == 2 || r == 4 || r == 8 ? r : 1;
+                    const int r = e ? std::atoi(e) : 2;
+                    return r == 1 || r == 4 || r == 8 ? r : 2;
                 }();
                 if (rps == 1)
                     md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);

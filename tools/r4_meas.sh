@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 measurement set on the current tree: the GPU suite, smoke(), the default
 # bench line (cal, CPU baselines), sf / tf / ScanNet lines, rocprofv3 kernel statistics
-# of short cal and sf runs.  Output under gpurun_out/$1 (default r4m).
+# of short cal, sf and tf runs.  Output under gpurun_out/$1 (default r4m).
 out=gpurun_out/${1:-r4m}
 mkdir -p "$out"
 export TMPDIR=/tmp
@@ -24,4 +24,6 @@ step 240 prof_cal.log rocprofv3 --kernel-trace --stats -d "$out/prof_cal" -o cal
 step 60 cal_summary.log python tools/prof_summary.py "$out/prof_cal" "$out/cal_kernel_stats.csv"
 step 240 prof_sf.log rocprofv3 --kernel-trace --stats -d "$out/prof_sf" -o sf -- python3 bench.py --workload sf --cpu-budget 0 --in-flight 1
 step 60 sf_summary.log python tools/prof_summary.py "$out/prof_sf" "$out/sf_kernel_stats.csv"
+step 240 prof_tf.log rocprofv3 --kernel-trace --stats -d "$out/prof_tf" -o tf -- python3 bench.py --workload tf --cpu-budget 0 --in-flight 1
+step 60 tf_summary.log python tools/prof_summary.py "$out/prof_tf" "$out/tf_kernel_stats.csv"
 exit 0
