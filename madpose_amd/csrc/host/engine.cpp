@@ -68,13 +68,16 @@ double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::n
 const double kMax = DBL_MAX;
 
 // Minimal-sample batches and their drawing: batch_draw.h.  MADPOSE_SAMPLER_TWO_PASS=0
-// keeps the draw-by-draw loop for hybrid batches too (A/B; identical draws).
-bool sampler_two_pass() {
-    static const bool on = [] {
+// keeps the draw-by-draw loop for hybrid batches too, MADPOSE_SAMPLER_SIMD=0 the scalar
+// two passes (A/B; identical draws).
+int sampler_mode() {
+    static const int mode = [] {
         const char *e = std::getenv("MADPOSE_SAMPLER_TWO_PASS");
-        return !(e && e[0] == '0');
+        if (e && e[0] == '0') return 0;
+        const char *v = std::getenv("MADPOSE_SAMPLER_SIMD");
+        return v && v[0] == '0' ? 1 : 2;
     }();
-    return on;
+    return mode;
 }
 
 // Background sampler: draws the next speculative batch while the current one is on
@@ -134,7 +137,7 @@ class Sampler {
             if (quit_) return;
             seen = gen_;
             lk.unlock();
-            const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, &abort_, sampler_two_pass());
+            const bool ok = draw_batch(rs_, *g_, B_, slot_, smp_, &abort_, sampler_mode());
             std::exception_ptr err;
             if (ok && after_) {
                 try {
@@ -1136,7 +1139,7 @@ class Run {
     int *slot_ptr(int slot) const { return X_.h_samples + (size_t)slot * 9 * max_batch_; }
     void generate(Batch &g, uint32_t B, int slot) {
         auto t0 = Clock::now();
-        draw_batch(rs_, g, B, slot, slot_ptr(slot), nullptr, sampler_two_pass());
+        draw_batch(rs_, g, B, slot, slot_ptr(slot), nullptr, sampler_mode());
         sample_s_ += secs(t0);
     }
     // both streams to the end of iteration j of batch g

@@ -11,6 +11,9 @@
 #pragma once
 #include <cmath>
 #include <cstdint>
+#if defined(__x86_64__) && (defined(__clang__) || defined(__GNUC__))
+#include <immintrin.h>
+#endif
 
 namespace mp {
 
@@ -39,6 +42,13 @@ class Mt19937 {
         if (idx_ >= 624) twist();
         return idx_ + k <= 624 ? out_ + idx_ : nullptr;
     }
+    // the buffered outputs from the current position to the end of the block (at
+    // least one: an exhausted block is refilled first); *n = how many
+    const uint32_t *rest(int *n) {
+        if (idx_ >= 624) twist();
+        *n = 624 - idx_;
+        return out_ + idx_;
+    }
     void skip(int k) {
         idx_ += k;
         draws_ += (uint64_t)k;
@@ -52,6 +62,13 @@ class Mt19937 {
         return far ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
     }
     void twist() {
+#if defined(__x86_64__) && (defined(__clang__) || defined(__GNUC__))
+        static const bool avx512 = __builtin_cpu_supports("avx512f");
+        if (avx512) {
+            twist_avx512();
+            return;
+        }
+#endif
         int i = 0;
         for (; i < 624 - 397; ++i) mt_[i] = step(mt_[i], mt_[i + 1], mt_[i + 397]);
         for (; i < 623; ++i) mt_[i] = step(mt_[i], mt_[i + 1], mt_[i + 397 - 624]);
@@ -66,6 +83,39 @@ class Mt19937 {
         }
         idx_ = 0;
     }
+#if defined(__x86_64__) && (defined(__clang__) || defined(__GNUC__))
+    // the same recurrence and tempering, 16 words per AVX-512 vector (integer
+    // operations: the same words); the wrap points as in twist()
+    __attribute__((target("avx512f"))) static inline __m512i step16(__m512i cur, __m512i nxt, __m512i far) {
+        const __m512i y = _mm512_or_si512(_mm512_and_si512(cur, _mm512_set1_epi32((int)0x80000000u)),
+                                          _mm512_and_si512(nxt, _mm512_set1_epi32(0x7fffffff)));
+        const __m512i mag = _mm512_and_si512(_mm512_sub_epi32(_mm512_setzero_si512(),
+                                                              _mm512_and_si512(y, _mm512_set1_epi32(1))),
+                                             _mm512_set1_epi32((int)0x9908b0dfu));
+        return _mm512_xor_si512(_mm512_xor_si512(far, _mm512_srli_epi32(y, 1)), mag);
+    }
+    __attribute__((target("avx512f"))) void twist_avx512() {
+        int i = 0;
+        for (; i + 16 <= 624 - 397; i += 16)
+            _mm512_storeu_si512(mt_ + i, step16(_mm512_loadu_si512(mt_ + i), _mm512_loadu_si512(mt_ + i + 1),
+                                                _mm512_loadu_si512(mt_ + i + 397)));
+        for (; i < 624 - 397; ++i) mt_[i] = step(mt_[i], mt_[i + 1], mt_[i + 397]);
+        for (; i + 16 <= 623; i += 16)
+            _mm512_storeu_si512(mt_ + i, step16(_mm512_loadu_si512(mt_ + i), _mm512_loadu_si512(mt_ + i + 1),
+                                                _mm512_loadu_si512(mt_ + i + 397 - 624)));
+        for (; i < 623; ++i) mt_[i] = step(mt_[i], mt_[i + 1], mt_[i + 397 - 624]);
+        mt_[623] = step(mt_[623], mt_[0], mt_[396]);
+        for (i = 0; i < 624; i += 16) { // 624 = 39 x 16
+            __m512i y = _mm512_loadu_si512(mt_ + i);
+            y = _mm512_xor_si512(y, _mm512_srli_epi32(y, 11));
+            y = _mm512_xor_si512(y, _mm512_and_si512(_mm512_slli_epi32(y, 7), _mm512_set1_epi32((int)0x9d2c5680u)));
+            y = _mm512_xor_si512(y, _mm512_and_si512(_mm512_slli_epi32(y, 15), _mm512_set1_epi32((int)0xefc60000u)));
+            y = _mm512_xor_si512(y, _mm512_srli_epi32(y, 18));
+            _mm512_storeu_si512(out_ + i, y);
+        }
+        idx_ = 0;
+    }
+#endif
     uint32_t mt_[624];
     uint32_t out_[624];
     int idx_;

@@ -2,6 +2,7 @@
 // against the draw-by-draw loop: same solver types, iteration lists, kept sample
 // indices, stream snapshots and end states.  Built and run by tests/test_sampler_cpu.py.
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -17,7 +18,13 @@ static bool same_stream(Mt19937 a, Mt19937 b) {
     return true;
 }
 
-int main() {
+// argv[1]: the mode under test (1 = scalar two passes, 2 = AVX-512 two passes)
+int main(int argc, char **argv) {
+    const int mode = argc > 1 ? std::atoi(argv[1]) : 2;
+    if (mode == 2 && !draw_simd_available()) {
+        std::printf("SKIP no AVX-512 on this host\n");
+        return 0;
+    }
     struct Case {
         int n, a, c;
         double p0, p1;
@@ -45,9 +52,9 @@ int main() {
             std::vector<int> s1(9 * (size_t)B, -1), s2(9 * (size_t)B, -1);
             Batch g1, g2;
             auto t0 = std::chrono::steady_clock::now();
-            draw_batch(r1, g1, B, 0, s1.data(), nullptr, false);
+            draw_batch(r1, g1, B, 0, s1.data(), nullptr, 0);
             auto t1 = std::chrono::steady_clock::now();
-            draw_batch(r2, g2, B, 0, s2.data(), nullptr, true);
+            draw_batch(r2, g2, B, 0, s2.data(), nullptr, mode);
             auto t2 = std::chrono::steady_clock::now();
             t_one += std::chrono::duration<double>(t1 - t0).count();
             t_two += std::chrono::duration<double>(t2 - t1).count();
@@ -63,12 +70,12 @@ int main() {
             }
             ok = ok && std::memcmp(s1.data() + 8 * (size_t)B, s2.data() + 8 * (size_t)B, sizeof(int) * B) == 0;
             if (!ok) {
-                std::printf("MISMATCH n=%d a=%d c=%d seed=%u rep=%d\n", c.n, c.a, c.c, c.seed, rep);
+                std::printf("MISMATCH mode=%d n=%d a=%d c=%d seed=%u rep=%d\n", mode, c.n, c.a, c.c, c.seed, rep);
                 return 1;
             }
         }
     }
-    std::printf("OK %llu iterations: one-pass %.2f ns/it, two-pass %.2f ns/it\n", (unsigned long long)iters,
-                1e9 * t_one / iters, 1e9 * t_two / iters);
+    std::printf("OK mode %d, %llu iterations: one-pass %.2f ns/it, two-pass %.2f ns/it\n", mode,
+                (unsigned long long)iters, 1e9 * t_one / iters, 1e9 * t_two / iters);
     return 0;
 }
