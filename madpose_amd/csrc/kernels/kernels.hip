@@ -961,26 +961,19 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
         const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
         if constexpr (v == kSF) {
             if (plain) {
-                // lanes per sample (MADPOSE_MDX_R, A/B): 2 -- the kernel 267 -> 212 us per
-                // launch, sf gpu_solve 8.17 -> 7.74 ms per pair; 4 and 8 shorten it further
-                // (190 / 230 us) but their extra waves slow the point chain beside it
-                // (pt_defl6_grp 80 -> 105 / 124 us), profiles/r04/mdxr/
-                static const int rps = [] {
+                // two lanes per sample: the kernel 267 -> 212 us per launch, sf gpu_solve
+                // 8.17 -> 7.74 ms per pair; 4 and 8 lanes shortened it further (190 / 230
+                // us) but their extra waves slowed the point chain beside it (pt_defl6_grp
+                // 80 -> 105 / 124 us), profiles/r04/mdxr/ (MADPOSE_MDX_R=1: one lane)
+                static const bool one = [] {
                     const char *e = std::getenv("MADPOSE_MDX_R");
-                    const int r = e ? std::atoi(e) : 2;
-                    return r == 1 || r == 4 || r == 8 ? r : 2;
+                    return e && e[0] == '1';
                 }();
-                if (rps == 1)
+                if (one)
                     md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
-                else if (rps == 2)
+                else
                     md_exact_kernel<v, 2><<<(nlist + 31) / 32, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
                                                                            counts, maxm);
-                else if (rps == 4)
-                    md_exact_kernel<v, 4><<<(nlist + 15) / 16, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
-                                                                           counts, maxm);
-                else
-                    md_exact_kernel<v, 8><<<(nlist + 7) / 8, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
-                                                                         counts, maxm);
                 return hipGetLastError();
             }
         } else if constexpr (v == kTF) {
