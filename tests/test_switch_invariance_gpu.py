@@ -1,0 +1,49 @@
+"""The engine's performance switches change no result: the full-size estimator cases
+and four pairs in flight, each switch setting in a fresh process (the engine reads them
+once), compared field by field with the default run to the last bit -- the early
+continuation forced off and on (MADPOSE_EARLY_CONT, §2 step 7 of DESIGN.md), the
+shared-focal exact MD on one lane per sample instead of two (MADPOSE_MDX_R), the scalar
+batch drawing instead of AVX-512 (MADPOSE_SAMPLER_SIMD), the 15x15 QR packed 16
+samples per wave instead of one sample per wave (MADPOSE_EIG_WAVES), and the
+draw-by-draw sampler (MADPOSE_SAMPLER_TWO_PASS)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import madpose
+
+pytestmark = pytest.mark.gpu
+
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "switch_worker.py")
+SETTINGS = {"early_off": {"MADPOSE_EARLY_CONT": "0"}, "early_on": {"MADPOSE_EARLY_CONT": "1"},
+            "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
+            "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"}}
+
+
+def _run(extra):
+    env = dict(os.environ)
+    for k in list(env):
+        if k.startswith("MADPOSE_"):
+            del env[k]
+    env.update(extra)
+    r = subprocess.run([sys.executable, WORKER], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.fixture(scope="module")
+def default_run():
+    if madpose.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X")
+    return _run({})
+
+
+@pytest.mark.parametrize("name", list(SETTINGS))
+def test_switch_changes_no_result(default_run, name):
+    other = _run(SETTINGS[name])
+    assert len(other) == len(default_run)
+    for k, (a, b) in enumerate(zip(default_run, other)):
+        assert a == b, (name, k, a, b)
