@@ -674,8 +674,13 @@ class Run {
         // 903 / 982 / 998 pairs/s at 128 / 512 / 1000 on one box, profiles/r03/s6)
         min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 1024;
         min_batch_ = std::min(min_batch_, max_batch_);
+        // growth: 1, and 2 for the shared focal, whose pair waits on the GPU (≈ 380 us of
+        // latency-bound point chain per batch, flat in the batch size): fewer, larger
+        // batches -- sf 11.48 / 11.48 / 11.49 ms at 1, 11.20 / 10.97 / 11.18 at 2, 10.88 /
+        // 11.16 / 11.13 at 3 on one box (profiles/r04/gab2); for cal, 0.5 and the
+        // waste it saves cost more round trips than they save work (gab)
         const char *env3 = std::getenv("MADPOSE_BATCH_GROWTH");
-        growth_ = env3 ? std::max(0.01, std::atof(env3)) : 1.0;
+        growth_ = env3 ? std::max(0.01, std::atof(env3)) : (variant_ == kSF ? 2.0 : 1.0);
         trace_ = std::getenv("MADPOSE_TRACE") != nullptr;
         double M = 0.0;
         for (int t = 0; t < 3; ++t) M += P.C.thr[t] * std::fabs(P.C.w[t]);
