@@ -29,6 +29,22 @@
 namespace mp {
 namespace {
 
+// Phase timing for tools/eig6_bench.hip (compiled out otherwise): wall-clock ticks of
+// the kernel's phases, summed over waves (lane 0)
+#ifdef MP_EIG6_PROFILE
+__device__ unsigned long long e6g_prof[10];
+#define E6G_MARK(i)                                                                                                    \
+    do {                                                                                                               \
+        const unsigned long long t_ = wall_clock64();                                                                 \
+        if (threadIdx.x == 0) atomicAdd(&e6g_prof[i], t_ - t_prev);                                                    \
+        t_prev = t_;                                                                                                   \
+    } while (0)
+#define E6G_START unsigned long long t_prev = wall_clock64()
+#else
+#define E6G_MARK(i) ((void)0)
+#define E6G_START ((void)0)
+#endif
+
 // value of v at lane `src` (0..15) of the caller's group (src group-uniform)
 __device__ inline double e6g_at(double v, int src) { return __shfl(v, (int)(threadIdx.x & ~15u) + src, 64); }
 
@@ -105,6 +121,7 @@ __device__ __forceinline__ void e6g_null(const double (&g)[NC], unsigned cols, i
 
 __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist, BatchGate gate) {
     if (batch_cancelled(gate.word, gate.hi)) return;
+    E6G_START;
     const int i = threadIdx.x & 15;
     const int idx = blockIdx.x * 4 + (threadIdx.x >> 4);
     const bool valid = idx < nlist;
@@ -127,6 +144,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
         // row i of M0^-1 [M2 M1] is the row pivoted in column i
         static_for<20>([&](auto j) { CB[j] = -e6g_at(g[10 + j], myrow < 0 ? 0 : myrow); });
     }
+    E6G_MARK(0);
     if (!ok) { // M0 singular: no roots (group-uniform)
         if (valid && i == 0) P[225] = 0.0;
         return;
@@ -148,6 +166,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
         for (int k = 0; k < 6; ++k) e6g_gj_step<10, 10>(g, 10, rows, cols, myrow);
         e6g_null<10, 10, 4>(g, cols, myrow, nr);
     }
+    E6G_MARK(1);
     // S = Nl^T M1 Nr (4 x 4, rank 3): lane c forms column c of T = Nl^T M1
     double S[4][4];
     {
@@ -215,6 +234,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
             cv[c] = x;
         });
     }
+    E6G_MARK(2);
     // v = Nr c (component i), rhs = -M1 v
     const double v = lr ? fma(nr[3], cv[3], fma(nr[2], cv[2], fma(nr[1], cv[1], nr[0] * cv[0]))) : 0.0;
     double rhs = 0.0;
@@ -235,6 +255,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
         const double gr = e6g_at(g[10], myrow < 0 ? 0 : myrow);
         pa = (lr && ((cols >> i) & 1u)) ? gr : 0.0;
     }
+    E6G_MARK(3);
     // ---- C <- Q^T C Q, Q = H_0 ... H_4 the Householder reflectors of Z = [Nr a; 0 v] ----
     double CA[20];
     static_for<20>([&](auto j) { CA[j] = (lr && j == 10 + i) ? 1.0 : 0.0; });
@@ -282,6 +303,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
             CB[j] = fma(-dB, hv[j], CB[j]);
         });
     });
+    E6G_MARK(4);
     // ---- the trailing 15 x 15 block, lane i' = row 5 + i' ----
     constexpr int N = 15;
     double h[N];
@@ -292,6 +314,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
             h[j] = i < 5 ? a : (i < 15 ? b : 0.0);
         });
     }
+    E6G_MARK(5);
     // ---- balance (EISPACK balanc without permutations) ----
     {
         const double radix = 2.0, sqrdx = 4.0;
@@ -328,6 +351,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
             });
         }
     }
+    E6G_MARK(6);
     // ---- elmhes: the eliminations of one column as one similarity ----
     static_for<N - 2>([&](auto mm) {
         constexpr int m = decltype(mm)::value + 1;
@@ -363,6 +387,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
         });
         h[m] = acc;
     });
+    E6G_MARK(7);
     static_for<N>([&](auto j) {
         if (j < i - 1) h[j] = 0.0;
     });

@@ -292,6 +292,19 @@ int main(int argc, char **argv) {
                 std::printf("\n");
             }
         }
+        {
+            unsigned long long gp[10] = {0}, z10[10] = {0};
+            CHECK(hipMemcpyToSymbol(HIP_SYMBOL(e6g_prof), z10, sizeof(z10)));
+            CHECK(hipMemcpy(d_pen3, d_pen, (size_t)ns * kPenStride * 8, hipMemcpyDeviceToDevice));
+            pt_defl6_grp_kernel<<<(ns + 3) / 4, 64>>>(d_pen3, ns, BatchGate{});
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipMemcpyFromSymbol(gp, HIP_SYMBOL(e6g_prof), sizeof(gp)));
+            const double waves = (ns + 3) / 4;
+            std::printf("group deflation phases per wave (us at 100 MHz ticks): C %.1f, null spaces %.1f, S / c %.1f, "
+                        "particular %.1f, similarity %.1f, block %.1f, balance %.1f, elmhes %.1f\n",
+                        gp[0] / waves / 100, gp[1] / waves / 100, gp[2] / waves / 100, gp[3] / waves / 100,
+                        gp[4] / waves / 100, gp[5] / waves / 100, gp[6] / waves / 100, gp[7] / waves / 100);
+        }
         std::printf("deflation + Hessenberg: one wave per sample %.1f us, 16-lane groups %.1f us; roots after the "
                     "lane QR agree (1e-9) on %ld of %d samples (roots %ld / %ld)\n",
                     1e3 * tw, 1e3 * tg, same, ns, ra, rb);
