@@ -200,17 +200,30 @@ struct SweepSlot {
     static size_t lm_bytes(int64_t nidx) { return 512 + sizeof(int) * (size_t)nidx; }
 };
 
+int active_runs(int device);
+
 // Worker threads for the parallel LO steps: run(n, f) calls f(job, lane) for jobs
-// 0..n-1, lane 0 being the calling thread and lanes 1..size-1 the workers.
+// 0..n-1, lane 0 being the calling thread and lanes 1..size-1 the workers.  While the
+// estimator has its device to itself, the workers spin (with pause, bounded by
+// lo_spin_us() as the LM pool's) before they block, and so does the caller at the
+// join: a futex wake-up per worker per LO delayed the steps of each LO by ~30 us
+// (steps phase 230 us for a 200 us longest step, profiles/r04/lotab).  With other
+// estimators on the device they block at once (their threads share the CPUs).
+// MADPOSE_LO_WORKER_SPIN=0 turns the spinning off.
 class LoWorkers {
   public:
-    explicit LoWorkers(int lanes) {
+    LoWorkers(int lanes, int device) : device_(device) {
+        // microseconds (MADPOSE_LO_WORKER_SPIN; 0: block at once); default 2000 -- the
+        // LO runs of a pair come ~0.3-1 ms apart, so a shorter spin sleeps through the
+        // gap -- or 0 where the LM pool does not spin either (a small CPU share per rank)
+        const char *e = std::getenv("MADPOSE_LO_WORKER_SPIN");
+        spin_ns_ = e ? std::max(0, std::atoi(e)) * 1000ll : (lo_spin_us() > 0 ? 2000 * 1000ll : 0);
         for (int i = 1; i < lanes; ++i) th_.emplace_back([this, i] { loop(i); });
     }
     ~LoWorkers() {
         {
             std::lock_guard<std::mutex> lk(mu_);
-            quit_ = true;
+            quit_.store(true);
         }
         cv_.notify_all();
         for (auto &t : th_) t.join();
@@ -222,19 +235,36 @@ class LoWorkers {
             f_ = &f;
             n_ = n;
             next_.store(0);
-            active_ = (int)th_.size();
+            active_.store((int)th_.size());
             err_ = nullptr;
-            ++gen_;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         work(0);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return active_ == 0; });
+        if (!spin_until([this] { return active_.load(std::memory_order_acquire) == 0; })) {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_cv_.wait(lk, [this] { return active_.load(std::memory_order_acquire) == 0; });
+        }
         f_ = nullptr;
         if (err_) std::rethrow_exception(err_);
     }
 
   private:
+    // polls ready() with pause for at most spin_ns_ (none with other estimators on the
+    // device); true once it held
+    template <class F> bool spin_until(const F &ready) const {
+        if (spin_ns_ <= 0 || active_runs(device_) > 1) return ready();
+        const auto t0 = Clock::now();
+        for (int k = 0;; ++k) {
+            if (ready()) return true;
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+            if ((k & 63) == 63 &&
+                std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count() > spin_ns_)
+                return ready();
+        }
+    }
     void work(int lane) {
         for (int k; (k = next_.fetch_add(1)) < n_;) {
             try {
@@ -248,26 +278,34 @@ class LoWorkers {
     void loop(int lane) {
         uint64_t seen = 0;
         for (;;) {
-            {
+            if (!spin_until([&] { return quit_.load() || gen_.load(std::memory_order_acquire) != seen; })) {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
-                if (quit_) return;
-                seen = gen_;
+                cv_.wait(lk, [&] { return quit_.load() || gen_.load(std::memory_order_acquire) != seen; });
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu_); // (pairs with run()'s publication)
+                if (quit_.load()) return;
+                seen = gen_.load(std::memory_order_relaxed);
             }
             work(lane);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--active_ == 0) done_cv_.notify_one();
+            if (active_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> lk(mu_);
+                done_cv_.notify_one();
+            }
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_, err_mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(int, int)> *f_ = nullptr;
-    int n_ = 0, active_ = 0;
+    int n_ = 0;
+    std::atomic<int> active_{0};
     std::atomic<int> next_{0};
-    uint64_t gen_ = 0;
-    bool quit_ = false;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<bool> quit_{false};
     std::exception_ptr err_;
+    int device_ = 0;
+    long long spin_ns_ = 0;
 };
 
 constexpr int kLoLanes = 12; // most concurrent LO steps (and sweep slots) per context
@@ -741,6 +779,7 @@ class Run {
     // + step 0's non-minimal fit and score, other steps' fit; step 0's first lsq_fit and
     // lsq iterations, the other steps' (mean)
     double lo_t_[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    double lo_seg_[3] = {0, 0, 0}; // steps phase: before, during and after the parallel run
     bool lo_parallel_ = true;
 
     // LO sweeps run on the issuing thread's core (host/lo_sweep.h): the reference's
@@ -1073,13 +1112,28 @@ class Run {
                     if (!step_skipped(r == 0 ? sample0 : sample1)) pos += per_step;
                 }
                 const Mt19937 base_sel = sel;
+                // the speculation hook runs as job 1, beside the steps: step 0 (the
+                // longest, on all base inliers) starts at once, and the lane that takes
+                // the hook takes a short step after it (the hook may wait for the
+                // sampler thread to finish launching a continuation it cancels)
+                Mt19937 end = base_sel;
+                const bool hook_job = predicted && X_.lo_workers->lanes() > 1;
                 if (predicted) {
-                    Mt19937 end = base_sel;
                     end.discard(pos - base_sel.draws());
-                    predicted(end);
+                    if (!hook_job) predicted(end);
                 }
                 std::vector<double> step_s(R, 0.0);
-                X_.lo_workers->run(R, [&](int r, int lane) {
+                const auto t_run = Clock::now();
+                lo_seg_[0] += std::chrono::duration<double>(t_run - t_steps).count();
+                X_.lo_workers->run(R + (hook_job ? 1 : 0), [&](int job, int lane) {
+                    if (hook_job && job == 1) {
+                        auto th = Clock::now();
+                        if (lane != 0) MP_HIP(hipSetDevice(X_.device));
+                        predicted(end);
+                        lo_seg_[2] += secs(th);
+                        return;
+                    }
+                    const int r = hook_job && job > 1 ? job - 1 : job;
                     auto ts = Clock::now();
                     if (lane != 0) MP_HIP(hipSetDevice(X_.device));
                     Mt19937 my = base_sel;
@@ -1091,6 +1145,7 @@ class Run {
                     outs[r].sel = my;
                     step_s[r] = secs(ts);
                 });
+                lo_seg_[1] += secs(t_run);
                 for (int r = 0; r < R; ++r) {
                     lo_t_[3] += step_s[r];
                     lo_t_[4] = std::max(lo_t_[4], step_s[r]);
@@ -1163,14 +1218,16 @@ class Run {
     // best: best_min_model_score when the batch starts (the scoring's early exit).
     bool batch_prof_[2] = {false, false};
     double launch_s_ = 0.0; // main-thread time in launch_batch (MADPOSE_LO_TIMING)
-    // early continuation (MADPOSE_EARLY_CONT=0: launch the continuation after reading
-    // the batch, as before; =1: also with other estimators on the device).  By default
-    // only while this estimator is alone on its device: with 8 shared-focal pairs in
-    // flight the discarded continuations took GPU time from the other pairs (ScanNet
-    // stand-in 747 -> 1064 pairs/s without them, profiles/r04/scab/)
+    // early continuation: off by default (MADPOSE_EARLY_CONT=1: on while this estimator
+    // is alone on its device, =2: always).  With 8 shared-focal pairs in flight the
+    // discarded continuations took GPU time from the other pairs (ScanNet stand-in 747
+    // -> 1064 pairs/s without them, profiles/r04/scab/); alone, an LO that cancels the
+    // continuation waits for the sampler thread to finish launching it (the speculation
+    // hook 31-48 us instead of 4 us, the LO steps phase 221-233 vs 180-194 us, cal 5.90-
+    // 5.99 vs 5.80-5.86 ms, profiles/r04/hook2/)
     const int early_mode_ = [] {
         const char *e = std::getenv("MADPOSE_EARLY_CONT");
-        return e ? (e[0] == '0' ? 0 : 2) : 1;
+        return e ? (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0)) : 0;
     }();
     bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
     int launch_n_ = 0;
@@ -1304,7 +1361,7 @@ void Run::run(Model *best, Stats *S) {
     }
     if (lo_parallel_) {
         const int nl = lo_lanes_setting();
-        if (!X_.lo_workers || X_.lo_workers->lanes() != nl) X_.lo_workers.reset(new LoWorkers(nl));
+        if (!X_.lo_workers || X_.lo_workers->lanes() != nl) X_.lo_workers.reset(new LoWorkers(nl, X_.device));
         for (int l = 1; l < nl; ++l) lanes_[l].slot = &X_.sweep_slot[l];
     }
     upload_pair(X_, P_, &D_);
@@ -1624,6 +1681,10 @@ void Run::run(Model *best, Stats *S) {
                      1e6 * lo_t_[5] / lo_t_[2], 1e6 * lo_t_[4], 1e6 * lo_t_[6] / lo_t_[2], 1e6 * lo_t_[7] / lo_t_[2],
                      1e6 * lo_t_[8] / lo_t_[2], 1e6 * lo_t_[9] / lo_t_[2], 1e6 * lo_t_[10] / lo_t_[2],
                      1e6 * lo_t_[11] / lo_t_[2], 1e6 * lo_t_[12] / lo_t_[2], lo_t_[13] / lo_t_[2]);
+    if (std::getenv("MADPOSE_LO_TIMING") && lo_t_[2] > 0)
+        std::fprintf(stderr, "[engine] LO steps phase: before the parallel run %.1f us, the run %.1f us, the speculation "
+                     "hook %.1f us (avg per LO)\n",
+                     1e6 * lo_seg_[0] / lo_t_[2], 1e6 * lo_seg_[1] / lo_t_[2], 1e6 * lo_seg_[2] / lo_t_[2]);
     if (std::getenv("MADPOSE_SWEEP_TIMING") && S->num_lo_sweeps > 0)
         std::fprintf(stderr, "[engine] %llu host sweeps: %.2f us (avg)\n", (unsigned long long)S->num_lo_sweeps,
                      1e6 * tsum[1] / S->num_lo_sweeps);

@@ -9,6 +9,7 @@
 // produced with this container's g++ 11.4 (std::mt19937 + std distributions), i.e.
 // the streams the reference consumes in src/hybrid_ransac.h:64,79-80,226-229.
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #if defined(__x86_64__) && (defined(__clang__) || defined(__GNUC__))
@@ -34,8 +35,14 @@ class Mt19937 {
     // outputs consumed since seeding: two copies of one stream are at the same
     // position iff their counts agree
     uint64_t draws() const { return draws_; }
-    void discard(uint64_t k) {
-        for (uint64_t i = 0; i < k; ++i) (*this)();
+    void discard(uint64_t k) { // block by block: the same state as k calls
+        while (k > 0) {
+            if (idx_ >= 624) twist();
+            const uint64_t take = std::min<uint64_t>(k, (uint64_t)(624 - idx_));
+            idx_ += (int)take;
+            draws_ += take;
+            k -= take;
+        }
     }
     // the next k outputs without consuming them, or nullptr if they cross a block
     const uint32_t *window(int k) {

@@ -1,7 +1,7 @@
 """The engine's performance switches change no result: the full-size estimator cases
 and four pairs in flight, each switch setting in a fresh process (the engine reads them
 once), compared field by field with the default run to the last bit -- the early
-continuation forced off and on (MADPOSE_EARLY_CONT, §2 step 7 of DESIGN.md), the
+continuation on while alone and always (MADPOSE_EARLY_CONT, §2 step 7 of DESIGN.md), the
 shared-focal exact MD on one lane per sample instead of two (MADPOSE_MDX_R), the scalar
 batch drawing instead of AVX-512 (MADPOSE_SAMPLER_SIMD), the 15x15 QR packed 16
 samples per wave instead of one sample per wave (MADPOSE_EIG_WAVES), and the
@@ -18,7 +18,7 @@ import madpose
 pytestmark = pytest.mark.gpu
 
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "switch_worker.py")
-SETTINGS = {"early_off": {"MADPOSE_EARLY_CONT": "0"}, "early_on": {"MADPOSE_EARLY_CONT": "1"},
+SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOSE_EARLY_CONT": "2"},
             "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
             "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"}}
 

@@ -13,10 +13,10 @@ for rep in $(seq 1 "$reps"); do
 import json, re, sys
 base, name = sys.argv[1], sys.argv[2]
 d = json.loads(open(base + ".json").read().strip().splitlines()[-1])
-keys = ["prefix", "steps", "step0", "longest step", "step0 fit", "step0 lsq", "step0 iters"]
+keys = ["prefix", "steps", "step0", "step0 fit", "step0 lsq", "step0 iters", "before the parallel run", "the run", "the speculation hook"]
 acc = {k: [] for k in keys}
 for line in open(base + ".err"):
-    if " LO: " not in line:
+    if " LO: " not in line and "LO steps phase" not in line:
         continue
     for k in keys:
         m = re.search(re.escape(k) + r" ([0-9.]+) us", line)
