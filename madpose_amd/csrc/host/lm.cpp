@@ -100,8 +100,9 @@ struct Acc {
 // all-inlier fits, >= kPoolBlocks residual blocks: ~100-500 us per evaluation on one
 // core, on the critical path of every LO); smaller problems (~10-100 us of work,
 // comparable to a thread wake-up) run inline.  MADPOSE_LO_THREADS sets the pool size
-// (default 4; 1 = off).  The blocks are reduced in fixed chunks in chunk order either
-// way, so the result does not depend on the pool.
+// (default 8, of which 4 take the problems below kPoolWide blocks; 1 = off).  The
+// blocks are reduced in fixed chunks in chunk order either way, so the result does not
+// depend on the pool.
 constexpr size_t kChunk = 256;
 constexpr size_t kPoolBlocks = 2048;
 // Workers spin (with pause) for a while after each job before they block on the
@@ -131,35 +132,49 @@ int lo_spin_us() {
 }
 
 namespace {
+// Workers 1..kNarrow-1 take part in every job; the rest (MADPOSE_LO_THREADS beyond
+// kNarrow) only in wide jobs -- problems of at least kPoolWide blocks, the two-focal
+// all-inlier fits (N = 4000: ~10k blocks), where 8 threads cut the LO's serial fits by
+// a third (prefix 257 -> 169-193 us, tf 13.2 -> 11.7-12.1 ms per pair) while the
+// calibrated / shared-focal ones (<= ~7.5k blocks) gained nothing from them
+// (profiles/r04/lotab, tflo).  The wide workers wait on a counter of their own, so a
+// narrow job neither wakes them nor keeps them spinning.
+constexpr int kNarrow = 4;
+constexpr size_t kPoolWide = 8192;
 class Pool {
   public:
     explicit Pool(int n) {
         spin_ns_ = lo_spin_us() * 1000ll;
-        for (int i = 0; i < n - 1; ++i) th_.emplace_back([this] { loop(); });
+        for (int i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i >= kNarrow); });
+        narrow_ = std::min((int)th_.size(), kNarrow - 1);
     }
     ~Pool() {
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
             gen_.fetch_add(1, std::memory_order_release);
+            gen_wide_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
-    // runs f(k) for k in [0, n); the calling thread takes part
-    void run(size_t n, const std::function<void(size_t)> &f) {
+    // runs f(k) for k in [0, n); the calling thread takes part, and the narrow workers
+    // (all workers when wide)
+    void run(size_t n, const std::function<void(size_t)> &f, bool wide = false) {
         if (th_.empty() || n < 2) {
             for (size_t k = 0; k < n; ++k) f(k);
             return;
         }
         std::lock_guard<std::mutex> job(job_mu_);
+        wide = wide && (int)th_.size() > narrow_;
         {
             std::lock_guard<std::mutex> lk(mu_);
             f_ = &f;
             n_ = n;
             next_.store(0);
-            active_.store((int)th_.size(), std::memory_order_relaxed);
+            active_.store(wide ? (int)th_.size() : narrow_, std::memory_order_relaxed);
             gen_.fetch_add(1, std::memory_order_release);
+            if (wide) gen_wide_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         work();
@@ -193,18 +208,19 @@ class Pool {
     void work() {
         for (size_t k; (k = next_.fetch_add(1)) < n_;) (*f_)(k);
     }
-    void loop() {
+    void loop(bool wide_only) {
+        const std::atomic<uint64_t> &g = wide_only ? gen_wide_ : gen_;
         uint64_t seen = 0;
         for (;;) {
-            const bool ready = spin_until([&] { return gen_.load(std::memory_order_acquire) != seen; });
+            const bool ready = spin_until([&] { return g.load(std::memory_order_acquire) != seen; });
             if (!ready) {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                cv_.wait(lk, [&] { return g.load(std::memory_order_acquire) != seen; });
             }
             {
                 std::lock_guard<std::mutex> lk(mu_); // (pairs with run()'s publication)
                 if (stop_) return;
-                seen = gen_.load(std::memory_order_relaxed);
+                seen = g.load(std::memory_order_relaxed);
             }
             work();
             if (active_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
@@ -214,13 +230,14 @@ class Pool {
         }
     }
     std::vector<std::thread> th_;
+    int narrow_ = 0;
     std::mutex mu_, job_mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(size_t)> *f_ = nullptr;
     size_t n_ = 0;
     std::atomic<size_t> next_{0};
     std::atomic<int> active_{0};
-    std::atomic<uint64_t> gen_{0};
+    std::atomic<uint64_t> gen_{0}, gen_wide_{0};
     bool stop_ = false;
     long long spin_ns_ = 0;
 };
@@ -228,7 +245,7 @@ class Pool {
 Pool &lo_pool() {
     static Pool pool([] {
         const char *e = std::getenv("MADPOSE_LO_THREADS");
-        const int n = e ? std::atoi(e) : 4;
+        const int n = e ? std::atoi(e) : 8;
         return std::max(1, std::min(n, 64));
     }());
     return pool;
@@ -301,7 +318,7 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
             range(k * kChunk, std::min(nb, (k + 1) * kChunk), parts[k]);
         };
         if (nb >= kPoolBlocks)
-            lo_pool().run(nchunks, chunk);
+            lo_pool().run(nchunks, chunk, nb >= kPoolWide);
         else
             for (size_t k = 0; k < nchunks; ++k) chunk(k);
         for (size_t k = 0; k < nchunks; ++k) total.merge(parts[k]);
