@@ -28,6 +28,8 @@
 // per lane.  The code compiles for the host as well (tests/md_exact_check.cpp
 // checks it against the oracle on the CPU).
 #pragma once
+#include <cfloat>
+
 #include "mp_md.h"
 
 namespace mp {
@@ -642,7 +644,256 @@ MP_HD double mean_abs_xy(const double (&x)[4][3]) {
     return s / (2 * 4);
 }
 
+// det3 (la.cpp:570-572), row-major
+MP_HD double det3(const double (&M)[3][3]) {
+#pragma clang fp contract(off)
+    return M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) - M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+           M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+}
+
+// The MD poses' SVD as the reference calls it, Eigen::JacobiSVD<MatrixXd>(S,
+// ComputeFullU | ComputeFullV) (src/solver.cpp:517, :722, :1026), restated from Eigen
+// 3.4 as the oracle restates it (la.cpp eigen_jacobi_svd3): scaling by the largest
+// |entry|, two-sided sweeps over (p, q) = (1, 0), (2, 0), (2, 1) until every
+// off-diagonal entry is below max(DBL_MIN, 2 eps max|diag|), each a real 2 x 2 Jacobi
+// SVD (real_2x2_jacobi_svd, makeJacobi) applied to the rows and columns, the signs of
+// the diagonal moved into U, and the singular values sorted descending by swaps.  It
+// converges in 3-5 sweeps also on the rank-2 cross-covariance of three points (the
+// one-sided Jacobi the oracle used before ran to its cap of 60 sweeps on about 1 % of
+// calibrated samples, 85 of 150 us per MD launch, profiles/r05/mdx).
+struct Rot2 {
+    double c, s;
+};
+// rows p, q of M: x' = c x + s y, y' = -s x + c y (Eigen apply_rotation_in_the_plane;
+// the identity is a no-op)
+template <int P, int Q> MP_HD void rot_rows(double (&M)[3][3], Rot2 j) {
+#pragma clang fp contract(off)
+    if (j.c == 1.0 && j.s == 0.0) return;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double xi = M[P][i], yi = M[Q][i];
+        M[P][i] = j.c * xi + j.s * yi;
+        M[Q][i] = -j.s * xi + j.c * yi;
+    }
+}
+// columns p, q: MatrixBase::applyOnTheRight(p, q, j) applies j^T = (c, -s)
+template <int P, int Q> MP_HD void rot_cols(double (&M)[3][3], Rot2 j) {
+#pragma clang fp contract(off)
+    const double c = j.c, s = -j.s;
+    if (c == 1.0 && s == 0.0) return;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double xi = M[i][P], yi = M[i][Q];
+        M[i][P] = c * xi + s * yi;
+        M[i][Q] = -s * xi + c * yi;
+    }
+}
+MP_HD Rot2 make_jacobi(double x, double y, double z) {
+#pragma clang fp contract(off)
+    const double deno = 2.0 * fabs(y);
+    if (deno < DBL_MIN) return Rot2{1.0, 0.0};
+    const double tau = (x - z) / deno;
+    const double w = sqrt(tau * tau + 1.0);
+    const double t = tau > 0.0 ? 1.0 / (tau + w) : 1.0 / (tau - w);
+    const double sign_t = t > 0.0 ? 1.0 : -1.0;
+    const double n = 1.0 / sqrt(t * t + 1.0);
+    return Rot2{n, -sign_t * (y / fabs(y)) * fabs(t) * n};
+}
+// one (p, q) step of the sweep
+template <int P, int Q>
+MP_HD void jacobi_step(double (&W)[3][3], double (&U)[3][3], double (&V)[3][3], double &max_diag, bool &finished) {
+#pragma clang fp contract(off)
+    const double pm = 2.0 * DBL_EPSILON * max_diag;
+    const double threshold = DBL_MIN < pm ? pm : DBL_MIN;
+    if (!(fabs(W[P][Q]) > threshold || fabs(W[Q][P]) > threshold)) return;
+    finished = false;
+    double m00 = W[P][P], m01 = W[P][Q], m10 = W[Q][P], m11 = W[Q][Q];
+    Rot2 rot1{1.0, 0.0};
+    const double t = m00 + m11, d = m10 - m01;
+    if (!(fabs(d) < DBL_MIN)) {
+        const double u = t / d;
+        const double tmp = sqrt(1.0 + u * u);
+        rot1 = Rot2{u / tmp, 1.0 / tmp};
+    }
+    if (!(rot1.c == 1.0 && rot1.s == 0.0)) {
+        const double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
+        m00 = rot1.c * x0 + rot1.s * y0;
+        m01 = rot1.c * x1 + rot1.s * y1;
+        m11 = -rot1.s * x1 + rot1.c * y1;
+    }
+    const Rot2 jr = make_jacobi(m00, m01, m11);
+    const double c2 = jr.c, s2 = -jr.s; // j_left = rot1 * j_right^T
+    const Rot2 jl{rot1.c * c2 - rot1.s * s2, rot1.c * s2 + rot1.s * c2};
+    rot_rows<P, Q>(W, jl);
+    rot_cols<P, Q>(U, Rot2{jl.c, -jl.s}); // U.applyOnTheRight(p, q, j_left^T)
+    rot_cols<P, Q>(W, jr);
+    rot_cols<P, Q>(V, jr);
+    const double dp = fabs(W[P][P]), dq = fabs(W[Q][Q]);
+    const double mm = dp < dq ? dq : dp;
+    max_diag = max_diag < mm ? mm : max_diag;
+}
+
+MP_HD void svd3(const double (&A)[3][3], double (&U)[3][3], double (&V)[3][3]) {
+#pragma clang fp contract(off)
+    double scale = 0.0;
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double a = fabs(A[i][j]);
+            nan = nan || a != a;
+            scale = scale < a ? a : scale;
+        }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) U[i][j] = V[i][j] = i == j ? 1.0 : 0.0;
+    if (nan || !(scale <= DBL_MAX)) return; // Eigen: InvalidInput
+    if (scale == 0.0) scale = 1.0;
+    double W[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) W[i][j] = A[i][j] / scale;
+    double max_diag = fabs(W[0][0]);
+    max_diag = max_diag < fabs(W[1][1]) ? fabs(W[1][1]) : max_diag;
+    max_diag = max_diag < fabs(W[2][2]) ? fabs(W[2][2]) : max_diag;
+    bool finished = false;
+    // (a cap far above the 3-6 sweeps finite data takes, against non-termination)
+    for (int sweep = 0; !finished && sweep < 1000; ++sweep) {
+        finished = true;
+        jacobi_step<1, 0>(W, U, V, max_diag, finished);
+        jacobi_step<2, 0>(W, U, V, max_diag, finished);
+        jacobi_step<2, 1>(W, U, V, max_diag, finished);
+    }
+    double sv[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double a = W[i][i];
+        sv[i] = fabs(a);
+        if (a < 0.0)
+#pragma unroll
+            for (int r = 0; r < 3; ++r) U[r][i] = -U[r][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sv[i] *= scale;
+    // descending by swaps: position i takes the first maximum of the tail
+    bool stop = false;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int pos = i;
+        double best = sv[i];
+#pragma unroll
+        for (int j = i + 1; j < 3; ++j)
+            if (sv[j] > best) {
+                best = sv[j];
+                pos = j;
+            }
+        stop = stop || best == 0.0;
+#pragma unroll
+        for (int j = i + 1; j < 3; ++j) {
+            const bool sw = !stop && pos == j;
+            const double a = opaque(sv[i]), b2 = opaque(sv[j]);
+            sv[i] = sw ? b2 : a;
+            sv[j] = sw ? a : b2;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const double ui = opaque(U[r][i]), uj = opaque(U[r][j]);
+                U[r][i] = sw ? uj : ui;
+                U[r][j] = sw ? ui : uj;
+                const double vi = opaque(V[r][i]), vj = opaque(V[r][j]);
+                V[r][i] = sw ? vj : vi;
+                V[r][j] = sw ? vi : vj;
+            }
+        }
+    }
+}
+
+// Kabsch without scale, Y ~ R X + t, as the oracle's procrustes (md.cpp:355-383;
+// src/solver.cpp:506-525): centroids, cross-covariance S = sum (Y - cy)(X - cx)^T,
+// R = U diag(1, 1, sign) V^T with the sign from det U det V, t = cy - R cx.
+template <int K> MP_HD void procrustes(const double (&X)[K][3], const double (&Y)[K][3], Model &m) {
+#pragma clang fp contract(off)
+    double cx[3] = {0, 0, 0}, cy[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            cx[c] += X[i][c];
+            cy[c] += Y[i][c];
+        }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        cx[c] /= K;
+        cy[c] /= K;
+    }
+    double S[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) S[a][b] += (Y[i][a] - cy[a]) * (X[i][b] - cx[b]);
+    double U[3][3], V[3][3];
+    svd3(S, U, V);
+    const double du = det3(U), dv = det3(V);
+    if (du * dv < 0)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) U[i][2] = -U[i][2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            double s = 0;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) s += U[a][c] * V[b][c];
+            m.R[3 * a + b] = s;
+        }
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        m.t[a] = cy[a] - (m.R[3 * a] * cx[0] + m.R[3 * a + 1] * cx[1] + m.R[3 * a + 2] * cx[2]);
+}
+
 } // namespace mdx
+
+// Pose stage of the MD solvers as the oracle's md_pose (md.cpp:394-434): the
+// positivity test of the corrected depths (src/solver.cpp:503-504), the focal
+// division, and the exact Procrustes above -- the model's every double is the
+// oracle's.  K = 3 (cal) or 4 (sf/tf) points; fx, fy the solution's focals.
+// md_pose_points: the corrected points and the positivity test (the model's scale and
+// offsets are the solution's, so whether it is kept is known before the Procrustes).
+template <int K>
+MP_HD bool md_pose_points(const double (&x)[K][3], const double (&y)[K][3], const double *dx, const double *dy,
+                          const double *sol, double fx, double fy, double (&X)[K][3], double (&Y)[K][3]) {
+#pragma clang fp contract(off)
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double d1 = dx[i] + sol[1];
+        const double d2 = dy[i] * sol[2] + sol[3];
+        if (!(d1 > 0.0) || !(d2 > 0.0)) ok = false;
+        X[i][0] = x[i][0] / fx * d1;
+        X[i][1] = x[i][1] / fx * d1;
+        X[i][2] = x[i][2] * d1;
+        Y[i][0] = y[i][0] / fy * d2;
+        Y[i][1] = y[i][1] / fy * d2;
+        Y[i][2] = y[i][2] * d2;
+    }
+    return ok;
+}
+
+template <int K>
+MP_HD bool md_pose_exact(const double (&x)[K][3], const double (&y)[K][3], const double *dx, const double *dy,
+                         const double *sol, double fx, double fy, Model &m) {
+    double X[K][3], Y[K][3];
+    if (!md_pose_points<K>(x, y, dx, dy, sol, fx, fy, X, Y)) return false;
+    mdx::procrustes<K>(X, Y, m);
+    m.scale = sol[2];
+    m.offset0 = sol[1];
+    m.offset1 = sol[3];
+    return true;
+}
 
 // The solvers in two parts, as the oracle's loop over roots: setup() builds the
 // sample's system and returns the ascending real roots of its resultant; root() turns

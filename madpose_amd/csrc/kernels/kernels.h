@@ -19,7 +19,7 @@ __device__ inline bool batch_cancelled(const unsigned long long *word, unsigned 
 // r0/r1 = 1 / |K^-1 x| for the calibrated bearings
 hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1);
 
-// MD minimal solver over the listed iterations (one thread per iteration).
+// MD minimal solver over the listed iterations (md_exact: R lanes per sample).
 hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm);
 // Workspace of the staged point solvers (per point sample: candidate roots and model

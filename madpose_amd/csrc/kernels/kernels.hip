@@ -1,9 +1,9 @@
 // HIP kernels of the MI355X hybrid-RANSAC engine (gfx950, wave64).
 //
 //  prep_pair          per-pair bearing norms (once per pair)
-//  md_solve_group<V>  MD minimal solvers, one 16-lane group per sample (side stream);
-//                     md_solve<V, ALT> keeps one sample per lane for the option-gated
-//                     paths and A/B runs
+//  md_exact<V, R>     MD minimal solvers with the oracle's arithmetic, R lanes per
+//                     sample (side stream); md_solve<V, ALT> keeps one sample per lane
+//                     for the option-gated paths (scale-only, no shift, alternates)
 //  pt_solve<V>        point minimal solvers in stages: root stage (group_5pt.h /
 //                     group_6pt.h / lane 7pt), tails per root (group_tail.h),
 //                     compaction into model slots
@@ -149,12 +149,6 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (k < ns && md_accept(C, tmp[k])) put(tmp[k]);
-        } else {
-            md_sols_cal_e(x, y, dx, dy, [&](const double (&sol)[6]) {
-                Model m;
-                m.focal0 = m.focal1 = 1.0;
-                if (md_pose_from_sol<3>(x, y, dx, dy, sol, 1.0, 1.0, m) && md_accept(C, m)) put(m);
-            });
         }
     } else {
         double x[4][3], y[4][3], dx[4], dy[4];
@@ -178,115 +172,9 @@ __global__ void __launch_bounds__(64) md_solve_kernel(PairData D, PairConst C, c
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (k < ns && md_accept(C, tmp[k])) put(tmp[k]);
-        } else {
-            auto pose = [&](const double (&sol)[6]) {
-                Model m;
-                const double fa = sol[4], fb = (V == kSF) ? sol[4] : sol[5];
-                m.focal0 = fa;
-                m.focal1 = fb;
-                if (md_pose_from_sol<4>(x, y, dx, dy, sol, fa, fb, m) && md_accept(C, m)) put(m);
-            };
-            if (V == kSF)
-                md_sols_sf_e(x, y, dx, dy, pose);
-            else
-                md_sols_tf_e(x, y, dx, dy, pose);
         }
     }
     counts[b] = n < maxm ? n : maxm;
-}
-
-// The default MD solvers (shift on, no alternates) on 16-lane groups, 4 samples per
-// wave: every lane builds the sample's system (md_setup_*), the resultant's real roots
-// are isolated over the group (group_sturm_roots), and each root is polished, turned
-// into a pose and filtered on its own lane; accepted models are compacted in root
-// order with a group scan, so slots and counts equal md_solve_kernel's.
-template <int V> struct MdGroup;
-template <> struct MdGroup<kCal> {
-    static constexpr int NR = 4, K = 3;
-    using Sys = MdCal;
-};
-template <> struct MdGroup<kSF> {
-    static constexpr int NR = 8, K = 4;
-    using Sys = MdSF;
-};
-template <> struct MdGroup<kTF> {
-    static constexpr int NR = 4, K = 4;
-    using Sys = MdTF;
-};
-
-template <int V>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kCal ? 3 : 2))) md_solve_group_kernel(PairData D, PairConst C, const int *list, int nlist,
-                                                            const int *samples, Model *models, ScoreRec *recs,
-                                                            int *counts, int maxm) {
-    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
-    using G = MdGroup<V>;
-    constexpr int NR = G::NR, K = G::K;
-    __shared__ GroupSturm<NR> st[kGrpPerWg];
-    const int g = threadIdx.x / kGrp, r = threadIdx.x % kGrp;
-    const int idx = blockIdx.x * kGrpPerWg + g;
-    const bool active = idx < nlist;
-    const int b = list[active ? idx : nlist - 1];
-    const int *s = samples + (size_t)b * kSampleStride;
-    double x[K][3], y[K][3], dx[K], dy[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const int i = s[j];
-        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
-        if (V == kCal) {
-            matvec3(C.K0i, xa, x[j]);
-            matvec3(C.K1i, xb, y[j]);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                x[j][q] = xa[q];
-                y[j][q] = xb[q];
-            }
-        }
-        dx[j] = D.d0[i];
-        dy[j] = D.d1[i];
-    }
-    typename G::Sys S;
-    bool ok;
-    double p[NR + 1];
-    if constexpr (V == kCal) {
-        ok = md_setup_cal(x, y, dx, dy, S);
-#pragma unroll
-        for (int k = 0; k <= NR; ++k) p[k] = S.poly[k];
-    } else if constexpr (V == kSF) {
-        ok = md_setup_sf(x, y, dx, dy, S);
-#pragma unroll
-        for (int k = 0; k <= NR; ++k) p[k] = S.R[k];
-    } else {
-        ok = md_setup_tf(x, y, dx, dy, S);
-#pragma unroll
-        for (int k = 0; k <= NR; ++k) p[k] = S.R[k];
-    }
-    double root = 0.0;
-    const bool has = group_sturm_roots<NR>(p, r, st[g], ok, &root);
-    bool keep = false;
-    Model m;
-    if (has) {
-        double sol[6];
-        bool good;
-        if constexpr (V == kCal)
-            good = md_root_cal(S, root, sol);
-        else if constexpr (V == kSF)
-            good = md_root_sf(S, root, sol);
-        else
-            good = md_root_tf(S, root, sol);
-        if (good) {
-            const double fa = sol[4], fb = sol[5];
-            m.focal0 = fa;
-            m.focal1 = fb;
-            keep = md_pose_from_sol<K>(x, y, dx, dy, sol, fa, fb, m) && md_accept(C, m);
-        }
-    }
-    int total;
-    const int pos = gscan(keep ? 1 : 0, &total);
-    if (active) {
-        if (keep && pos < maxm) put_model(C, m, b, pos, maxm, models, recs);
-        if (r == 0) counts[b] = total < maxm ? total : maxm;
-    }
 }
 
 // The MD solvers with the oracle's arithmetic (mp_md_exact.h: setup() = system +
@@ -300,11 +188,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(V == kC
 //         two-focal quartic, whose roots' polish + pose dominate a lane's serial chain
 //         (165 -> 91 us per tf launch, under the 206 us point chain; tf 13.4 -> 12.8 ms
 //         per pair, profiles/r04/mdx4/), R = 2 for the shared-focal octic (below).
-// Accepted models go to their slots in root order, as md_solve_group's.  The
-// calibrated MD solver keeps md_solve_group (57 us): its exact form, 152 us lane per
-// sample and 106 us lane per root, outlasts the 99 us calibrated point chain (cal
-// 5.6-6.7 -> 5.9-6.7 ms per pair with it, profiles/r04/calx/, mdx4/); its parity at the
-// full sizes holds either way.
+// Accepted models go to their slots in root order.  Round 5: the calibrated MD solver
+// runs this kernel too (it ran md_solve_group, a Sturm isolation on 16-lane groups,
+// whose floating-point chain can lose or invent roots on wide-range samples, as it did
+// for sf / tf), and the pose stage of every variant is the oracle's Procrustes with its
+// Jacobi SVD (md_pose_exact), so an MD model is the oracle's to the bit.
 template <int V> struct MdxSys;
 template <> struct MdxSys<kCal> {
     using S = MdxCal;
@@ -356,7 +244,7 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
     auto accept = [&](const double (&sol)[6], Model &m) {
         m.focal0 = sol[4];
         m.focal1 = sol[5];
-        return md_pose_from_sol<K>(x, y, dx, dy, sol, sol[4], sol[5], m) && md_accept(C, m);
+        return md_pose_exact<K>(x, y, dx, dy, sol, sol[4], sol[5], m) && md_accept(C, m);
     };
     if constexpr (R == 1) {
         int n = 0;
@@ -382,15 +270,30 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
             for (int c = 0; c < R; ++c)
                 if (c == r) root = opaque(roots[j * R + c]);
             Model m;
+            double X[K][3], Y[K][3];
             bool keep = false;
             if (active && q < nr) {
                 double sol[6];
-                keep = sys.root(root, sol) && accept(sol, m);
+                if (sys.root(root, sol)) {
+                    m.focal0 = sol[4];
+                    m.focal1 = sol[5];
+                    // whether the solution becomes a model depends on its depths and
+                    // offsets only, so the slot is known before the Procrustes
+                    if (md_pose_points<K>(x, y, dx, dy, sol, sol[4], sol[5], X, Y)) {
+                        m.scale = sol[2];
+                        m.offset0 = sol[1];
+                        m.offset1 = sol[3];
+                        keep = md_accept(C, m);
+                    }
+                }
             }
             const unsigned long long ball = __ballot(keep);
             const unsigned long long mine = (ball >> g0) & ((1ull << R) - 1);
             const int pos = n + __popcll(mine & ((1ull << r) - 1));
-            if (keep && pos < maxm) put_model(C, m, b, pos, maxm, models, recs);
+            if (keep && pos < maxm) {
+                mdx::procrustes<K>(X, Y, m);
+                put_model(C, m, b, pos, maxm, models, recs);
+            }
             n += __popcll(mine);
             if (!__any(active && (j + 1) * R < nr)) break; // (uniform) no sample of the wave has more roots
         }
@@ -797,14 +700,18 @@ __global__ void md_direct_kernel(int variant, int alt, const double *in, double 
             dx[j] = in[18 + j];
             dy[j] = in[21 + j];
         }
-        double sols[4][6];
-        const int ns = md_sols_cal(x, y, dx, dy, sols);
+        double sols[4][6], scr[kMdxScratchCal];
+        int ns = 0;
+        mdx_sols_cal(LaneScratch{scr, 1}, x, y, dx, dy, [&](const double (&sol)[6]) {
+            for (int c = 0; c < 6; ++c) sols[ns][c] = sol[c];
+            ++ns;
+        });
         int np = 0;
         for (int k = 0; k < ns; ++k) {
             for (int c = 0; c < 4; ++c) sols_out[4 * k + c] = sols[k][c];
             Model m;
             m.focal0 = m.focal1 = 1.0;
-            if (md_pose_from_sol<3>(x, y, dx, dy, sols[k], 1.0, 1.0, m)) poses[np++] = m;
+            if (md_pose_exact<3>(x, y, dx, dy, sols[k], 1.0, 1.0, m)) poses[np++] = m;
         }
         *nsols = ns;
         *nposes = np;
@@ -838,7 +745,7 @@ __global__ void md_direct_kernel(int variant, int alt, const double *in, double 
         const double fa = sols[k][4], fb = (variant == kSF) ? sols[k][4] : sols[k][5];
         m.focal0 = fa;
         m.focal1 = fb;
-        if (md_pose_from_sol<4>(x, y, dx, dy, sols[k], fa, fb, m)) poses[np++] = m;
+        if (md_pose_exact<4>(x, y, dx, dy, sols[k], fa, fb, m)) poses[np++] = m;
     }
     *nsols = ns;
     *nposes = np;
@@ -956,38 +863,31 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
     const int grid = (nlist + 63) / 64;
     return by_variant(C.variant, [&](auto V) {
         constexpr int v = decltype(V)::value;
-        // default solvers on 16-lane groups (MADPOSE_MD_LANE: one sample per lane)
-        static const bool lane_md = std::getenv("MADPOSE_MD_LANE") != nullptr;
+        // the default solvers (shift on, no alternates): md_exact, R lanes per sample.
+        // sf: two lanes per sample (the kernel 267 -> 212 us per launch, sf gpu_solve 8.17
+        // -> 7.74 ms per pair; 4 and 8 lanes shortened it further, 190 / 230 us, but
+        // their extra waves slowed the point chain beside it, pt_defl6_grp 80 -> 105 /
+        // 124 us, profiles/r04/mdxr/); tf and cal: one lane per root.
+        // MADPOSE_MDX_R=1|2|4 overrides (results are the same: a lane's arithmetic never
+        // depends on the others; tests/test_switch_invariance_gpu.py)
         const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
-        if constexpr (v == kSF) {
-            if (plain) {
-                // two lanes per sample: the kernel 267 -> 212 us per launch, sf gpu_solve
-                // 8.17 -> 7.74 ms per pair; 4 and 8 lanes shortened it further (190 / 230
-                // us) but their extra waves slowed the point chain beside it (pt_defl6_grp
-                // 80 -> 105 / 124 us), profiles/r04/mdxr/ (MADPOSE_MDX_R=1: one lane)
-                static const bool one = [] {
-                    const char *e = std::getenv("MADPOSE_MDX_R");
-                    return e && e[0] == '1';
-                }();
-                if (one)
-                    md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
-                else
-                    md_exact_kernel<v, 2><<<(nlist + 31) / 32, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
-                                                                           counts, maxm);
-                return hipGetLastError();
-            }
-        } else if constexpr (v == kTF) {
-            if (plain) {
+        if (plain) {
+            static const int r_env = [] {
+                const char *e = std::getenv("MADPOSE_MDX_R");
+                return e ? std::atoi(e) : 0;
+            }();
+            const int r = (r_env == 1 || r_env == 2 || r_env == 4) ? r_env : (v == kSF ? 2 : 4);
+            if (r == 1)
+                md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
+            else if (r == 2)
+                md_exact_kernel<v, 2><<<(nlist + 31) / 32, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
+                                                                       counts, maxm);
+            else
                 md_exact_kernel<v, 4><<<(nlist + 15) / 16, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
                                                                        counts, maxm);
-                return hipGetLastError();
-            }
-        }
-        if (plain && !lane_md) {
-            md_solve_group_kernel<v><<<(nlist + kGrpPerWg - 1) / kGrpPerWg, 64, 0, s>>>(D, C, list, nlist, samples,
-                                                                                     models, recs, counts, maxm);
             return hipGetLastError();
         }
+        // scale-only / no-shift (calibrated) and the use_ours / use_4p4d alternates
         if (C.md_alt != 0)
             md_solve_kernel<decltype(V)::value, true><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs,
                                                                           counts, maxm);

@@ -2,6 +2,7 @@
 #include "la.h"
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <limits>
 
@@ -562,6 +563,130 @@ void jacobi_svd(const Mat &A0, Mat *U, std::vector<double> *s, Mat *V) {
                     for (int i = 0; i < m; ++i) (*U)(i, k) = u[i] / nn;
                     break;
                 }
+            }
+        }
+    }
+}
+
+// Eigen 3.4's two-sided Jacobi SVD as the reference calls it for the MD poses
+// (Eigen::JacobiSVD<Eigen::MatrixXd>(S, ComputeFullU | ComputeFullV), src/solver.cpp:517,
+// :722, :1026; Eigen is not vendored in /root/reference: restated from Eigen 3.4.0
+// JacobiSVD.h compute(), RealSvd2x2.h real_2x2_jacobi_svd and Jacobi.h makeJacobi /
+// apply_rotation_in_the_plane, square real input, no QR preconditioner).  Parity with
+// Eigen itself is unpinned; the device restates this function operation for operation
+// (madpose_amd/csrc/include/mp_md_exact.h mdx::svd3).
+namespace {
+struct Rot {
+    double c, s;
+};
+// rows p, q of the row-major 3 x 3 M: x' = c x + s y, y' = -s x + c y (the identity is a no-op)
+void rot_rows(double *M, int p, int q, Rot j) {
+    if (j.c == 1.0 && j.s == 0.0) return;
+    for (int i = 0; i < 3; ++i) {
+        const double xi = M[3 * p + i], yi = M[3 * q + i];
+        M[3 * p + i] = j.c * xi + j.s * yi;
+        M[3 * q + i] = -j.s * xi + j.c * yi;
+    }
+}
+// columns p, q: MatrixBase::applyOnTheRight(p, q, j) applies j^T = (c, -s) to the columns
+void rot_cols(double *M, int p, int q, Rot j) {
+    const Rot t{j.c, -j.s};
+    if (t.c == 1.0 && t.s == 0.0) return;
+    for (int i = 0; i < 3; ++i) {
+        const double xi = M[3 * i + p], yi = M[3 * i + q];
+        M[3 * i + p] = t.c * xi + t.s * yi;
+        M[3 * i + q] = -t.s * xi + t.c * yi;
+    }
+}
+Rot make_jacobi(double x, double y, double z) {
+    const double deno = 2.0 * std::fabs(y);
+    if (deno < DBL_MIN) return Rot{1.0, 0.0};
+    const double tau = (x - z) / deno;
+    const double w = std::sqrt(tau * tau + 1.0);
+    const double t = tau > 0.0 ? 1.0 / (tau + w) : 1.0 / (tau - w);
+    const double sign_t = t > 0.0 ? 1.0 : -1.0;
+    const double n = 1.0 / std::sqrt(t * t + 1.0);
+    return Rot{n, -sign_t * (y / std::fabs(y)) * std::fabs(t) * n};
+}
+} // namespace
+
+void eigen_jacobi_svd3(const double A[9], double U[9], double V[9]) {
+    const double precision = 2.0 * DBL_EPSILON, consider_zero = DBL_MIN;
+    double scale = 0.0;
+    for (int i = 0; i < 9; ++i) {
+        const double a = std::fabs(A[i]);
+        if (std::isnan(a)) scale = a;
+        else if (!std::isnan(scale)) scale = scale < a ? a : scale;
+    }
+    double W[9];
+    for (int i = 0; i < 9; ++i) U[i] = V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (!std::isfinite(scale)) { // Eigen: InvalidInput, U and V left as they are
+        return;
+    }
+    if (scale == 0.0) scale = 1.0;
+    for (int i = 0; i < 9; ++i) W[i] = A[i] / scale;
+    double max_diag = std::fabs(W[0]);
+    for (int i = 1; i < 3; ++i) max_diag = max_diag < std::fabs(W[4 * i]) ? std::fabs(W[4 * i]) : max_diag;
+    bool finished = false;
+    while (!finished) {
+        finished = true;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                const double pm = precision * max_diag;
+                const double threshold = consider_zero < pm ? pm : consider_zero;
+                if (std::fabs(W[3 * p + q]) > threshold || std::fabs(W[3 * q + p]) > threshold) {
+                    finished = false;
+                    // real_2x2_jacobi_svd on [W(p,p) W(p,q); W(q,p) W(q,q)]
+                    double m00 = W[3 * p + p], m01 = W[3 * p + q], m10 = W[3 * q + p], m11 = W[3 * q + q];
+                    Rot rot1;
+                    const double t = m00 + m11, d = m10 - m01;
+                    if (std::fabs(d) < DBL_MIN) {
+                        rot1 = Rot{1.0, 0.0};
+                    } else {
+                        const double u = t / d;
+                        const double tmp = std::sqrt(1.0 + u * u);
+                        rot1 = Rot{u / tmp, 1.0 / tmp};
+                    }
+                    if (!(rot1.c == 1.0 && rot1.s == 0.0)) { // m.applyOnTheLeft(0, 1, rot1)
+                        const double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
+                        m00 = rot1.c * x0 + rot1.s * y0;
+                        m10 = -rot1.s * x0 + rot1.c * y0;
+                        m01 = rot1.c * x1 + rot1.s * y1;
+                        m11 = -rot1.s * x1 + rot1.c * y1;
+                    }
+                    (void)m10;
+                    const Rot jr = make_jacobi(m00, m01, m11);
+                    // j_left = rot1 * j_right^T, (c1, s1) * (c2, s2) = (c1 c2 - s1 s2, c1 s2 + s1 c2)
+                    const double c2 = jr.c, s2 = -jr.s;
+                    const Rot jl{rot1.c * c2 - rot1.s * s2, rot1.c * s2 + rot1.s * c2};
+                    rot_rows(W, p, q, jl);
+                    rot_cols(U, p, q, Rot{jl.c, -jl.s}); // U.applyOnTheRight(p, q, j_left^T)
+                    rot_cols(W, p, q, jr);
+                    rot_cols(V, p, q, jr);
+                    const double dp = std::fabs(W[3 * p + p]), dq = std::fabs(W[3 * q + q]);
+                    const double m = dp < dq ? dq : dp;
+                    max_diag = max_diag < m ? m : max_diag;
+                }
+            }
+    }
+    double sv[3];
+    for (int i = 0; i < 3; ++i) {
+        const double a = W[4 * i];
+        sv[i] = std::fabs(a);
+        if (a < 0.0)
+            for (int r = 0; r < 3; ++r) U[3 * r + i] = -U[3 * r + i];
+    }
+    for (int i = 0; i < 3; ++i) sv[i] *= scale;
+    for (int i = 0; i < 3; ++i) {
+        int pos = i; // maxCoeff(&pos) over the tail: the first maximum
+        for (int j = i + 1; j < 3; ++j)
+            if (sv[j] > sv[pos]) pos = j;
+        if (sv[pos] == 0.0) break;
+        if (pos != i) {
+            std::swap(sv[i], sv[pos]);
+            for (int r = 0; r < 3; ++r) {
+                std::swap(U[3 * r + i], U[3 * r + pos]);
+                std::swap(V[3 * r + i], V[3 * r + pos]);
             }
         }
     }

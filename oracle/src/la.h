@@ -68,6 +68,9 @@ std::vector<double> poly_real_roots(std::vector<double> c);
 
 // One-sided Jacobi SVD of a small square matrix: A = U diag(s) V^T, s descending.
 void jacobi_svd(const Mat &A, Mat *U, std::vector<double> *s, Mat *V);
+// Eigen 3.4 JacobiSVD<MatrixXd>(A, ComputeFullU | ComputeFullV) of a real 3 x 3 matrix
+// (row-major A, U, V; A = U diag(s) V^T, s descending); see la.cpp
+void eigen_jacobi_svd3(const double A[9], double U[9], double V[9]);
 
 double det3(const double M[9]);
 

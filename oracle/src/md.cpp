@@ -363,20 +363,20 @@ void procrustes(const double *X, const double *Y, int k, double R[9], double t[3
         cx[c] /= k;
         cy[c] /= k;
     }
-    Mat S(3, 3);
+    double S[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < k; ++i)
         for (int a = 0; a < 3; ++a)
-            for (int b = 0; b < 3; ++b) S(a, b) += (Y[3 * i + a] - cy[a]) * (X[3 * i + b] - cx[b]);
-    Mat U, V;
-    std::vector<double> sv;
-    jacobi_svd(S, &U, &sv, &V);
-    double du = det3(U.a.data()), dv = det3(V.a.data());
+            for (int b = 0; b < 3; ++b) S[3 * a + b] += (Y[3 * i + a] - cy[a]) * (X[3 * i + b] - cx[b]);
+    // Eigen::JacobiSVD<MatrixXd>(S, ComputeFullU | ComputeFullV) (src/solver.cpp:517)
+    double U[9], V[9];
+    eigen_jacobi_svd3(S, U, V);
+    double du = det3(U), dv = det3(V);
     if (du * dv < 0)
-        for (int i = 0; i < 3; ++i) U(i, 2) = -U(i, 2);
+        for (int i = 0; i < 3; ++i) U[3 * i + 2] = -U[3 * i + 2];
     for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b) {
             double s = 0;
-            for (int c = 0; c < 3; ++c) s += U(a, c) * V(b, c);
+            for (int c = 0; c < 3; ++c) s += U[3 * a + c] * V[3 * b + c];
             R[3 * a + b] = s;
         }
     for (int a = 0; a < 3; ++a) t[a] = cy[a] - (R[3 * a] * cx[0] + R[3 * a + 1] * cx[1] + R[3 * a + 2] * cx[2]);

@@ -1,5 +1,6 @@
-"""The shared-/two-focal (and calibrated) MD solvers of mp_md_exact.h against the oracle,
-bit for bit, on the CPU: the header is compiled for the host by clang with FMA
+"""The calibrated, shared- and two-focal MD solvers of mp_md_exact.h and their pose stage
+(md_pose_exact: the oracle's Procrustes with its Jacobi SVD) against the oracle, bit for
+bit, on the CPU: the header is compiled for the host by clang with FMA
 available (-march=x86-64-v3) and contraction off by the header's own pragmas, behind
 the C ABI of tests/md_exact_check.cpp.  Equal solution lists (count, order, every
 double) for random samples, for samples whose resultant's roots span several orders
@@ -41,12 +42,20 @@ def mdx(tmp_path_factory):
     assert r.returncode == 0, r.stderr[-4000:]
     lib = ctypes.CDLL(so)
     lib.mdx_check_solve.restype = ctypes.c_int
+    lib.mdx_check_pose.restype = ctypes.c_int
 
     def solve(v, x, y, dx, dy):
         a = [np.ascontiguousarray(t, dtype=np.float64) for t in (x, y, dx, dy)]
         out = np.zeros(48)
         n = lib.mdx_check_solve(v, *[t.ctypes.data_as(_dp) for t in a], out.ctypes.data_as(_dp))
         return out[:6 * n].reshape(n, 6)[:, :[4, 5, 6][v]]
+
+    def pose(v, x, y, dx, dy):
+        a = [np.ascontiguousarray(t, dtype=np.float64) for t in (x, y, dx, dy)]
+        out = np.zeros(8 * 17)
+        n = lib.mdx_check_pose(v, *[t.ctypes.data_as(_dp) for t in a], out.ctypes.data_as(_dp))
+        return out[:17 * n].reshape(n, 17)
+    solve.pose = pose
     return solve
 
 
@@ -55,9 +64,20 @@ def _oracle(v, x, y, dx, dy):
     return s.reshape(-1, [4, 5, 6][v])
 
 
+def oracle_poses(v, x, y, dx, dy):
+    """The oracle's md_pose models as rows of 17 doubles (mp_model layout)."""
+    rows = []
+    for m in oracle.md_pose(v, x, y, dx, dy):
+        f0, f1 = (1.0, 1.0) if v == 0 else (m["focal0"], m["focal1"])
+        rows.append(np.r_[m["R"].ravel(), m["t"], m["scale"], m["offset0"], m["offset1"], f0, f1])
+    return np.asarray(rows, dtype=np.float64).reshape(-1, 17)
+
+
 def _check(mdx, v, x, y, dx, dy):
     a, b = mdx(v, x, y, dx, dy), _oracle(v, x, y, dx, dy)
     assert a.shape == b.shape and np.array_equal(a, b), (v, a, b)
+    pa, pb = mdx.pose(v, x, y, dx, dy), oracle_poses(v, x, y, dx, dy)
+    assert pa.shape == pb.shape and np.array_equal(pa, pb), (v, pa, pb)
     return len(a)
 
 
@@ -73,17 +93,21 @@ def test_random_samples_bit_exact(mdx, variant):
     assert total > 1000  # solutions were found and compared
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_wide_root_range_bit_exact(mdx, variant):
+def wide_range_sample(rng, k):
     """Depths spread over several orders of magnitude and nearly collinear points: the
     resultant's roots then span many decades (the Sturm chain's failure class)."""
+    x = np.c_[rng.standard_normal((k, 2)) * 10.0 ** rng.uniform(-3, 1), np.ones(k)]
+    y = np.c_[x[:, :2] + rng.standard_normal((k, 2)) * 10.0 ** rng.uniform(-4, 0), np.ones(k)]
+    return x, y, 10.0 ** rng.uniform(-2, 3, k), 10.0 ** rng.uniform(-2, 3, k)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_wide_root_range_bit_exact(mdx, variant):
     rng = np.random.default_rng(50 + variant)
+    total = 0
     for _ in range(3000):
-        x = np.c_[rng.standard_normal((4, 2)) * 10.0 ** rng.uniform(-3, 1), np.ones(4)]
-        y = np.c_[x[:, :2] + rng.standard_normal((4, 2)) * 10.0 ** rng.uniform(-4, 0), np.ones(4)]
-        dx = 10.0 ** rng.uniform(-2, 3, 4)
-        dy = 10.0 ** rng.uniform(-2, 3, 4)
-        _check(mdx, variant, x, y, dx, dy)
+        total += _check(mdx, variant, *wide_range_sample(rng, 3 if variant == 0 else 4))
+    assert total > 300
 
 
 def test_estimator_diag_samples_bit_exact(mdx):

@@ -2,7 +2,8 @@
 and four pairs in flight, each switch setting in a fresh process (the engine reads them
 once), compared field by field with the default run to the last bit -- the early
 continuation on while alone and always (MADPOSE_EARLY_CONT, §2 step 7 of DESIGN.md), the
-shared-focal exact MD on one lane per sample instead of two (MADPOSE_MDX_R), the scalar
+exact MD solvers on one or two lanes per sample instead of the defaults (MADPOSE_MDX_R; cal
+and tf 4, sf 2), the scalar
 batch drawing instead of AVX-512 (MADPOSE_SAMPLER_SIMD), the 15x15 QR packed 16
 samples per wave instead of one sample per wave (MADPOSE_EIG_WAVES), and the
 draw-by-draw sampler (MADPOSE_SAMPLER_TWO_PASS)."""
@@ -19,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "switch_worker.py")
 SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOSE_EARLY_CONT": "2"},
-            "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
+            "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "mdx_two_lanes": {"MADPOSE_MDX_R": "2"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
             "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"}}
 
 
