@@ -147,13 +147,26 @@ int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, 
  * calibrated / shared-focal / two-focal variant, problem units), counts[b] of them
  * used by iteration b.  best: the pre-batch best; flags: 1 the exact early exit
  * against it, 2 the record skip.  Outputs per iteration: res_best, res_slot (bit 16:
- * another model within the tie margin), rec_models[b] (the mapped record model,
- * written when res_best[b] < best + tie); tie: the margin used. */
+ * another model's screening interval reaches the best's; bit 17: a correspondence
+ * outside the margins' cover was flagged), rec_models[b] (the mapped record model,
+ * written when the iteration could hold a new best), res_hi_lo (nullable, 2 per
+ * iteration: best + its margin, min over models of score - margin), model_ties
+ * (nullable, num_iterations x M: each model's screening margin). */
 int mp_debug_score_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
                          const double *d1, const double *cam0, const double *cam1, const mp_ransac_options *options,
                          const mp_estimator_config *config, int32_t num_iterations, const int32_t *counts,
                          const mp_model *models, double best, int32_t flags, double *res_best, int32_t *res_slot,
-                         mp_model *rec_models, double *tie, int device);
+                         mp_model *rec_models, double *res_hi_lo, double *model_ties, int device);
+
+/* mp_debug_score_terms: score_batch's residual evaluation of explicit models, per
+ * correspondence -- test hook of the screening margins.  errors: num_models x 3 x n
+ * (reprojection 0 -> 1, 1 -> 0, Sampson; the score kernel's own forms and gating);
+ * flags: num_models x n (1: the correspondence lies outside the margins' cover); taus
+ * (nullable): num_models x 3 per-term bounds; ties (nullable): each model's margin. */
+int mp_debug_score_terms(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                         const double *d1, const double *cam0, const double *cam1, const mp_ransac_options *options,
+                         const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *errors,
+                         int32_t *flags, double *taus, double *ties, int device);
 
 /* mp_debug_lo_sweep: the same models through the engine's host LO sweep
  * (madpose_amd/csrc/host/lo_sweep.h), the sweep LocalOptimization and

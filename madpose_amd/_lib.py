@@ -154,7 +154,13 @@ EXPORTS = {
                                             c_double_p, c_double_p, c_double_p, ctypes.POINTER(mp_ransac_options),
                                             ctypes.POINTER(mp_estimator_config), ctypes.c_int32, c_int32_p,
                                             ctypes.POINTER(mp_model), ctypes.c_double, ctypes.c_int32, c_double_p,
-                                            c_int32_p, ctypes.POINTER(mp_model), c_double_p, ctypes.c_int]),
+                                            c_int32_p, ctypes.POINTER(mp_model), c_double_p, c_double_p,
+                                            ctypes.c_int]),
+    "mp_debug_score_terms": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p,
+                                            c_double_p, c_double_p, c_double_p, ctypes.POINTER(mp_ransac_options),
+                                            ctypes.POINTER(mp_estimator_config), ctypes.POINTER(mp_model),
+                                            ctypes.c_int32, c_double_p, c_int32_p, c_double_p, c_double_p,
+                                            ctypes.c_int]),
     "mp_debug_lo_sweep": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p, c_double_p,
                                          c_double_p, c_double_p, ctypes.POINTER(mp_ransac_options),
                                          ctypes.POINTER(mp_estimator_config), ctypes.POINTER(mp_model), ctypes.c_int32,

@@ -698,7 +698,9 @@ def debug_score_batch(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_
                       exit=True, record_skip=True):
     """The estimator's scoring kernel on explicit per-iteration model lists (test hook,
     mp_debug_score_batch).  iterations: list of model lists (problem units).  Returns
-    (best scores, slots with the ambiguity bit, record models, tie margin)."""
+    (best scores, slots with the ambiguity / uncertainty bits, record models, bounds):
+    bounds["hi"], bounds["lo"] per iteration and bounds["tie"][b][m], each model's
+    screening margin (mp_score.h score_margins)."""
     x0 = _pts(x0, "x0")
     x1 = _pts(x1, "x1")
     n = x0.shape[0]
@@ -717,15 +719,46 @@ def debug_score_batch(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_
     rb = np.zeros(B)
     rs = np.zeros(B, dtype=np.int32)
     rec = (L.mp_model * B)()
-    tie = ctypes.c_double(0.0)
+    hilo = np.zeros(2 * B)
+    ties = np.zeros(B * M)
     o = options._to_c()
     c = (est_config or EstimatorConfig())._to_c()
     flags = (1 if exit else 0) | (2 if record_skip else 0)
     L.check(L.lib().mp_debug_score_batch(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1),
                                          ctypes.byref(o), ctypes.byref(c), B, counts.ctypes.data_as(L.c_int32_p),
                                          arr, float(best), flags, _dp(rb), rs.ctypes.data_as(L.c_int32_p), rec,
-                                         ctypes.byref(tie), _DEFAULT_DEVICE))
-    return rb, rs, [_model_from_c(rec[b], variant) for b in range(B)], tie.value
+                                         _dp(hilo), _dp(ties), _DEFAULT_DEVICE))
+    bounds = {"hi": hilo[0::2].copy(), "lo": hilo[1::2].copy(),
+              "tie": [ties[b * M:b * M + counts[b]].copy() for b in range(B)]}
+    return rb, rs, [_model_from_c(rec[b], variant) for b in range(B)], bounds
+
+
+def debug_score_terms(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, models):
+    """score_batch's per-correspondence errors of explicit models (test hook,
+    mp_debug_score_terms).  Returns (errors [nm x 3 x n], flags [nm x n], taus [nm x 3],
+    ties [nm])."""
+    x0 = _pts(x0, "x0")
+    x1 = _pts(x1, "x1")
+    n = x0.shape[0]
+    d0 = _vec(depth0, n, "depth0")
+    d1 = _vec(depth1, n, "depth1")
+    c0 = np.ascontiguousarray(np.asarray(cam0, dtype=np.float64).reshape(-1))
+    c1 = np.ascontiguousarray(np.asarray(cam1, dtype=np.float64).reshape(-1))
+    nm = len(models)
+    arr = (L.mp_model * max(nm, 1))()
+    for m, mod in enumerate(models):
+        arr[m] = _model_to_c(mod, variant)
+    err = np.zeros(max(nm, 1) * 3 * n)
+    flags = np.zeros(max(nm, 1) * n, dtype=np.int32)
+    taus = np.zeros(max(nm, 1) * 3)
+    ties = np.zeros(max(nm, 1))
+    o = options._to_c()
+    c = (est_config or EstimatorConfig())._to_c()
+    L.check(L.lib().mp_debug_score_terms(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1),
+                                         ctypes.byref(o), ctypes.byref(c), arr, nm, _dp(err),
+                                         flags.ctypes.data_as(L.c_int32_p), _dp(taus), _dp(ties), _DEFAULT_DEVICE))
+    return (err[:nm * 3 * n].reshape(nm, 3, n), flags[:nm * n].reshape(nm, n), taus[:3 * nm].reshape(nm, 3),
+            ties[:nm])
 
 
 def device_count():

@@ -279,30 +279,44 @@ int mp_solve_scale_shift_pose_alt(int variant, int alt, const double *x_homo, co
     return r <= -1000 ? -(r + 1000) : -r;
 }
 
-int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
-                    const double *cam0, const double *cam1, const mp_ransac_options *options,
-                    const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
-                    double *errors, int device) {
+extern "C++" {
+namespace {
+// the shared argument handling of mp_score_models and mp_debug_lo_sweep: `sweep`
+// receives the pair, the converted options and the models
+template <class F>
+int with_models(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
+                const double *cam0, const double *cam1, const mp_ransac_options *options,
+                const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
+                F &&sweep) {
     return guarded([&]() {
         if (!options || !models || !scores || num_models < 0) throw std::invalid_argument("bad arguments");
         const double md[2] = {0.0, 0.0};
         mp::PairInput in = make_input(variant, n, x0, x1, d0, d1, md, cam0, cam1);
         std::vector<mp::Model> ms(num_models);
         std::memcpy(ms.data(), models, sizeof(mp_model) * num_models);
-        if (device == -1000) // mp_debug_lo_sweep
-            mp::lo_sweep_models(in, to_opts(options), to_cfg(config), ms.data(), num_models, scores, errors);
-        else
-            mp::score_models(in, to_opts(options), to_cfg(config), ms.data(), num_models, scores, errors, device,
-                             nullptr);
+        sweep(in, to_opts(options), to_cfg(config), ms);
         return MP_OK;
     });
+}
+} // namespace
+} // extern "C++"
+
+int mp_score_models(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
+                    const double *cam0, const double *cam1, const mp_ransac_options *options,
+                    const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
+                    double *errors, int device) {
+    return with_models(variant, n, x0, x1, d0, d1, cam0, cam1, options, config, models, num_models, scores,
+                       [&](const mp::PairInput &in, const mp::RansacOptions &o, const mp::EstimatorConfig &c,
+                           std::vector<mp::Model> &ms) {
+                           mp::score_models(in, o, c, ms.data(), num_models, scores, errors, device, nullptr);
+                       });
 }
 
 int mp_debug_score_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
                          const double *d1, const double *cam0, const double *cam1, const mp_ransac_options *options,
                          const mp_estimator_config *config, int32_t num_iterations, const int32_t *counts,
                          const mp_model *models, double best, int32_t flags, double *res_best, int32_t *res_slot,
-                         mp_model *rec_models, double *tie, int device) {
+                         mp_model *rec_models, double *res_hi_lo, double *model_ties, int device) {
     return guarded([&]() {
         if (!options || !counts || !models || !res_best || !res_slot || num_iterations <= 0)
             throw std::invalid_argument("bad arguments");
@@ -312,9 +326,25 @@ int mp_debug_score_batch(int variant, int64_t n, const double *x0, const double 
         std::vector<mp::Model> ms((size_t)num_iterations * maxm), rm(num_iterations);
         std::memcpy(ms.data(), models, sizeof(mp_model) * ms.size());
         mp::debug_score_batch(in, to_opts(options), to_cfg(config), num_iterations, counts, ms.data(), best, flags,
-                              res_best, res_slot, rm.data(), tie, device);
+                              res_best, res_slot, rm.data(), res_hi_lo, model_ties, device);
         if (rec_models)
             for (int b = 0; b < num_iterations; ++b) to_model(rm[b], &rec_models[b]);
+        return MP_OK;
+    });
+}
+
+int mp_debug_score_terms(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                         const double *d1, const double *cam0, const double *cam1, const mp_ransac_options *options,
+                         const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *errors,
+                         int32_t *flags, double *taus, double *ties, int device) {
+    return guarded([&]() {
+        if (!options || !models || !errors || !flags || num_models < 0) throw std::invalid_argument("bad arguments");
+        const double md[2] = {0.0, 0.0};
+        mp::PairInput in = make_input(variant, n, x0, x1, d0, d1, md, cam0, cam1);
+        std::vector<mp::Model> ms(num_models);
+        std::memcpy(ms.data(), models, sizeof(mp_model) * num_models);
+        mp::debug_score_terms(in, to_opts(options), to_cfg(config), ms.data(), num_models, errors, flags, taus, ties,
+                              device);
         return MP_OK;
     });
 }
@@ -323,15 +353,22 @@ int mp_debug_lo_sweep(int variant, int64_t n, const double *x0, const double *x1
                       const double *cam0, const double *cam1, const mp_ransac_options *options,
                       const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
                       double *errors) {
-    return mp_score_models(variant, n, x0, x1, d0, d1, cam0, cam1, options, config, models, num_models, scores, errors,
-                           -1000);
+    return with_models(variant, n, x0, x1, d0, d1, cam0, cam1, options, config, models, num_models, scores,
+                       [&](const mp::PairInput &in, const mp::RansacOptions &o, const mp::EstimatorConfig &c,
+                           std::vector<mp::Model> &ms) {
+                           mp::lo_sweep_models(in, o, c, ms.data(), num_models, scores, errors);
+                       });
 }
 
-int mp_lm_refine_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
-                       const double *d1, const double *min_depth, const double *cam0, const double *cam1,
-                       const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
-                       const int32_t *kinds, const int64_t *sample_offsets, const int32_t *sample_idx,
-                       mp_model *models, int32_t *status, int device) {
+extern "C++" {
+namespace {
+// the shared argument handling of mp_lm_refine_batch and mp_debug_lm_refine_host
+template <class F>
+int with_lm_problems(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
+                     const double *min_depth, const double *cam0, const double *cam1,
+                     const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
+                     const int64_t *sample_offsets, const int32_t *sample_idx, mp_model *models, int32_t *status,
+                     F &&refine) {
     return guarded([&]() {
         if (!options || num_problems < 0 || (num_problems > 0 && (!sample_offsets || !models || !status)))
             throw std::invalid_argument("bad arguments");
@@ -341,15 +378,26 @@ int mp_lm_refine_batch(int variant, int64_t n, const double *x0, const double *x
         mp::PairInput in = make_input(variant, n, x0, x1, d0, d1, min_depth ? min_depth : md0, cam0, cam1);
         std::vector<mp::Model> ms(num_problems);
         std::memcpy(ms.data(), models, sizeof(mp_model) * num_problems);
-        if (device == -1000) // mp_debug_lm_refine_host
-            mp::lm_refine_batch_host(in, to_opts(options), to_cfg(config), num_problems, kinds, sample_offsets,
-                                     sample_idx, ms.data(), status);
-        else
-            mp::lm_refine_batch_device(in, to_opts(options), to_cfg(config), num_problems, kinds, sample_offsets,
-                                       sample_idx, ms.data(), status, device);
+        refine(in, to_opts(options), to_cfg(config), ms);
         for (int j = 0; j < num_problems; ++j) to_model(ms[j], &models[j]);
         return MP_OK;
     });
+}
+} // namespace
+} // extern "C++"
+
+int mp_lm_refine_batch(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
+                       const double *d1, const double *min_depth, const double *cam0, const double *cam1,
+                       const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
+                       const int32_t *kinds, const int64_t *sample_offsets, const int32_t *sample_idx,
+                       mp_model *models, int32_t *status, int device) {
+    return with_lm_problems(variant, n, x0, x1, d0, d1, min_depth, cam0, cam1, options, config, num_problems,
+                            sample_offsets, sample_idx, models, status,
+                            [&](const mp::PairInput &in, const mp::RansacOptions &o, const mp::EstimatorConfig &c,
+                                std::vector<mp::Model> &ms) {
+                                mp::lm_refine_batch_device(in, o, c, num_problems, kinds, sample_offsets, sample_idx,
+                                                           ms.data(), status, device);
+                            });
 }
 
 int mp_debug_lm_refine_host(int variant, int64_t n, const double *x0, const double *x1, const double *d0,
@@ -357,8 +405,13 @@ int mp_debug_lm_refine_host(int variant, int64_t n, const double *x0, const doub
                             const mp_ransac_options *options, const mp_estimator_config *config, int32_t num_problems,
                             const int32_t *kinds, const int64_t *sample_offsets, const int32_t *sample_idx,
                             mp_model *models, int32_t *status) {
-    return mp_lm_refine_batch(variant, n, x0, x1, d0, d1, min_depth, cam0, cam1, options, config, num_problems, kinds,
-                              sample_offsets, sample_idx, models, status, -1000);
+    return with_lm_problems(variant, n, x0, x1, d0, d1, min_depth, cam0, cam1, options, config, num_problems,
+                            sample_offsets, sample_idx, models, status,
+                            [&](const mp::PairInput &in, const mp::RansacOptions &o, const mp::EstimatorConfig &c,
+                                std::vector<mp::Model> &ms) {
+                                mp::lm_refine_batch_host(in, o, c, num_problems, kinds, sample_offsets, sample_idx,
+                                                         ms.data(), status);
+                            });
 }
 
 static int point_direct(int kind, const double *x1, const double *x2, mp_model *out, int max_out, int device) {

@@ -572,6 +572,52 @@ LmJob make_lm_job(const Problem &P, const EstimatorConfig &cfg, const int *sizes
     return J;
 }
 
+// The pair's magnitudes behind the screening margins (PairConst::ea.., mp_score.h
+// score_margins): maxima of the rays' absolute sums, depths and coordinates.
+void pair_magnitudes(PairConst &C, const HostPair &H) {
+    const bool cal = C.variant == kCal;
+    double ea = 0, eap = 0, exi = 0, eb = 0, ebp = 0, exj = 0, ed0 = 0, ed1 = 0, ex0 = 0, ex1 = 0;
+    for (int i = 0; i < H.n; ++i) {
+        const double u0 = H.x0[2 * i], v0 = H.x0[2 * i + 1], u1 = H.x1[2 * i], v1 = H.x1[2 * i + 1];
+        ex0 = std::max(ex0, std::max(std::fabs(u0), std::fabs(v0)));
+        ex1 = std::max(ex1, std::max(std::fabs(u1), std::fabs(v1)));
+        ed0 = std::max(ed0, std::fabs(H.d0[i]));
+        ed1 = std::max(ed1, std::fabs(H.d1[i]));
+        if (cal) {
+            auto ray = [](const double *Ki, double u, double v, double *abs1, double *absp, double *xi) {
+                double a[3], p = 0.0;
+                for (int j = 0; j < 3; ++j) {
+                    a[j] = Ki[3 * j] * u + Ki[3 * j + 1] * v + Ki[3 * j + 2];
+                    p += std::fabs(Ki[3 * j] * u) + std::fabs(Ki[3 * j + 1] * v) + std::fabs(Ki[3 * j + 2]);
+                }
+                *abs1 = std::max(*abs1, std::fabs(a[0]) + std::fabs(a[1]) + std::fabs(a[2]));
+                *absp = std::max(*absp, p);
+                *xi = std::max(*xi, p / (std::fabs(a[0]) + std::fabs(a[1]) + 1.0));
+            };
+            ray(C.K0i, u0, v0, &ea, &eap, &exi);
+            ray(C.K1i, u1, v1, &eb, &ebp, &exj);
+        } else {
+            ea = std::max(ea, std::fabs(u0) + std::fabs(v0));
+            eb = std::max(eb, std::fabs(u1) + std::fabs(v1));
+        }
+    }
+    if (!cal) {
+        eap = ea;
+        ebp = eb;
+    }
+    // (a NaN coordinate makes every margin NaN, i.e. infinite: no screening)
+    C.ea = ea * (1 + 1e-12);
+    C.eap = eap * (1 + 1e-12);
+    C.exi = exi * (1 + 1e-12);
+    C.eb = eb * (1 + 1e-12);
+    C.ebp = ebp * (1 + 1e-12);
+    C.exj = exj * (1 + 1e-12);
+    C.ed0 = ed0;
+    C.ed1 = ed1;
+    C.ex0 = ex0;
+    C.ex1 = ex1;
+}
+
 Problem make_problem(const PairInput &in, const RansacOptions &o, const EstimatorConfig &cfg) {
     // no FMA contraction: the normalization scale (and with it every normalized
     // coordinate the MD solvers see) is the oracle's to the bit (estimator.cpp:88-103)
@@ -638,6 +684,11 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
         thr1 /= scale * scale;
         for (int i = 0; i < 9; ++i) C.K0[i] = C.K1[i] = C.K0i[i] = C.K1i[i] = (i % 4 == 0) ? 1.0 : 0.0;
         C.loss_scale = 1.0;
+    }
+    pair_magnitudes(C, H);
+    {
+        const char *ts = std::getenv("MADPOSE_TIE_SCALE");
+        C.tie_scale = ts ? std::max(1.0, std::atof(ts)) : 1.0;
     }
     std::memcpy(H.K0, C.K0, sizeof(H.K0));
     std::memcpy(H.K1, C.K1, sizeof(H.K1));
@@ -720,10 +771,6 @@ class Run {
         const char *env3 = std::getenv("MADPOSE_BATCH_GROWTH");
         growth_ = env3 ? std::max(0.01, std::atof(env3)) : (variant_ == kSF ? 2.0 : 1.0);
         trace_ = std::getenv("MADPOSE_TRACE") != nullptr;
-        double M = 0.0;
-        for (int t = 0; t < 3; ++t) M += P.C.thr[t] * std::fabs(P.C.w[t]);
-        const char *ts = std::getenv("MADPOSE_TIE_SCALE");
-        tie_ = 4e-12 * std::max(n_, 64) * M * (ts ? std::max(1.0, std::atof(ts)) : 1.0);
     }
 
     void run(Model *best, Stats *S);
@@ -740,19 +787,20 @@ class Run {
     int max_batch_, min_batch_;
     double growth_; // batch = growth_ x iterations so far (MADPOSE_BATCH_GROWTH)
     bool trace_ = false;
-    // Tie margin: an absolute bound on |device score_batch sum - reference-order sum| of
-    // one model.  Every MSAC term is min(e, thr_t) w_t with e >= 0, so |term| <=
-    // thr_t |w_t| and a sum has |terms| <= M = n (thr_0 |w_0| + thr_1 |w_1| + thr_2 |w_2|);
-    // either summation order is within gamma_{3n} M ~ 3n eps M of the exact sum and the
-    // two residual forms differ by a few ulp per term, so the margin 4e-12 M holds for
-    // n up to ~5000 with room (it is the bound the early exit, the record skip and the
-    // host's near-tie resolution use).  MADPOSE_TIE_SCALE multiplies it (tests force the
+    // New bests are decided on reference-order sums (exact_score); score_batch's sums
+    // screen with per-model margins (ScoreRec::tie, mp_score.h score_margins: |device
+    // sum - reference-order sum| <= tie unless the iteration is flagged uncertain), see
+    // the walk in run().  MADPOSE_TIE_SCALE multiplies every margin (tests force the
     // resolution path with a large factor).
-    double tie_ = 0.0;
     uint64_t tie_checks_ = 0;
     // MADPOSE_COUNT_DUMP=<file>: one line per walked iteration (iteration, solver type,
     // model count, the solver's sample) -- a diagnostic (tools/diag_counts.py)
     FILE *count_dump_ = nullptr;
+    // MADPOSE_MODEL_DUMP=<file>: per walked iteration (int32 iteration, int32 model count,
+    // the models as 17 doubles each, problem units) -- the oracle replays them
+    // (ORACLE_MODEL_REPLAY, oracle/src/ransac.cpp) to separate the selection logic from
+    // the solvers' rounding (tests/test_ties_gpu.py)
+    FILE *model_dump_ = nullptr;
     PairData D_;
     Stats *S_ = nullptr;
     IterationStream rs_; // sampler + selection/LO streams
@@ -1270,7 +1318,7 @@ class Run {
         if (prof) MP_HIP(hipEventRecord(Q.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
         Q.epoch_hi = epoch_hi;
-        MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.d_res, best, tie_,
+        MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.d_res, best,
                                   prof ? Q.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
                                   Q.d_models, Q.d_recmodel));
         if (prof) MP_HIP(hipEventRecord(Q.ev[2], s));
@@ -1292,26 +1340,36 @@ class Run {
     // a new best starts with a sweep of the same model and finds it cached.
     double exact_score(const Model &m) { return score(lanes_[0], m); }
 
-    // Iteration j of the last batch could hold a new best but its device best is within
-    // the tie margin of best_min_score, or another of its models is within the margin of
-    // its best: re-score the contenders in the reference's order and take the first
-    // minimum (GetBestEstimatedModelId, src/hybrid_ransac.h:245-263).  Models whose
-    // device score is more than the margin above the device best cannot be the exact
-    // winner.  Rare (tests/test_engine_gpu.py::test_tie_margin_inflated forces it).
+    // Iteration j of the last batch could hold a new best but it is not certain which of
+    // its models wins in the reference order: its best's interval [S - T, S + T] reaches
+    // another model's (kSlotAmbiguous), best_min_score lies inside it, or the iteration
+    // is uncertain (a flagged correspondence: no margin holds, every model is a
+    // contender).  Re-score the contenders in the reference's order and take the first
+    // minimum (GetBestEstimatedModelId, src/hybrid_ransac.h:245-263); a model whose lower
+    // bound S - T exceeds the smallest upper bound of the iteration cannot be the
+    // reference's winner.  Rare (tests/test_ties_gpu.py forces it).
     void resolve_tie(const BatchBufs &Q, uint32_t j, Model *out, double *out_score) {
         const int nm = Q.h_res[j].count;
-        const double bl = Q.h_res[j].best;
+        const bool uncertain = (Q.h_res[j].slot & kSlotUncertain) != 0;
         std::vector<double> dsc(nm);
         std::vector<Model> ms(nm);
+        std::vector<ScoreRec> rc(nm);
         // (the batch is complete; the main stream may already hold the next one)
         MP_HIP(hipMemcpyAsync(dsc.data(), Q.d_scores + (size_t)j * maxm_, sizeof(double) * nm,
                               hipMemcpyDeviceToHost, X_.copy_stream));
         MP_HIP(hipMemcpyAsync(ms.data(), Q.d_models + (size_t)j * maxm_, sizeof(Model) * nm, hipMemcpyDeviceToHost,
                               X_.copy_stream));
+        MP_HIP(hipMemcpyAsync(rc.data(), Q.d_recs + (size_t)j * maxm_, sizeof(ScoreRec) * nm, hipMemcpyDeviceToHost,
+                              X_.copy_stream));
         MP_HIP(hipStreamSynchronize(X_.copy_stream));
+        double hi_min = kMax; // the smallest upper bound of a model's reference-order score
+        for (int m = 0; m < nm; ++m)
+            if (dsc[m] < kMax) hi_min = std::min(hi_min, dsc[m] + rc[m].tie);
         *out_score = kMax;
         for (int m = 0; m < nm; ++m) {
-            if (!(dsc[m] < kMax) || !(dsc[m] <= bl + tie_)) continue;
+            // (a model the exit killed reports DBL_MAX: its reference sum reached the
+            // pre-batch best, it cannot win)
+            if (!uncertain && (!(dsc[m] < kMax) || dsc[m] - rc[m].tie > hi_min)) continue;
             const double e = exact_score(ms[m]);
             if (e < *out_score) { // strict '<': the first minimum wins
                 *out_score = e;
@@ -1331,6 +1389,9 @@ void Run::run(Model *best, Stats *S) {
     const char *dump_path = std::getenv("MADPOSE_COUNT_DUMP");
     std::unique_ptr<FILE, int (*)(FILE *)> dump(dump_path ? std::fopen(dump_path, "w") : nullptr, &std::fclose);
     count_dump_ = dump.get();
+    const char *mdump_path = std::getenv("MADPOSE_MODEL_DUMP");
+    std::unique_ptr<FILE, int (*)(FILE *)> mdump(mdump_path ? std::fopen(mdump_path, "wb") : nullptr, &std::fclose);
+    model_dump_ = mdump.get();
     S_ = S;
     *S = Stats();
     S->best_model_score = kMax;
@@ -1510,6 +1571,13 @@ void Run::run(Model *best, Stats *S) {
             g_prof.score_ms += ms_score;
         }
 
+        std::vector<Model> dumped;
+        if (model_dump_) {
+            dumped.resize((size_t)B * maxm_);
+            MP_HIP(hipMemcpyAsync(dumped.data(), Q.d_models, sizeof(Model) * dumped.size(), hipMemcpyDeviceToHost,
+                                  X_.copy_stream));
+            MP_HIP(hipStreamSynchronize(X_.copy_stream));
+        }
         bool invalidated = false;
         bool spec = false; // the sampler holds the post-LO speculation, not the Bn batch
         uint64_t spec_draws = 0;
@@ -1520,6 +1588,11 @@ void Run::run(Model *best, Stats *S) {
             S->num_iterations_per_solver[st] += 1;
             const int nm = Q.h_res[j].count;
             S->num_hypotheses += (uint64_t)nm;
+            if (model_dump_) {
+                const int32_t hdr[2] = {(int32_t)iter, (int32_t)nm};
+                std::fwrite(hdr, sizeof(hdr), 1, model_dump_);
+                std::fwrite(dumped.data() + (size_t)j * maxm_, sizeof(Model), (size_t)nm, model_dump_);
+            }
             if (count_dump_) {
                 const int *smp = slot_ptr(g.slot) + 8 * (size_t)j;
                 std::fprintf(count_dump_, "%u %d %d", iter, st, nm);
@@ -1529,18 +1602,21 @@ void Run::run(Model *best, Stats *S) {
             bool lo_here = false;
             if (nm > 0) {
                 // The device sums screen; the decision is taken on reference-order sums
-                // (exact_score) -- see tie_margin.  `maybe`: the iteration could hold a new
-                // best; `certain`: it does, and its best model is unambiguous.
+                // (exact_score) -- see resolve_tie.  `maybe`: the iteration could hold a new
+                // best (some model's lower bound is below the running best, or no bound
+                // holds); `certain`: it does, and its best model is the reference's winner.
                 const double bl = Q.h_res[j].best;
                 const int raw = Q.h_res[j].slot;
-                const bool maybe = best_min_score == kMax ? bl < kMax : bl < best_min_score + tie_;
+                const bool uncertain = (raw & kSlotUncertain) != 0;
+                const bool maybe = uncertain || (best_min_score == kMax ? bl < kMax : Q.h_res[j].lo < best_min_score);
                 if (maybe || iter == lo_start) {
                     bool new_best = false;
                     if (maybe) {
-                        const bool certain = best_min_score == kMax || bl < best_min_score - tie_;
+                        const bool certain = !uncertain && !(raw & kSlotAmbiguous) &&
+                                             (best_min_score == kMax || Q.h_res[j].hi < best_min_score);
                         Model m;
                         double e = kMax;
-                        if (certain && !(raw & kSlotAmbiguous)) {
+                        if (certain) {
                             m = fetch_model(Q, (int)j);
                             e = exact_score(m);
                         } else {
@@ -1776,6 +1852,34 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
     MP_HIP(hipStreamSynchronize(X.stream));
 }
 
+// score_batch's per-correspondence errors and flags of explicit models, with each
+// model's per-term bounds and margin (mp_debug_score_terms; test hook of the screening
+// margins, mp_score.h score_margins)
+void debug_score_terms(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
+                       int nm, double *errors, int *flags, double *taus, double *ties, int device) {
+    validate(in, opts);
+    if (nm <= 0) return;
+    CtxLease lease(device);
+    DeviceCtx &X = *lease.c;
+    Problem P = make_problem(in, opts, cfg);
+    X.ensure(in.n, 64, max_models(in.variant == kScaleOnly ? kCal : in.variant));
+    PairData D;
+    upload_pair(X, P, &D);
+    std::vector<ScoreRec> recs(nm);
+    for (int m = 0; m < nm; ++m) {
+        prepare_score_rec(P.C, models[m], recs[m], taus ? taus + 3 * m : nullptr);
+        if (ties) ties[m] = recs[m].tie;
+    }
+    DevArray<ScoreRec> d_recs(nm);
+    DevArray<double> d_err((size_t)nm * 3 * in.n);
+    DevArray<int> d_flags((size_t)nm * in.n);
+    MP_HIP(hipMemcpyAsync(d_recs.p, recs.data(), sizeof(ScoreRec) * nm, hipMemcpyHostToDevice, X.stream));
+    MP_HIP(launch_debug_terms(X.stream, D, P.C, d_recs.p, nm, d_err.p, d_flags.p));
+    MP_HIP(hipMemcpyAsync(errors, d_err.p, sizeof(double) * nm * 3 * in.n, hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipMemcpyAsync(flags, d_flags.p, sizeof(int) * nm * in.n, hipMemcpyDeviceToHost, X.stream));
+    MP_HIP(hipStreamSynchronize(X.stream));
+}
+
 void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
                      int nm, double *scores, double *errors) {
     validate(in, opts);
@@ -1790,11 +1894,11 @@ void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const Estim
 }
 
 // score_batch on explicit per-iteration model lists (mp_debug_score_batch, test hook):
-// the estimator's launch with the pre-batch best `best`, its tie margin, and the exact
-// early exit / record skip as flags allow; results and record models back
+// the estimator's launch with the pre-batch best `best`, and the exact early exit /
+// record skip as flags allow; results, bounds, margins and record models back
 void debug_score_batch(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nb,
                        const int *counts, const Model *models, double best, int flags, double *res_best,
-                       int *res_slot, Model *rec_models, double *tie_out, int device) {
+                       int *res_slot, Model *rec_models, double *res_hi_lo, double *model_ties, int device) {
     validate(in, opts);
     const int v = in.variant == kScaleOnly ? kCal : in.variant;
     const int maxm = max_models(v);
@@ -1817,10 +1921,8 @@ void debug_score_batch(const PairInput &in, const RansacOptions &opts, const Est
             ms[(size_t)b * maxm + m] = models[(size_t)b * maxm + m];
             prepare_score_rec(P.C, ms[(size_t)b * maxm + m], recs[(size_t)b * maxm + m]);
         }
-    double M = 0.0;
-    for (int t = 0; t < 3; ++t) M += P.C.thr[t] * std::fabs(P.C.w[t]);
-    const double tie = 4e-12 * std::max<int64_t>(in.n, 64) * M;
-    if (tie_out) *tie_out = tie;
+    if (model_ties)
+        for (size_t k = 0; k < recs.size(); ++k) model_ties[k] = recs[k].tie;
     MP_HIP(hipMemcpyAsync(Q.d_recs, recs.data(), sizeof(ScoreRec) * recs.size(), hipMemcpyHostToDevice, X.stream));
     MP_HIP(hipMemcpyAsync(Q.d_models, ms.data(), sizeof(Model) * ms.size(), hipMemcpyHostToDevice, X.stream));
     MP_HIP(hipMemcpyAsync(Q.d_counts, counts, sizeof(int) * nb, hipMemcpyHostToDevice, X.stream));
@@ -1828,7 +1930,7 @@ void debug_score_batch(const PairInput &in, const RansacOptions &opts, const Est
     const bool exit = (flags & 1) != 0, skip = (flags & 2) != 0;
     const unsigned epoch_hi = ~(++X.epoch);
     MP_HIP(launch_score_batch(X.stream, D, P.C, Q.d_recs, Q.d_counts, nb, maxm, Q.d_scores, Q.d_res,
-                              exit ? best : DBL_MAX, tie, nullptr, skip ? X.d_recword : nullptr, epoch_hi, Q.d_models,
+                              exit ? best : DBL_MAX, nullptr, skip ? X.d_recword : nullptr, epoch_hi, Q.d_models,
                               Q.d_recmodel));
     std::vector<IterResult> res(nb);
     MP_HIP(hipMemcpyAsync(res.data(), Q.d_res, sizeof(IterResult) * nb, hipMemcpyDeviceToHost, X.stream));
@@ -1836,6 +1938,10 @@ void debug_score_batch(const PairInput &in, const RansacOptions &opts, const Est
     for (int b = 0; b < nb; ++b) {
         res_best[b] = res[b].best;
         res_slot[b] = res[b].slot;
+        if (res_hi_lo) {
+            res_hi_lo[2 * b] = res[b].hi;
+            res_hi_lo[2 * b + 1] = res[b].lo;
+        }
     }
     if (rec_models) std::memcpy(rec_models, Q.h_recmodel, sizeof(Model) * nb);
 }

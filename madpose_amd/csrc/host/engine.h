@@ -66,12 +66,19 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
 void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
                      int nm, double *scores, double *errors);
 
+// score_batch's residuals of explicit models: errors nm x 3 x n, flags nm x n, taus nm x
+// 3 (per-term bounds), ties nm (margins) -- mp_debug_score_terms, test hook
+void debug_score_terms(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
+                       int nm, double *errors, int *flags, double *taus, double *ties, int device);
+
 // score_batch over explicit models (mp_debug_score_batch; test hook).  models: nb x
 // max_models(variant) (problem units), counts[b] of them used per iteration.  flags: 1
-// exact early exit against `best`, 2 record skip.  res_slot keeps kSlotAmbiguous.
+// exact early exit against `best`, 2 record skip.  res_slot keeps kSlotAmbiguous /
+// kSlotUncertain; res_hi_lo (nullable): hi, lo per iteration; model_ties (nullable, nb x
+// max_models): the margins.
 void debug_score_batch(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, int nb,
                        const int *counts, const Model *models, double best, int flags, double *res_best,
-                       int *res_slot, Model *rec_models, double *tie_out, int device);
+                       int *res_slot, Model *rec_models, double *res_hi_lo, double *model_ties, int device);
 
 // Batched device LM (mp_lm_refine_batch): problem j refines models[j] (problem units)
 // over the residual blocks idx[offsets[3j] .. offsets[3j+1]) (reproj 0->1),

@@ -15,8 +15,130 @@
 
 namespace mp {
 
-// Prepare the sweep constants of a model (host or device).
-MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r) {
+// ---------------------------------------------------------------------------
+// Screening margins.  score_batch's sums decide nothing by themselves:
+// the host decides every new best on reference-order sums (host/lo_sweep.h).  The
+// device sums screen, and the screen must never hide a model the reference would take.
+// For that the device needs, per model, a bound T on |S_dev - S_ref|, where S_ref is
+// the reference's ScoreModel sum (src/hybrid_ransac.h:274-281: one running sum, type
+// outer, index inner, of min(e, thr_t) w_t with e from EvaluateModelOnPoint) and S_dev
+// this kernel's sum of its own residuals (other operations, FMA, another order).
+//
+// Two sources of difference, bounded separately:
+// * summation order: both sums add the same kind of 3n terms, each in [0, thr_t |w_t|]
+//   (a gated term is thr_t w_t), so each is within gamma_k * M of the exact sum of its
+//   terms (k = 3n for the reference's sequential sum, 3 * trips + 16 for the device's
+//   per-lane sums and fixed trees; gamma_k = k u / (1 - k u), u = 2^-53, M = n sum_t
+//   thr_t |w_t|), for every n;
+// * the terms themselves: min(., thr) is 1-Lipschitz and bounded by thr, so a term
+//   differs by at most min(thr, |e_dev - e_ref|), and for a correspondence that is an
+//   inlier on either side (e <= thr) |e_dev - e_ref| <= delta (2 sqrt(thr) + delta)
+//   when the residual vectors differ by at most delta.  delta is a forward-error bound of
+//   both forms against exact arithmetic on the same input doubles, per model from the
+//   pair's magnitudes (score_margins below; the z < 1e-2 gate bounds 1 / z for the
+//   correspondences it lets through).  That leaves the correspondences where no such
+//   bound holds -- a depth within the error window of the z gate, a cheirality quantity
+//   within its window, a Sampson denominator so small against |G| |a| |b| that the
+//   relative error of the distance is unbounded -- and these the kernel flags
+//   (eval_corr*: `flag`); an iteration with a flag is screened out entirely (its
+//   models go to the host's reference-order resolution, its early exit stops).
+// Every constant below is rounded up, and the whole bound is multiplied by kSafe = 4.
+// The bound is exercised against the host's reference-order errors on adversarial
+// samples (tests/test_margins_gpu.py).
+constexpr double kU = 0x1p-53;
+constexpr double kSafe = 4.0;
+constexpr double kSampsonKappa = 0x1p-26; // den < kappa g^2 (alpha beta)^2: flagged
+MP_HD double gam(double k) { return k * kU / (1.0 - k * kU); }
+
+// |e_dev - e_ref| bound for a term e = |r|^2 clipped at thr, residual vectors within delta
+MP_HD double clip_term_bound(double thr, double delta) {
+    const double b = delta * (2.0 * sqrt(thr) + delta) + 8.0 * kU * thr;
+    return b < thr ? b : thr;
+}
+
+// reprojection t (0: x0 -> image 1 through K1; 1: x1 -> image 0 through K0): the
+// forward-error bound delta of the residual vector (pixels) of both forms, for the
+// correspondences the z gate lets through (z >= 1e-2 - wz) that are inliers on either
+// side.  Ks: max row |.|_1 of the target K's first two rows; Kis: |K^-1|_inf of the target;
+// X: max |coordinate| in the target image; Eq: bound on |q_dev - q| of the point q.
+MP_HD double reproj_delta(double thr, double Ks, double Kis, double X, double Bp, double Eq) {
+    const double zinv = 1.0 / (1e-2 - 2.0 * Eq);      // (Eq <= 1e-3 checked by the caller)
+    const double U = X + sqrt(thr) + 1.0;              // |projection| of an inlier
+    const double Qn = Kis * (U + 1.0);                 // |q_xy / q_z| of an inlier
+    return kSafe * (2.0 * zinv * Eq * (Ks + U + Ks * Qn) + gam(8) * (Ks * (Qn + Bp) + U) +
+                    8.0 * kU * Ks * Kis * (X + 1.0));
+}
+
+MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0)[9], const double (&K1)[9],
+                         const double (&K0i)[9], const double (&K1i)[9], ScoreRec &r, double *taus = nullptr) {
+    const double inf = __builtin_inf();
+    const bool cal = C.variant == kCal;
+    const double *t = m.t;
+    const double tinf = fmax(fabs(t[0]), fmax(fabs(t[1]), fabs(t[2])));
+    const double t1 = fabs(t[0]) + fabs(t[1]) + fabs(t[2]);
+    // |a|_1 and the per-point absolute sums of K^-1 x, in this model's K (uncal: 1/f)
+    const double f0 = cal ? 1.0 : K0[0], f1 = cal ? 1.0 : K1[0];
+    const double A = cal ? C.ea : C.ea / f0 + 1.0, Ap = cal ? C.eap : A;
+    const double B = cal ? C.eb : C.eb / f1 + 1.0, Bp = cal ? C.ebp : B;
+    auto rows_abs = [](const double (&K)[9]) {
+        const double a = fabs(K[0]) + fabs(K[1]) + fabs(K[2]), b = fabs(K[3]) + fabs(K[4]) + fabs(K[5]);
+        return a > b ? a : b;
+    };
+    auto inf_norm = [](const double (&K)[9]) {
+        double v = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            const double rsum = fabs(K[3 * i]) + fabs(K[3 * i + 1]) + fabs(K[3 * i + 2]);
+            v = v > rsum ? v : rsum;
+        }
+        return v;
+    };
+    const double Ks1 = rows_abs(K1), Ks0 = rows_abs(K0), Ki1 = inf_norm(K1i), Ki0 = inf_norm(K0i);
+    // the point q before projection, each form within Eq of exact arithmetic
+    const double Eq0 = gam(12) * ((A + Ap) * (C.ed0 + fabs(m.offset0)) + tinf);
+    const double Eq1 = gam(14) * ((B + Bp) * (C.ed1 + fabs(m.offset1)) * fabs(m.scale) + t1);
+    r.wz0 = kSafe * 2.0 * Eq0;
+    r.wz1 = kSafe * 2.0 * Eq1;
+    double tau0 = inf, tau1 = inf, tau2 = inf;
+    if (Eq0 <= 1e-3) tau0 = clip_term_bound(C.thr[0], reproj_delta(C.thr[0], Ks1, Ki1, C.ex1, Bp, Eq0));
+    if (Eq1 <= 1e-3) tau1 = clip_term_bound(C.thr[1], reproj_delta(C.thr[1], Ks0, Ki0, C.ex0, Ap, Eq1));
+    // Sampson: g = max |G_ij|; for an unflagged correspondence (den >= kappa g^2 (alpha
+    // beta)^2, alpha = |a_0| + |a_1| + 1, beta likewise) |c_dev - c_ref| / sqrt(den) <= rho
+    // and den is known to a relative rel_den, so the distances sqrt(S) differ by at most
+    // rho + sqrt(S) (rel_den / 2 + 4u).  Cc: the coefficient of u g alpha beta in |dc|
+    // (the products of the rays' own errors, exi / exj, and of G's formation included).
+    double g = 0.0;
+    for (int i = 0; i < 9; ++i) g = fmax(g, fabs(r.G[i]));
+    r.kg2 = kSampsonKappa * g * g;
+    {
+        const double Cc = 8.0 * (2.0 + 2.0 * C.exi + 2.0 * C.exj) + 60.0;
+        const double isk = 1.0 / sqrt(kSampsonKappa);
+        const double rho = kSafe * 2.0 * Cc * kU * isk;
+        const double rel_den = kSafe * 16.0 * Cc * kU * isk + gam(8);
+        const double L = cal ? C.loss_scale : 1.0;
+        const double thr = C.thr[2] / L;
+        const double d2 = rho + sqrt(thr) * (rel_den / 2.0 + 4.0 * kU);
+        const double b = L * (d2 * (2.0 * sqrt(thr) + d2)) + 8.0 * kU * C.thr[2];
+        tau2 = b < C.thr[2] ? b : C.thr[2];
+    }
+    if (taus) { // (test hook: the per-term bounds, before the safety factor of the sum)
+        taus[0] = tau0;
+        taus[1] = tau1;
+        taus[2] = tau2;
+    }
+    // cheirality (calibrated): l1, l2 and min_depth (1 - a^2) 1e-2 of both forms
+    r.wl = cal ? kSafe * gam(16) * (8.0 * t1 + 0.1) : 0.0;
+    const double n = C.n;
+    const double Mabs = n * (C.thr[0] * fabs(C.w[0]) + C.thr[1] * fabs(C.w[1]) + C.thr[2] * fabs(C.w[2]));
+    const double trips = (double)((C.n + 255) / 256);
+    const double terms = n * (fabs(C.w[0]) * tau0 + fabs(C.w[1]) * tau1 + fabs(C.w[2]) * tau2);
+    const double order = (gam(3.0 * n + 8.0) + gam(3.0 * trips + 16.0)) * Mabs;
+    const double T = (kSafe * (terms + order) + 16.0 * n * 0x1p-1074) * (C.tie_scale > 1.0 ? C.tie_scale : 1.0);
+    r.tie = (T == T) ? T : inf; // (NaN: no screening)
+}
+
+// Prepare the sweep constants of a model (host or device).  taus (nullable): the
+// per-term bounds of score_margins (a test hook).
+MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r, double *taus = nullptr) {
     double K0[9], K1[9], K0i[9], K1i[9];
     if (C.variant == kCal) {
 #pragma unroll
@@ -78,16 +200,17 @@ MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r) {
     r.o0 = m.offset0;
     r.s = m.scale;
     r.o1s = m.offset1 * m.scale;
-    r.pad = 0.0;
+    score_margins(C, m, K0, K1, K0i, K1i, r, taus);
 }
 
 // One correspondence as the sweeps read it.  For the calibrated estimator the
 // model-independent rays are formed once per correspondence (corr_rays), outside the
 // loops over models: a = K0^-1 x0, b = K1^-1 x1 (xy; the Sampson terms) and the unit
-// bearings n0, n1 (the cheirality test).
+// bearings n0, n1 (the cheirality test).  ab2 = (alpha beta)^2 with alpha = |a_0| + |a_1|
+// + 1 (the Sampson conditioning test of score_margins; a = x0 for the uncalibrated).
 struct Corr {
     double x0u, x0v, x1u, x1v, d0, d1, r0, r1;
-    double a0, a1, b0, b1, n0[3], n1[3];
+    double a0, a1, b0, b1, n0[3], n1[3], ab2;
 };
 
 MP_HD void corr_rays(const PairConst &C, Corr &p) {
@@ -108,6 +231,12 @@ MP_HD void corr_rays(const PairConst &C, Corr &p) {
     p.n1[0] = b0 * p.r1;
     p.n1[1] = b1 * p.r1;
     p.n1[2] = b2 * p.r1;
+}
+MP_HD void corr_cond(Corr &p, bool cal) {
+    const double al = (cal ? fabs(p.a0) + fabs(p.a1) : fabs(p.x0u) + fabs(p.x0v)) + 1.0;
+    const double be = (cal ? fabs(p.b0) + fabs(p.b1) : fabs(p.x1u) + fabs(p.x1v)) + 1.0;
+    const double ab = al * be;
+    p.ab2 = ab * ab;
 }
 
 // Reciprocals of the sweeps.  On the device, the hardware reciprocal refined by two
@@ -134,24 +263,46 @@ MP_HD double div_nonneg(double q, double x) {
     return q / x;
 }
 
-MP_HD double reproj_err(const double *M, const double *k, double u, double v, double a, double tu, double tv) {
+// `flag` (OR-accumulated): the correspondence lies where the margins of score_margins do
+// not hold -- the depth within wz of the z < 1e-2 gate, a cheirality quantity within wl
+// of its threshold, or a Sampson denominator below the conditioning floor.
+MP_HD double reproj_err(const double *M, const double *k, double u, double v, double a, double tu, double tv,
+                        double wz, bool &flag) {
     const double px = (M[0] * u + M[1] * v + M[2]) * a + k[0];
     const double py = (M[3] * u + M[4] * v + M[5]) * a + k[1];
     const double pz = (M[6] * u + M[7] * v + M[8]) * a + k[2];
+    flag = flag || fabs(pz - 1e-2) <= wz;
     if (pz < 1e-2) return DBL_MAX;
     const double iz = rcp_depth(pz);
     const double ex = px * iz - tu, ey = py * iz - tv;
     return ex * ex + ey * ey;
 }
 
-MP_HD double sampson_err(const double *G, double au, double av, double bu, double bv) {
+MP_HD double sampson_err(const ScoreRec &r, double au, double av, double bu, double bv, double ab2, bool &flag) {
+    const double *G = r.G;
     const double e0 = G[0] * au + G[1] * av + G[2];
     const double e1 = G[3] * au + G[4] * av + G[5];
     const double e2 = G[6] * au + G[7] * av + G[8];
     const double f0 = G[0] * bu + G[3] * bv + G[6];
     const double f1 = G[1] * bu + G[4] * bv + G[7];
     const double c = bu * e0 + bv * e1 + e2;
-    return div_nonneg(c * c, e0 * e0 + e1 * e1 + f0 * f0 + f1 * f1);
+    const double den = e0 * e0 + e1 * e1 + f0 * f0 + f1 * f1;
+    flag = flag || !(den >= r.kg2 * ab2);
+    return div_nonneg(c * c, den);
+}
+
+// check_cheirality(R, t, n0, n1, 1e-2) (src/solver.cpp:1188-1206) given R n0: l1 > md
+// and l2 > md decided by the signs of the differences (the same decisions for finite
+// values), each flagged when within wl of zero
+MP_HD bool cheirality_rn(const double *rn, const double *n1, const double *t, double wl, bool &flag) {
+    const double a = -(rn[0] * n1[0] + rn[1] * n1[1] + rn[2] * n1[2]);
+    const double b1 = -(rn[0] * t[0] + rn[1] * t[1] + rn[2] * t[2]);
+    const double b2 = n1[0] * t[0] + n1[1] * t[1] + n1[2] * t[2];
+    const double l1 = b1 - a * b2, l2 = -a * b1 + b2;
+    const double md = 1e-2 * (1 - a * a);
+    const double d1 = l1 - md, d2 = l2 - md;
+    flag = flag || fabs(d1) <= wl || fabs(d2) <= wl;
+    return d1 > 0.0 && d2 > 0.0;
 }
 
 // Calibrated residuals in ray form (C.kstd: K = [k00 k01 k02; 0 k11 k12; 0 0 1] for
@@ -162,14 +313,16 @@ MP_HD double sampson_err(const double *G, double au, double av, double bu, doubl
 // with K1 q / (K1 q)_z rewritten, and R a shared with the cheirality test (R n0 =
 // (R a) r0) -- fewer FP64 instructions per (correspondence, model) than the matrix
 // form M0 = K1 R K0^-1 of reproj_err.
-MP_HD double reproj_ray(const double *q, const double *K, double bu, double bv) {
+MP_HD double reproj_ray(const double *q, const double *K, double bu, double bv, double wz, bool &flag) {
+    flag = flag || fabs(q[2] - 1e-2) <= wz;
     if (q[2] < 1e-2) return DBL_MAX;
     const double iz = rcp_depth(q[2]);
     const double dx = fma(q[0], iz, -bu), dy = fma(q[1], iz, -bv);
     const double ex = fma(K[1], dy, K[0] * dx), ey = K[4] * dy;
     return fma(ex, ex, ey * ey);
 }
-MP_HD void eval_corr_cal_ray(const PairConst &C, const ScoreRec &r, const Corr &p, double &e0, double &e1, double &e2) {
+MP_HD void eval_corr_cal_ray(const PairConst &C, const ScoreRec &r, const Corr &p, double &e0, double &e1, double &e2,
+                             bool &flag) {
     const double *R = r.R, *t = r.t;
     // R a and R^T b (a_2 = b_2 = 1)
     const double ra0 = fma(R[0], p.a0, fma(R[1], p.a1, R[2]));
@@ -181,36 +334,31 @@ MP_HD void eval_corr_cal_ray(const PairConst &C, const ScoreRec &r, const Corr &
     {
         const double s0 = p.d0 + r.o0;
         const double q[3] = {fma(ra0, s0, t[0]), fma(ra1, s0, t[1]), fma(ra2, s0, t[2])};
-        e0 = reproj_ray(q, C.K1, p.b0, p.b1);
+        e0 = reproj_ray(q, C.K1, p.b0, p.b1, r.wz0, flag);
     }
     {
         const double s1 = fma(p.d1, r.s, r.o1s);
         const double q[3] = {fma(rb0, s1, r.nrt[0]), fma(rb1, s1, r.nrt[1]), fma(rb2, s1, r.nrt[2])};
-        e1 = reproj_ray(q, C.K0, p.a0, p.a1);
+        e1 = reproj_ray(q, C.K0, p.a0, p.a1, r.wz1, flag);
     }
     // check_cheirality(R, t, n0, n1, 1e-2) with R n0 = (R a) r0
-    const double rn0 = ra0 * p.r0, rn1 = ra1 * p.r0, rn2 = ra2 * p.r0;
-    const double a = -(rn0 * p.n1[0] + rn1 * p.n1[1] + rn2 * p.n1[2]);
-    const double b1 = -(rn0 * t[0] + rn1 * t[1] + rn2 * t[2]);
-    const double b2 = p.n1[0] * t[0] + p.n1[1] * t[1] + p.n1[2] * t[2];
-    const double l1 = b1 - a * b2, l2 = -a * b1 + b2;
-    const double md = 1e-2 * (1 - a * a);
-    if (!(l1 > md && l2 > md)) {
+    const double rn[3] = {ra0 * p.r0, ra1 * p.r0, ra2 * p.r0};
+    if (!cheirality_rn(rn, p.n1, t, r.wl, flag)) {
         e2 = DBL_MAX;
         return;
     }
-    e2 = sampson_err(r.G, p.a0, p.a1, p.b0, p.b1) * C.loss_scale;
+    e2 = sampson_err(r, p.a0, p.a1, p.b0, p.b1, p.ab2, flag) * C.loss_scale;
 }
 
 // Squared errors of the three data types for one correspondence.
 // gate: apply the score_type gating of EvaluateModelOnPoint (is_for_inlier == false).
 template <int V>
 MP_HD void eval_corr(const PairConst &C, const ScoreRec &r, const Corr &p, bool gate, double &e0, double &e1,
-                     double &e2) {
+                     double &e2, bool &flag) {
     const bool skip_md = gate && C.score_type == 1;  // EPI_ONLY: reprojection gated
     const bool skip_epi = gate && C.score_type == 2; // MD_ONLY: Sampson gated
-    e0 = skip_md ? DBL_MAX : reproj_err(r.M0, r.k0, p.x0u, p.x0v, p.d0 + r.o0, p.x1u, p.x1v);
-    e1 = skip_md ? DBL_MAX : reproj_err(r.M1, r.k1, p.x1u, p.x1v, p.d1 * r.s + r.o1s, p.x0u, p.x0v);
+    e0 = skip_md ? DBL_MAX : reproj_err(r.M0, r.k0, p.x0u, p.x0v, p.d0 + r.o0, p.x1u, p.x1v, r.wz0, flag);
+    e1 = skip_md ? DBL_MAX : reproj_err(r.M1, r.k1, p.x1u, p.x1v, p.d1 * r.s + r.o1s, p.x0u, p.x0v, r.wz1, flag);
     if (C.scale_only) { // HybridPoseEstimatorScaleOnly also rejects small priors (:395, :408)
         if (p.d0 < 1e-2) e0 = DBL_MAX;
         if (p.d1 < 1e-2) e1 = DBL_MAX;
@@ -221,13 +369,15 @@ MP_HD void eval_corr(const PairConst &C, const ScoreRec &r, const Corr &p, bool 
     }
     if (V == kCal) {
         // calibrated rays and unit bearings (corr_rays)
-        if (!check_cheirality(r.R, r.t, p.n0, p.n1, 1e-2)) {
+        double rn[3];
+        matvec3(r.R, p.n0, rn);
+        if (!cheirality_rn(rn, p.n1, r.t, r.wl, flag)) {
             e2 = DBL_MAX;
             return;
         }
-        e2 = sampson_err(r.G, p.a0, p.a1, p.b0, p.b1) * C.loss_scale;
+        e2 = sampson_err(r, p.a0, p.a1, p.b0, p.b1, p.ab2, flag) * C.loss_scale;
     } else {
-        e2 = sampson_err(r.G, p.x0u, p.x0v, p.x1u, p.x1v);
+        e2 = sampson_err(r, p.x0u, p.x0v, p.x1u, p.x1v, p.ab2, flag);
     }
 }
 

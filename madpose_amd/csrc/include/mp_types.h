@@ -43,9 +43,16 @@ struct Model {
 //   t=2:  Sampson with G (E for calibrated rays, F for normalized pixels),
 //         cheirality with R, t on unit bearings (calibrated variant only).
 //   nrt = -R^T t (the ray form of t=1, calibrated intrinsics of the kstd shape)
+//   tie:      the model's screening margin, a bound on |device sum - reference-order
+//             sum| of its MSAC score when no correspondence is flagged (mp_score.h
+//             score_margins)
+//   wz0, wz1: half-widths of the z < 1e-2 gates (t = 0, 1) within which the device's
+//             and the reference's depth may fall on different sides
+//   wl:       the same for the calibrated cheirality test (l1, l2 against min_depth)
+//   kg2:      Sampson conditioning floor: den < kg2 (alpha beta)^2 flags the correspondence
 struct ScoreRec {
     double M0[9], k0[3], M1[9], k1[3], G[9], R[9], t[3], nrt[3];
-    double o0, s, o1s, pad;
+    double o0, s, o1s, tie, wz0, wz1, wl, kg2;
 };
 
 // Per-pair constants (uniform over a launch).
@@ -62,6 +69,13 @@ struct PairConst {
     double thr[3], w[3];                 // squared thresholds / weights after the option transform
     double loss_scale;                   // calibrated Sampson scale (src/hybrid_pose_estimator.h:35-36)
     double min_depth[2];
+    // magnitudes of the pair for the screening margins (mp_score.h score_margins):
+    // cal: ea = max_i |a_i|_1 with a = K0^-1 x0, eap = max_i sum_jk |K0^-1_jk x0_k|, exi =
+    // max_i eap_i / (|a_0| + |a_1| + 1); uncal: ea = eap = max_i |u_i| + |v_i| of the
+    // normalized points, exi = 0.  eb, ebp, exj: the same for x1 / K1.  ed0, ed1: max
+    // |depth|; ex0, ex1: max |coordinate| of x0, x1 (pixels, or normalized).
+    double ea, eap, exi, eb, ebp, exj, ed0, ed1, ex0, ex1;
+    double tie_scale; // multiplies every margin (MADPOSE_TIE_SCALE: tests force the host resolution)
 };
 
 // Device-resident correspondence arrays of one pair (structure of arrays, doubles).
@@ -83,11 +97,17 @@ struct BatchGate {
 // Per-iteration outcome of a batch (score_batch): the iteration's best score
 // (GetBestEstimatedModelId), its model slot and the number of models -- one 16-byte
 // record, so a batch's results come back in one copy.
+// hi = best + the best model's margin (its reference-order score is below hi), lo = the
+// smallest score - margin over the iteration's models (no reference-order score of the
+// iteration is below lo).  slot | kSlotAmbiguous: another model's interval reaches the
+// best's; | kSlotUncertain: a correspondence was flagged (a gate or Sampson value the
+// margins do not cover), so only the reference-order sums decide (engine.cpp).
 struct IterResult {
-    double best;
-    int slot, count; // slot | kSlotAmbiguous: another model within the tie margin (score_batch)
+    double best, hi, lo;
+    int slot, count;
 };
 constexpr int kSlotAmbiguous = 1 << 16;
+constexpr int kSlotUncertain = 1 << 17;
 constexpr int kSlotMask = kSlotAmbiguous - 1;
 
 // One least-squares problem of the batched device LM (kernels/lm_device.h): residual

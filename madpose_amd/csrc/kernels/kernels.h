@@ -38,22 +38,26 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
                            const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
                            int maxm);
 // scoring sweep: one workgroup per iteration, every model of the iteration scored
-// over all correspondences; per-iteration argmin (first minimum wins) into res[b].
-// best: the best minimal-model score before the batch (DBL_MAX: none yet), tie: the
-// absolute margin between this kernel's sums and the reference-order sums (engine.cpp
-// tie_margin); a model whose partial MSAC sum exceeds best + tie cannot win and is
-// dropped early (exact early exit, kernels.hip ScoreBound; only with non-negative
-// weights), reporting DBL_MAX.  An iteration whose second-best model is within tie of
-// its best reports slot | kSlotAmbiguous.  work (nullable): per iteration the (model,
-// 256-correspondence trip) pairs evaluated.  rec (nullable): the record word of a
-// batch that is cut at its first new best (kernels.hip ScoreBound), with epoch_hi =
-// ~epoch, a value unique to the batch; published below best - tie.  rec_out (nullable,
-// device-mapped host memory, nb Models): iterations whose best is below best + tie
-// write that model (from models, nb x maxm) to rec_out[b].
+// over all correspondences; per-iteration argmin (first minimum wins) into res[b] with
+// the screening bounds hi / lo and the kSlotAmbiguous / kSlotUncertain flags (each
+// model's margin is ScoreRec::tie, mp_score.h score_margins).  best: the best
+// minimal-model score before the batch (DBL_MAX: none yet); with non-negative weights a
+// model whose partial sum minus its margin reaches best cannot win and is dropped early
+// (exact early exit, kernels.hip ScoreBound), reporting DBL_MAX.  work (nullable): per
+// iteration the (model, 256-correspondence trip) pairs evaluated.  rec (nullable): the
+// record word of a batch that is cut at its first new best (kernels.hip ScoreBound),
+// with epoch_hi = ~epoch, a value unique to the batch; published when hi < best without
+// a flag.  rec_out (nullable, device-mapped host memory, nb Models): iterations whose lo
+// is below best, or that are uncertain, write their best model (from models, nb x maxm)
+// to rec_out[b].
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
-                              double tie, int *work, unsigned long long *rec = nullptr, unsigned epoch_hi = 0,
+                              int *work, unsigned long long *rec = nullptr, unsigned epoch_hi = 0,
                               const Model *models = nullptr, Model *rec_out = nullptr);
+// score_batch's per-correspondence errors (3 x n per model) and flags (n per model) of
+// nm explicit models (test hook)
+hipError_t launch_debug_terms(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
+                              double *err, int *flags);
 // single-model sweep: per-point squared errors (3 x n, no gating) + gated MSAC score
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,
                         double *score);

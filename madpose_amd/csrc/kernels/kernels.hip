@@ -65,6 +65,7 @@ __device__ inline Corr load_corr(const PairConst &C, const PairData &D, int i, b
     p.r0 = cal ? D.r0[i] : 0.0;
     p.r1 = cal ? D.r1[i] : 0.0;
     if (cal) corr_rays(C, p);
+    corr_cond(p, cal);
     return p;
 }
 
@@ -414,51 +415,50 @@ __global__ void __launch_bounds__(64) pt_compact_kernel(PairConst C, const int *
 // FAST: score_type 0 (hybrid, no gating) and not scale-only, and for the calibrated
 // variant intrinsics of the kstd shape (ray form, mp_score.h eval_corr_cal_ray);
 // everything else takes the general path (runtime gating, matrix form).
-// Exact early exit (ScoreBound): `cut` is the best minimal-model score before the
-// batch (best_min_model_score of src/hybrid_ransac.h:74, 123-131), widened by a
-// relative 1e-12.  An iteration's best score is only ever compared with the running
-// best by a strict '<' (:123), the running best only decreases inside a batch, and
-// every MSAC term min(e, thr) * w is >= 0 -- so a model whose partial sum already
-// exceeds `cut` can never win, and the rest of its sweep is skipped.  The margin
-// keeps the decision away from the last-bit differences between this sum and the
-// reference's sequential one.  Checks run at trip boundaries (one trip = 256
-// correspondences): each live model's workgroup partial (wave sums, then the four
-// waves in LDS in a fixed order -- every lane forms the same value, so the live mask
-// stays uniform) is compared with `cut`; the workgroup leaves once no model is live.
-// Killed models report DBL_MAX and never enter the argmin; a model that could win is
-// never killed, so the winner and its score are those of the full sweep.
+//
+// Screening.  The host decides every new best on reference-order sums
+// (host/lo_sweep.h); this kernel's sums only screen.  Each model carries a margin T_m
+// (ScoreRec::tie, mp_score.h score_margins) with |S_dev - S_ref| <= T_m unless a
+// correspondence of the iteration was flagged.  Per iteration the kernel reports the
+// best device score, hi = best + T_best (the best model's reference score is below it),
+// lo = min_m (S_m - T_m) (no reference score of the iteration is below it), the argmin
+// (first minimum wins), kSlotAmbiguous when another model's interval reaches hi, and
+// kSlotUncertain when a correspondence was flagged or a sum is NaN -- then the margins
+// say nothing and the host re-scores every model of the iteration.
+//
+// Exact early exit (`best`: the best minimal-model score before the batch,
+// best_min_model_score of src/hybrid_ransac.h:74, 123-131).  An iteration's best score
+// is only ever compared with the running best by a strict '<' (:123), the running best
+// only decreases inside a batch, and every MSAC term min(e, thr) * w is >= 0 -- so a
+// model whose partial device sum minus T_m already reaches `best` has a reference sum
+// >= best and can never win: the rest of its sweep is skipped.  Checks run at trip
+// boundaries (one trip = 256 correspondences): each live model's workgroup partial
+// (wave sums, then the four waves in LDS in a fixed order -- every lane forms the same
+// value, so the live mask stays uniform) is compared; the workgroup leaves once no model
+// is live.  Once a flag has been seen the exit stops killing (the partial sums are then
+// no bound), and a model killed earlier was killed on correspondences without flags.
+// Killed models report DBL_MAX and never enter the argmin.
 //
 // Record skip (ScoreBound::rec, batches at or past lo_starting_iterations only): there
 // every new best runs LO, which consumes the selection stream, so the host cuts the
-// batch at the first iteration whose best beats the pre-batch best
-// (src/hybrid_ransac.h:123-156) and discards every later one.  A workgroup whose
-// iteration scores below `best` (the same comparison on the same doubles as the
-// host's) publishes its index by an atomic minimum; a workgroup that sees an earlier
-// published record at one of its early-exit checks (the word is read at the start and
-// after each check, the check's barrier shares the verdict) stops there.  Only
-// batches with a finite pre-batch best (the EXIT kernel) skip.  Iterations up to the first record
-// are always scored in full, so the host's walk never reads a skipped one.  The word
-// carries an epoch in its high half (complemented, so a new batch's first record
-// always wins the minimum) and needs no reset between batches.
-//
-// Near ties.  The host decides every new best on reference-order sums
-// (host/lo_sweep.h); this kernel's sums only screen, with a proven margin `tie` (an
-// absolute bound on |device sum - reference-order sum|): a record is published (and
-// the iterations behind it skipped) only when the best is below the pre-batch best by
-// more than the margin (rec_lo), the model is handed to the host whenever it could be a
-// new best (rec_hi), and an iteration whose second-best model is within the margin of
-// its best is flagged (kSlotAmbiguous in its result's slot) for the host to resolve.
+// batch at the first iteration that holds a new best (src/hybrid_ransac.h:123-156) and
+// discards every later one.  A workgroup whose hi is below `best` without a flag -- its
+// iteration holds a new best in the reference order for certain -- publishes its index
+// by an atomic minimum; a workgroup that sees an earlier published record at one of its
+// early-exit checks (the word is read at the start and after each check, the check's
+// barrier shares the verdict) stops there.  Iterations up to the first record are
+// always scored in full, so the host's walk never reads a skipped one.  The word
+// carries an epoch in its high half (complemented, so a new batch's first record always
+// wins the minimum) and needs no reset between batches.
 struct ScoreBound {
-    double cut;          // +inf: no early exit
+    double best;         // +inf: no early exit
     int first, every;    // first check after `first` trips, then every `every` trips
     int *work;           // per iteration: (model, trip) pairs evaluated (profiling)
     unsigned long long *rec; // nullptr: no record skip
     unsigned epoch_hi;       // ~epoch of this batch
-    double rec_lo, rec_hi;   // pre-batch best -/+ tie
-    double tie;              // the margin
-    // record models (nullable): an iteration whose best is below rec_hi writes that model
-    // to rec_out[b] (mapped host memory), so the host reads a new best's model without
-    // a copy round trip (every new best of a batch is below the pre-batch best)
+    // record models (nullable): an iteration whose lo is below best (it could hold a new
+    // best) writes its best model to rec_out[b] (mapped host memory), so the host reads
+    // a new best's model without a copy round trip
     const Model *models;
     Model *rec_out;
 };
@@ -475,7 +475,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     const int nm = counts[b];
     if (nm == 0) {
         if (threadIdx.x == 0) {
-            res[b] = IterResult{DBL_MAX, 0, 0};
+            res[b] = IterResult{DBL_MAX, DBL_MAX, DBL_MAX, 0, 0};
             if (sb.work) sb.work[b] = 0;
         }
         return;
@@ -486,7 +486,10 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     unsigned long long recw = ~0ull;
     if (EXIT && sb.rec && threadIdx.x == 0) recw = __hip_atomic_load(sb.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ int s_skip[2];
+    __shared__ int s_flag[2][kBlock / 64];
     bool skipped = false;
+    bool flag = false;       // this lane met a flagged correspondence
+    bool uncertain = false;  // (uniform) the workgroup did, as of the last check
     const ScoreRec *R = recs + (size_t)b * MAXM;
     double acc[MAXM];
 #pragma unroll
@@ -501,15 +504,15 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     const int ntrip = (C.n + kBlock - 1) / kBlock;
     if (!EXIT) {
         for (int i = threadIdx.x; i < C.n; i += kBlock) {
-            const Corr p = load_corr(C, D, i, V == kCal);
+            Corr p = load_corr(C, D, i, V == kCal);
 #pragma unroll
             for (int m = 0; m < MAXM; ++m) {
                 if (m < nm) {
                     double e0, e1, e2;
                     if (FAST && V == kCal)
-                        eval_corr_cal_ray(C, R[m], p, e0, e1, e2);
+                        eval_corr_cal_ray(C, R[m], p, e0, e1, e2, flag);
                     else
-                        eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2);
+                        eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2, flag);
                     acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
                 }
             }
@@ -519,15 +522,15 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     for (int trip = 0; EXIT && trip < ntrip; ++trip) {
         const int i = trip * kBlock + threadIdx.x;
         if (i < C.n) {
-            const Corr p = load_corr(C, D, i, V == kCal);
+            Corr p = load_corr(C, D, i, V == kCal);
 #pragma unroll
             for (int m = 0; m < MAXM; ++m) {
                 if ((live >> m) & 1u) {
                     double e0, e1, e2;
                     if (FAST && V == kCal)
-                        eval_corr_cal_ray(C, R[m], p, e0, e1, e2);
+                        eval_corr_cal_ray(C, R[m], p, e0, e1, e2, flag);
                     else
-                        eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2);
+                        eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2, flag);
                     acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
                 }
             }
@@ -547,15 +550,21 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                     if (lane == 0) part[par][wave][m] = v;
                 }
             }
+            const bool wf = __any(flag);
+            if (lane == 0) s_flag[par][wave] = wf;
             __syncthreads();
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) uncertain = uncertain || s_flag[par][w] != 0;
             unsigned keep = live;
+            if (!uncertain) {
 #pragma unroll
-            for (int m = 0; m < MAXM; ++m) {
-                if ((live >> m) & 1u) {
-                    double v = 0.0;
+                for (int m = 0; m < MAXM; ++m) {
+                    if ((live >> m) & 1u) {
+                        double v = 0.0;
 #pragma unroll
-                    for (int w = 0; w < kBlock / 64; ++w) v += part[par][w][m];
-                    if (v > sb.cut) keep &= ~(1u << m);
+                        for (int w = 0; w < kBlock / 64; ++w) v += part[par][w][m];
+                        if (v - R[m].tie >= sb.best) keep &= ~(1u << m);
+                    }
                 }
             }
             live = __builtin_amdgcn_readfirstlane(keep);
@@ -575,38 +584,88 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
             if (lane == 0) part[par][wave][m] = v;
         }
     }
+    {
+        const bool wf = __any(flag);
+        if (lane == 0) s_flag[par][wave] = wf;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double bs = DBL_MAX, s2 = DBL_MAX; // best and second-best score
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) uncertain = uncertain || s_flag[par][w] != 0;
+        double bs = DBL_MAX; // best score
         int bi = 0;
-        for (int m = 0; m < nm; ++m) {
-            double v = DBL_MAX; // killed: cannot win
-            if ((live >> m) & 1u) {
+        double sc[MAXM];
+#pragma unroll
+        for (int m = 0; m < MAXM; ++m) {
+            double v = DBL_MAX; // killed (or absent): cannot win
+            if (m < nm && ((live >> m) & 1u)) {
                 v = 0.0;
 #pragma unroll
                 for (int w = 0; w < kBlock / 64; ++w) v += part[par][w][m];
+                uncertain = uncertain || v != v;
             }
-            scores[(size_t)b * MAXM + m] = v;
-            if (v < bs) { // strict '<': first minimum wins (src/hybrid_ransac.h:258)
-                s2 = bs;
-                bs = v;
-                bi = m;
-            } else if (v < s2) {
-                s2 = v;
+            sc[m] = v;
+            if (m < nm) {
+                scores[(size_t)b * MAXM + m] = v;
+                if (v < bs) { // strict '<': first minimum wins (src/hybrid_ransac.h:258)
+                    bs = v;
+                    bi = m;
+                }
             }
         }
-        const int amb = (bs < DBL_MAX && s2 - bs <= sb.tie) ? kSlotAmbiguous : 0;
-        res[b] = skipped ? IterResult{DBL_MAX, 0, nm} : IterResult{bs, bi | amb, nm};
+        // hi: the best's reference score is below it; lo: no model's is below it; a
+        // model other than the best whose interval reaches hi could be the reference's
+        // first minimum instead
+        double Tb = 0.0;
+#pragma unroll
+        for (int m = 0; m < MAXM; ++m)
+            if (m == bi) Tb = R[m].tie;
+        const double hi = bs < DBL_MAX ? bs + Tb : DBL_MAX;
+        double lo = DBL_MAX;
+        bool amb = false;
+#pragma unroll
+        for (int m = 0; m < MAXM; ++m) {
+            if (m < nm && sc[m] < DBL_MAX) {
+                const double l = sc[m] - R[m].tie;
+                lo = l < lo ? l : lo;
+                amb = amb || (m != bi && l <= hi);
+            }
+        }
+        const int flags = (amb ? kSlotAmbiguous : 0) | (uncertain ? kSlotUncertain : 0);
+        res[b] = skipped ? IterResult{DBL_MAX, DBL_MAX, DBL_MAX, 0, nm} : IterResult{bs, hi, lo, bi | flags, nm};
         // (a record-skipped iteration reports its trips negated: profiling only)
         if (sb.work) sb.work[b] = skipped ? -work : work;
-        if (sb.rec && !skipped && bs < sb.rec_lo)
+        if (sb.rec && !skipped && !uncertain && hi < sb.best)
             atomicMin(sb.rec, ((unsigned long long)sb.epoch_hi << 32) | (unsigned long long)(unsigned)b);
-        if (sb.rec_out && !skipped && bs < sb.rec_hi) {
+        if (sb.rec_out && !skipped && (uncertain || lo < sb.best)) {
             const double *src = (const double *)(sb.models + (size_t)b * MAXM + bi);
             double *dst = (double *)(sb.rec_out + b);
 #pragma unroll
             for (int q = 0; q < (int)(sizeof(Model) / sizeof(double)); ++q) dst[q] = src[q];
         }
+    }
+}
+
+// score_batch's residuals of explicit models, per correspondence, with the flag of
+// each (mp_debug_score_terms; a test hook of the screening margins): one workgroup per
+// model, the same load and evaluation as score_batch (FAST: the ray form)
+template <int V, bool FAST>
+__global__ void __launch_bounds__(kBlock) debug_terms_kernel(PairData D, PairConst C, const ScoreRec *recs,
+                                                             double *err, int *flags) {
+    const ScoreRec &r = recs[blockIdx.x];
+    double *e = err + (size_t)blockIdx.x * 3 * C.n;
+    for (int i = threadIdx.x; i < C.n; i += kBlock) {
+        const Corr p = load_corr(C, D, i, V == kCal);
+        double e0, e1, e2;
+        bool flag = false;
+        if (FAST && V == kCal)
+            eval_corr_cal_ray(C, r, p, e0, e1, e2, flag);
+        else
+            eval_corr<V>(C, r, p, !FAST, e0, e1, e2, flag);
+        e[i] = e0;
+        e[C.n + i] = e1;
+        e[2 * C.n + i] = e2;
+        flags[(size_t)blockIdx.x * C.n + i] = flag ? 1 : 0;
     }
 }
 
@@ -619,7 +678,8 @@ __global__ void __launch_bounds__(1024) sweep_kernel(PairData D, PairConst C, co
     for (int i = threadIdx.x; i < C.n; i += blockDim.x) {
         const Corr p = load_corr(C, D, i, V == kCal);
         double e0, e1, e2;
-        eval_corr<V>(C, r, p, false, e0, e1, e2);
+        bool flag = false; // (unused: an explicit sweep screens nothing)
+        eval_corr<V>(C, r, p, false, e0, e1, e2, flag);
         err[i] = e0;
         err[C.n + i] = e1;
         err[2 * C.n + i] = e2;
@@ -645,7 +705,8 @@ __global__ void __launch_bounds__(kBlock) score_models_kernel(PairData D, PairCo
     for (int i = threadIdx.x; i < C.n; i += kBlock) {
         const Corr p = load_corr(C, D, i, V == kCal);
         double e0, e1, e2;
-        eval_corr<V>(C, r, p, true, e0, e1, e2);
+        bool flag = false;
+        eval_corr<V>(C, r, p, true, e0, e1, e2, flag);
         acc += msac(e0, C.thr[0], C.w[0]) + msac(e1, C.thr[1], C.w[1]) + msac(e2, C.thr[2], C.w[2]);
     }
     __shared__ double part[kBlock / 64];
@@ -961,8 +1022,8 @@ hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C,
 
 // Early-exit schedule (MADPOSE_SCORE_EXIT=0 turns the exit off; MADPOSE_SCORE_CHECK
 // "first,every" in trips of 256 correspondences overrides the schedule).
-static ScoreBound score_bound(const PairConst &C, double best, double tie, int *work, unsigned long long *rec,
-                              unsigned epoch_hi, const Model *models, Model *rec_out) {
+static ScoreBound score_bound(const PairConst &C, double best, int *work, unsigned long long *rec, unsigned epoch_hi,
+                              const Model *models, Model *rec_out, bool *exit) {
     const int n = C.n;
     static const int mode = [] {
         const char *e = std::getenv("MADPOSE_SCORE_EXIT");
@@ -984,7 +1045,8 @@ static ScoreBound score_bound(const PairConst &C, double best, double tie, int *
     // weights, and with a negative one every iteration is scored in full
     const bool nonneg = C.w[0] >= 0.0 && C.w[1] >= 0.0 && C.w[2] >= 0.0;
     const bool on = mode != 0 && best < DBL_MAX && nonneg;
-    sb.cut = on ? best + tie : __builtin_inf();
+    *exit = on;
+    sb.best = best;
     const int ntrip = (n + kBlock - 1) / kBlock;
     // default: a check every quarter of the trips, at most every two trips (512
     // correspondences; each check costs a wave reduction per live model and a barrier).
@@ -1002,9 +1064,6 @@ static ScoreBound score_bound(const PairConst &C, double best, double tie, int *
     }();
     sb.rec = (skip && on) ? rec : nullptr;
     sb.epoch_hi = epoch_hi;
-    sb.rec_lo = best < DBL_MAX ? best - tie : DBL_MAX;
-    sb.rec_hi = best < DBL_MAX ? best + tie : DBL_MAX;
-    sb.tie = tie;
     sb.models = models;
     sb.rec_out = rec_out;
     return sb;
@@ -1012,13 +1071,13 @@ static ScoreBound score_bound(const PairConst &C, double best, double tie, int *
 
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
-                              double tie, int *work, unsigned long long *rec, unsigned epoch_hi, const Model *models,
+                              int *work, unsigned long long *rec, unsigned epoch_hi, const Model *models,
                               Model *rec_out) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
     const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
-    const ScoreBound sb = score_bound(C, best, tie, work, rec, epoch_hi, models, rec_out);
-    const bool exit = sb.cut < __builtin_inf();
+    bool exit = false;
+    const ScoreBound sb = score_bound(C, best, work, rec, epoch_hi, models, rec_out, &exit);
     auto go = [&](auto V, auto M, auto F) {
         constexpr int kV = decltype(V)::value, kM = decltype(M)::value;
         constexpr bool kF = decltype(F)::value;
@@ -1059,6 +1118,20 @@ hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C,
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+hipError_t launch_debug_terms(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
+                              double *err, int *flags) {
+    if (nm <= 0) return hipSuccess;
+    const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
+    return by_variant(C.variant, [&](auto V) {
+        constexpr int v = decltype(V)::value;
+        if (fast)
+            debug_terms_kernel<v, true><<<nm, kBlock, 0, s>>>(D, C, recs, err, flags);
+        else
+            debug_terms_kernel<v, false><<<nm, kBlock, 0, s>>>(D, C, recs, err, flags);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_sweep(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *rec, double *err,

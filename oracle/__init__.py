@@ -226,11 +226,13 @@ def estimate(variant, x0, x1, d0, d1, min_depth, cam0, cam1, opts, cfg):
     model = OrModel()
     stats = OrStats()
     idx = np.zeros(3 * max(n, 1), dtype=np.int32)
-    lib().oracle_estimate(
+    rc = lib().oracle_estimate(
         variant, ctypes.c_int64(n), _dp(_c(x0)), _dp(_c(x1)), _dp(_c(d0)), _dp(_c(d1)), _dp(_c(min_depth)),
         _dp(_c(cam0)), _dp(_c(cam1)), ctypes.byref(opts), ctypes.byref(cfg), ctypes.byref(model), ctypes.byref(stats),
         idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
     )
+    if rc != 0:
+        raise RuntimeError("oracle_estimate failed (model replay out of step?)")
     inl = [idx[t * n: t * n + stats.num_inliers[t]].copy() for t in range(3)]
     return model_to_dict(model), stats, inl
 

@@ -4,6 +4,8 @@
 // are declared here independently so the oracle shares no code with the product.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <stdexcept>
 #include <cstdint>
 #include <cstring>
 #include <random>
@@ -226,8 +228,13 @@ int oracle_estimate(int variant, int64_t n, const double *x0, const double *x1, 
     auto t0 = std::chrono::steady_clock::now();
     oracle::Model best;
     oracle::Stats S;
-    oracle::estimate_pose((oracle::Variant)variant, (int)n, x0, x1, d0, d1, min_depth, cam0, cam1, to_opts(o),
-                          to_cfg(c), &best, &S);
+    try {
+        oracle::estimate_pose((oracle::Variant)variant, (int)n, x0, x1, d0, d1, min_depth, cam0, cam1, to_opts(o),
+                              to_cfg(c), &best, &S);
+    } catch (const std::exception &e) { // (ORACLE_MODEL_REPLAY out of step)
+        std::fprintf(stderr, "[oracle] %s\n", e.what());
+        return -1;
+    }
     put_model(best, out);
     std::memset(st, 0, sizeof(*st));
     st->best_model_score = S.best_model_score;

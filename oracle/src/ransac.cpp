@@ -13,6 +13,7 @@
 // i.e. exactly what the reference consumes.
 #include <cstdlib>
 #include <cstdio>
+#include <stdexcept>
 #include <algorithm>
 #include <cmath>
 #include <limits>
@@ -237,6 +238,13 @@ struct Engine {
                 if (f) std::fclose(f);
             }
         } closer{dump};
+        // ORACLE_MODEL_REPLAY=<file>: the models of every iteration come from the file
+        // (the engine's MADPOSE_MODEL_DUMP: int32 iteration, int32 count, count x 17
+        // doubles) instead of the minimal solvers -- the selection, LO and termination
+        // logic then runs on the engine's own models (tests/test_ties_gpu.py)
+        const char *replay_path = std::getenv("ORACLE_MODEL_REPLAY");
+        FILE *replay = replay_path ? std::fopen(replay_path, "rb") : nullptr;
+        Closer closer2{replay};
 
         for (S->num_iterations_total = 0; S->num_iterations_total < max_total; ++S->num_iterations_total) {
             const uint32_t it = S->num_iterations_total;
@@ -262,7 +270,17 @@ struct Engine {
             if (st < 0) st = prior[1] > 0 ? 1 : 0; // unreachable: u < psum
             S->num_iterations_per_solver[st] += 1;
             for (int t = 0; t < 3; ++t) sampler.draw(ss[st][t], &sample[t]);
-            const int nm = minimal_solver(P, sample, st, &models);
+            int nm = minimal_solver(P, sample, st, &models);
+            if (replay) {
+                int32_t hdr[2] = {-1, 0};
+                if (std::fread(hdr, sizeof(hdr), 1, replay) != 1 || hdr[0] != (int32_t)it || hdr[1] < 0)
+                    throw std::runtime_error("model replay out of step");
+                models.resize(hdr[1]);
+                static_assert(sizeof(Model) == 17 * sizeof(double), "Model layout");
+                if (hdr[1] > 0 && std::fread(models.data(), sizeof(Model), hdr[1], replay) != (size_t)hdr[1])
+                    throw std::runtime_error("model replay truncated");
+                nm = hdr[1];
+            }
             S->num_hypotheses += nm;
             if (dump) {
                 std::fprintf(dump, "%u %d %d", it, st, nm);
