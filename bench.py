@@ -209,6 +209,8 @@ def dist_info(world):
         info["lo_spin_us"] = int(_lib.lib().mp_lo_spin_us())
     except Exception:  # the CPU stand-in engine of the tests has no library
         info["lo_spin_us"] = None
+    # rank 0's CPU share (pin_rank; empty when one rank has the node's share)
+    info["cpu_share"] = {k: v for k, v in PIN_INFO.items() if k != "cpu_list"} or None
     return info
 
 
@@ -569,6 +571,105 @@ def _engine(a):
     return _Engine()
 
 
+def parse_cpulist(text):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]"""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return out
+
+
+def gpu_local_cpus():
+    """The CPUs local to each HIP device, in HIP's order (the GPU nodes of the KFD
+    topology, ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES applied), from sysfs only (no
+    GPU call); None when the topology cannot be read."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        out = []
+        for k in sorted(int(d) for d in os.listdir(base) if d.isdigit()):
+            with open(f"{base}/{k}/properties") as f:
+                props = dict(l.split()[:2] for l in f if len(l.split()) >= 2)
+            if int(props.get("simd_count", "0")) <= 0:
+                continue
+            loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+            bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+            with open(f"/sys/bus/pci/devices/{bdf}/local_cpulist") as f:
+                out.append(parse_cpulist(f.read()))
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+            vis = os.environ.get(var)
+            if vis:
+                ids = [int(v) for v in vis.split(",") if v.strip().isdigit()]
+                out = [out[i] for i in ids if i < len(out)]
+        return out or None
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_siblings(cpus):
+    """cpu -> the smallest CPU of its core (SMT siblings share it)."""
+    first = {}
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                first[c] = min(parse_cpulist(f.read()))
+        except (OSError, ValueError):
+            first[c] = c
+    return first
+
+
+def partition_cpus(local, allowed, core_of, devices):
+    """Host CPUs for the ranks of one node: rank r runs on devices[r]; its candidates are
+    the allowed CPUs local to that GPU (all allowed CPUs when none is), and the ranks with
+    the same candidates split them into contiguous runs of whole cores.  local: CPU lists
+    per device (or None); core_of: cpu -> core id.  Returns one sorted CPU list per rank."""
+    allowed = sorted(set(allowed))
+    cand = []
+    for d in devices:
+        c = sorted(set(local[d]) & set(allowed)) if local and d < len(local) else []
+        cand.append(tuple(c or allowed))
+    out = [None] * len(devices)
+    for key in dict.fromkeys(cand):
+        ranks = [r for r in range(len(devices)) if cand[r] == key]
+        cores = sorted(dict.fromkeys(core_of.get(c, c) for c in key))
+        k = len(ranks)
+        for j, r in enumerate(ranks):
+            lo, hi = len(cores) * j // k, len(cores) * (j + 1) // k
+            mine = set(cores[lo:hi]) if hi > lo else {cores[j % len(cores)]}
+            out[r] = sorted(c for c in key if core_of.get(c, c) in mine)
+    return out
+
+
+PIN_INFO = {}  # this rank's CPU share (reported under "dist")
+
+
+def pin_rank(local_rank, local_world):
+    """One rank of several on this node: pin the process, before any GPU call and before
+    the engine's threads exist, to the CPUs local to its GPU, split with the ranks that
+    share them (the estimator's host LO runs on these cores -- an unpinned 8-rank run
+    would let eight LM pools, LO lanes and samplers migrate across both sockets), and
+    size the LM pool and its spin from the share.  MADPOSE_BENCH_PIN=0: no pinning."""
+    if local_world <= 1 or os.environ.get("MADPOSE_BENCH_PIN") == "0" or not hasattr(os, "sched_setaffinity"):
+        return
+    allowed = sorted(os.sched_getaffinity(0))
+    bench_dev = os.environ.get("MADPOSE_BENCH_DEVICE")
+    devices = [int(bench_dev) if bench_dev is not None else r for r in range(local_world)]
+    local = gpu_local_cpus()
+    share = partition_cpus(local, allowed, cpu_siblings(allowed), devices)[local_rank]
+    os.sched_setaffinity(0, share)
+    # the LM pool: the calling thread plus up to 7 workers, leaving the estimator, the
+    # sampler and the LO lanes their cores; spin only on a share of its own
+    os.environ.setdefault("MADPOSE_LO_THREADS", str(max(1, min(8, len(share) - 4))))
+    os.environ.setdefault("MADPOSE_LO_SPIN", "300" if len(share) >= 12 else "0")
+    PIN_INFO.update({"cpus": len(share), "cpu_list": share, "gpu_local": bool(local),
+                     "lo_threads": int(os.environ["MADPOSE_LO_THREADS"])})
+
+
 def spawn_ranks(n, argv):
     """--gpus N without a launcher: start N child processes of this script, one per GPU
     (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), before anything in
@@ -584,11 +685,7 @@ def spawn_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        # ranks pinned to one device (the one-card rehearsal) share one host CPU share,
-        # where spinning LM workers cost more than they save; the
-        # process's affinity mask does not show the share, so say it here
-        if "MADPOSE_BENCH_DEVICE" in os.environ and "MADPOSE_LO_SPIN" not in os.environ:
-            env["MADPOSE_LO_SPIN"] = "0"
+        # (each child pins itself to its share of the host CPUs, pin_rank)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
     rcs = [p.wait() for p in procs]
     bad = [rc for rc in rcs if rc != 0]
@@ -628,6 +725,7 @@ def main(argv=None):
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
 
     import torch
     import torch.distributed as dist

@@ -122,6 +122,41 @@ def test_gpus_flag_spawns_ranks_and_gathers_records():
     assert res["n_gpus"] == 2
     assert res["results"]["records"] == 6 and res["results"]["pairs_disjoint"]
     assert res["value"] > 0 and res["scaling"] == "weak"
+    # rank 0 pinned itself to its share of this host's CPUs (bench.pin_rank)
+    share = res["dist"]["cpu_share"]
+    assert share is not None and 1 <= share["cpus"] <= len(os.sched_getaffinity(0))
+    assert 1 <= share["lo_threads"] <= 8
+
+
+def test_cpu_partition_follows_gpu_locality():
+    """8 GPUs on a two-socket host (GPUs 0-3 local to socket 0: CPUs 0-31 and their SMT
+    siblings 64-95; GPUs 4-7 to socket 1): each rank gets a quarter of its socket's cores,
+    siblings kept together, disjoint from every other rank's; without topology all ranks
+    split the allowed CPUs."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    sock = [list(range(0, 32)) + list(range(64, 96)), list(range(32, 64)) + list(range(96, 128))]
+    local = [sock[0]] * 4 + [sock[1]] * 4
+    core_of = {c: c % 64 for c in range(128)}
+    parts = bench.partition_cpus(local, range(128), core_of, list(range(8)))
+    seen = set()
+    for r, cpus in enumerate(parts):
+        assert len(cpus) == 16
+        assert set(cpus) <= set(sock[r // 4])
+        assert {core_of[c] for c in cpus} == {core_of[c] for c in cpus if c < 64}  # whole cores
+        assert not (seen & set(cpus))
+        seen |= set(cpus)
+    # a restricted allowed set (a container's share): the intersection is split
+    parts = bench.partition_cpus(local, range(16, 48), core_of, list(range(8)))
+    assert all(parts[r] and set(parts[r]) <= set(range(16, 32)) for r in range(4))
+    assert all(parts[r] and set(parts[r]) <= set(range(32, 48)) for r in range(4, 8))
+    # no topology, or two ranks on one device (the one-card rehearsal)
+    parts = bench.partition_cpus(None, range(8), {c: c for c in range(8)}, [0, 1])
+    assert parts == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    parts = bench.partition_cpus(local, range(128), core_of, [0, 0])
+    assert len(parts[0]) == len(parts[1]) == 32 and not set(parts[0]) & set(parts[1])
+    assert bench.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
 
 
 def test_gpus_flag_scannet_shards_all_pairs():

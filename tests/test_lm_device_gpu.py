@@ -9,7 +9,12 @@ off, and the EPI_ONLY / MD_ONLY LO modes.
 Every drawn problem counts: the oracle alone
 classifies it; the test prints and bounds how many it excludes, requires device and host
 LM to agree with the oracle on every kept problem, and on every problem requires both to
-end at no higher cost than the start."""
+end at no higher cost than the start.  On the excluded problems (the oracle itself has
+no isolated minimum there) device and host LM must still agree with each other -- by the
+strict criterion, or for EPI_ONLY fits by the cost criterion of lm_cases (|t| is a gauge
+there, tests/golden/lm_gauge_cal.json) -- on all but MAX_PAIR_SPLIT of them (VERDICT r04
+weak #4; measured: every one outside EPI_ONLY, 17-18 of 20 in the two-focal EPI_ONLY
+case, whose focals ride a ridge, tests/golden/lm_ridge_tf.json)."""
 import numpy as np
 import pytest
 
@@ -20,6 +25,7 @@ pytestmark = pytest.mark.gpu
 
 N_PROBLEMS = 96
 MAX_EXCLUDED = {0: 14, 1: 32, 2: 26}  # of 96 (measured: 0-11 / 23-28 / 15-21)
+MAX_PAIR_SPLIT = {0: 0, 1: 3, 2: 0}  # per LO_type: excluded problems where device and host part
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -68,11 +74,18 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
             excluded[reason] += 1
             agree["device"] += okd
             agree["host"] += okh
-            agree["each_other"] += LC.close(m, LC.oracle_model(mh, variant), variant, epi_only=lo_type == 1)
+            hm = LC.oracle_model(mh, variant)
+            same = LC.close(m, hm, variant, epi_only=lo_type == 1)
+            if not same and lo_type == 1:
+                cd = LC.lm_cost(variant, args, o, c, m, lists, norm_scale)
+                chh = LC.lm_cost(variant, args, o, c, mh, lists, norm_scale)
+                same = LC.epi_only_equivalent(m, hm, cd, chh)
+            agree["each_other"] += same
     n_ex = sum(excluded.values())
     print(f"variant {variant} nonmono {nonmono} LO {lo_type}: {N_PROBLEMS} problems, excluded {excluded}; "
           f"of those, agreeing with the oracle: {agree}")
     assert n_ex <= MAX_EXCLUDED[variant], excluded
+    assert agree["each_other"] >= n_ex - MAX_PAIR_SPLIT[lo_type], (excluded, agree)
 
 
 def test_device_lm_many_problems_deterministic():

@@ -86,3 +86,36 @@ def test_lm_ridge_fixture():
     assert abs(ch - cr) <= 1e-6 * cr                           # ... to the same cost level
     assert ca < cr * (1 - 1e-3) and rot_angle_deg(again["R"], ref["R"]) > 1.0  # the ridge: no isolated minimum
     assert rot_angle_deg(mh.R(), ref["R"]) < 1e-2              # the stops differ along it
+
+
+def test_lm_gauge_fixture():
+    """Why the EPI_ONLY agreement of tests/lm_cases.py close() is 1e-3 deg / 1e-4 in t
+    direction instead of 1e-6 deg: with Sampson residuals alone |t| is unobserved (the
+    Sampson distance is invariant to the scale of E = [t]x R), so an LM wanders along
+    |t| by rounding and stops, by Ceres' function tolerance, where its own path leaves
+    it.  Pinned (tests/golden/lm_gauge_cal.json, tests/golden/gen_lm_gauge.py): on this
+    calibrated all-inlier fit the host LM and the oracle end at the same cost (8 parts in
+    1e9, the host lower) with |t| 1.729 against 1.753 and the rotations 6e-6 deg apart --
+    beyond the strict 1e-6 deg, well inside the EPI_ONLY bound; and scaling the oracle's
+    t to the host's |t| leaves its cost unchanged to rounding."""
+    with open(os.path.join(GOLDEN, "lm_gauge_cal.json")) as f:
+        g = json.load(f)
+    variant, nonmono, lo_type = g["variant"], g["nonmono"], g["lo_type"]
+    p, o, c, args, norm_scale, est = LC.setup(variant, nonmono, lo_type)
+    lists = [np.asarray(l, dtype=np.int64) for l in g["lists"]]
+    m0 = LC.model_of(g["start"], variant)
+    ref, ran = oracle.least_squares(variant, *args, oracle_opts(o), oracle_cfg(c), g["kind"], lists,
+                                    LC.oracle_model(m0, variant))
+    (mh, st), = madpose.lm_refine_batch(variant, *args, o, c, [(g["kind"], lists, m0)], on_host=True)
+    cr = LC.lm_cost(variant, args, o, c, LC.model_of(ref, variant), lists, norm_scale)
+    ch = LC.lm_cost(variant, args, o, c, mh, lists, norm_scale)
+    assert abs(cr - g["oracle_cost"]) <= 1e-9 * cr and abs(ch - g["host_cost"]) <= 1e-9 * ch
+    assert abs(ch - cr) <= 2e-6 * cr  # the same cost level (epi_only_equivalent)
+    assert not LC.close(mh, ref, variant)  # the strict agreement fails ...
+    assert LC.close(mh, ref, variant, epi_only=True)  # ... the EPI_ONLY one holds
+    tn_h, tn_r = np.linalg.norm(mh.t()), np.linalg.norm(ref["t"])
+    assert abs(tn_h - tn_r) > 1e-3 * tn_r  # the stops differ along |t|
+    scaled = dict(ref)
+    scaled["t"] = np.asarray(ref["t"]) * (tn_h / tn_r)
+    cs = LC.lm_cost(variant, args, o, c, LC.model_of(scaled, variant), lists, norm_scale)
+    assert abs(cs - cr) <= 1e-9 * cr  # |t| is a gauge of the EPI_ONLY cost
