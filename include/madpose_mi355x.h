@@ -171,11 +171,13 @@ int mp_debug_score_terms(int variant, int64_t n, const double *x0, const double 
 /* mp_debug_lo_sweep: the same models through the engine's host LO sweep
  * (madpose_amd/csrc/host/lo_sweep.h), the sweep LocalOptimization and
  * UpdateRANSACTerminationCriteria use (src/hybrid_ransac.h:265-349, 383-538): errors
- * and ScoreModel sums in the reference's operation order -- test hook, no device. */
+ * and ScoreModel sums in the reference's operation order -- test hook, no device.
+ * fast_bounds (nullable, 2 per model): the LO's fast sum of the same terms and its
+ * bound on the distance to the reference-order sum (lo_sweep.h lo_sweep_fast). */
 int mp_debug_lo_sweep(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
                       const double *cam0, const double *cam1, const mp_ransac_options *options,
                       const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
-                      double *errors);
+                      double *errors, double *fast_bounds);
 
 /* get_depths (madpose/utils.py:4-22) for many pairs in one launch: pair p's depth map
  * (dims[4p] x dims[4p+1], row-major, float32 for dtype 0 or float64 for dtype 1) is

@@ -164,7 +164,7 @@ EXPORTS = {
     "mp_debug_lo_sweep": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p, c_double_p,
                                          c_double_p, c_double_p, ctypes.POINTER(mp_ransac_options),
                                          ctypes.POINTER(mp_estimator_config), ctypes.POINTER(mp_model), ctypes.c_int32,
-                                         c_double_p, c_double_p]),
+                                         c_double_p, c_double_p, c_double_p]),
     "mp_relpose_5pt": (ctypes.c_int, [c_double_p, c_double_p, ctypes.POINTER(mp_model), ctypes.c_int, ctypes.c_int]),
     "mp_debug_pt5_roots": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, c_double_p, c_double_p, c_double_p,
                                           ctypes.POINTER(ctypes.c_int32), ctypes.c_int]),

@@ -666,9 +666,11 @@ def solve_scale_shift_pose_two_focal_4p4d(x_homo, y_homo, depth_x, depth_y):
 
 
 def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_config, models, with_errors=False,
-                 host_lo=False):
+                 host_lo=False, fast_bounds=None):
     """Device ScoreModel over explicit models given in problem units (tests / diagnostics).
-    host_lo=True: the engine's host LO sweep instead (mp_debug_lo_sweep; no device)."""
+    host_lo=True: the engine's host LO sweep instead (mp_debug_lo_sweep; no device);
+    fast_bounds (host_lo only): an (nm, 2) float64 array filled with the LO's fast sums
+    and their bounds (lo_sweep.h lo_sweep_fast)."""
     x0 = _pts(x0, "x0")
     x1 = _pts(x1, "x1")
     n = x0.shape[0]
@@ -685,7 +687,8 @@ def score_models(variant, x0, x1, depth0, depth1, cam0, cam1, options, est_confi
     if host_lo:
         code = L.lib().mp_debug_lo_sweep(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1),
                                          ctypes.byref(o), ctypes.byref(c), arr, nm, _dp(scores),
-                                         _dp(errors) if with_errors else None)
+                                         _dp(errors) if with_errors else None,
+                                         _dp(fast_bounds) if fast_bounds is not None else None)
     else:
         code = L.lib().mp_score_models(variant, n, _dp(x0), _dp(x1), _dp(d0), _dp(d1), _dp(c0), _dp(c1),
                                        ctypes.byref(o), ctypes.byref(c), arr, nm, _dp(scores),

@@ -352,11 +352,11 @@ int mp_debug_score_terms(int variant, int64_t n, const double *x0, const double 
 int mp_debug_lo_sweep(int variant, int64_t n, const double *x0, const double *x1, const double *d0, const double *d1,
                       const double *cam0, const double *cam1, const mp_ransac_options *options,
                       const mp_estimator_config *config, const mp_model *models, int32_t num_models, double *scores,
-                      double *errors) {
+                      double *errors, double *fast_bounds) {
     return with_models(variant, n, x0, x1, d0, d1, cam0, cam1, options, config, models, num_models, scores,
                        [&](const mp::PairInput &in, const mp::RansacOptions &o, const mp::EstimatorConfig &c,
                            std::vector<mp::Model> &ms) {
-                           mp::lo_sweep_models(in, o, c, ms.data(), num_models, scores, errors);
+                           mp::lo_sweep_models(in, o, c, ms.data(), num_models, scores, errors, fast_bounds);
                        });
 }
 

@@ -815,7 +815,9 @@ class Run {
         Mt19937 *sel = nullptr;
         Model model;
         bool valid = false;
-        double score = 0.0;
+        double fast = 0.0, bound = 0.0; // the fast sum and its distance bound (lo_sweep_fast)
+        bool exact_valid = false;
+        double score = 0.0;              // the reference-order sum, once taken
         const double *err = nullptr; // the buffer holding the last result
         std::vector<double> herr;    // host sweeps' errors (3 x n)
         uint64_t count = 0;
@@ -834,17 +836,16 @@ class Run {
     // residual operations and ScoreModel order, bit-identical to the oracle; a lane
     // keeps its last result (LO asks for the same model's score and inliers in turn)
     LoSweepData hsw_;
-    const double *sweep(Lane &L, const Model &m, double *score) {
-        if (L.valid && std::memcmp(&m, &L.model, sizeof(Model)) == 0) {
-            *score = L.score;
-            return L.err;
-        }
+    // the errors of m (and its fast sum), cached per lane
+    const double *sweep(Lane &L, const Model &m) {
+        if (L.valid && std::memcmp(&m, &L.model, sizeof(Model)) == 0) return L.err;
         auto t_sw = Clock::now();
         if (L.herr.size() < 3 * (size_t)n_) L.herr.resize(3 * (size_t)n_);
-        L.score = lo_sweep(P_.C, hsw_, m, L.herr.data());
+        lo_sweep_fast(P_.C, hsw_, m, L.herr.data(), &L.fast, &L.bound);
         L.err = L.herr.data();
         L.model = m;
         L.valid = true;
+        L.exact_valid = false;
         L.count++;
         const double dt = secs(t_sw);
         L.t[1] += dt;
@@ -853,17 +854,28 @@ class Run {
             g_prof.sweeps += 1;
             g_prof.sweep_wall_ms += 1e3 * dt;
         }
-        *score = L.score;
         return L.err;
     }
+    // ScoreModel's reference-order sum of m
     double score(Lane &L, const Model &m) {
-        double s;
-        sweep(L, m, &s);
-        return s;
+        sweep(L, m);
+        if (!L.exact_valid) {
+            L.score = lo_ordered_score(P_.C, L.err, n_);
+            L.exact_valid = true;
+        }
+        return L.score;
+    }
+    // Whether m's reference-order score could be below b: false when the fast sum
+    // decides it cannot (fast - bound >= b); otherwise the reference-order score in *e
+    // (the caller compares it).  UpdateBestModel needs the exact sum only then.
+    bool score_below(Lane &L, const Model &m, double b, double *e) {
+        sweep(L, m);
+        if (!L.exact_valid && L.fast - L.bound >= b) return false;
+        *e = score(L, m);
+        return true;
     }
     int inliers(Lane &L, const Model &m, const double *thr, std::vector<int> out[3]) {
-        double s;
-        const double *e = sweep(L, m, &s);
+        const double *e = sweep(L, m);
         // Branch-free compaction: whether a correspondence is an inlier is close to a
         // coin flip along the index, so a conditional push_back mispredicts about every
         // other element (measured on the build host, 3 x 2000 errors at ~50 % inliers:
@@ -1082,10 +1094,22 @@ class Run {
     };
     // One LO step (the loop body of src/hybrid_ransac.h:435-470) from m_init on the
     // non-minimal sample `sample_all`, drawing from *L.sel.
+    // The step's update_best calls are applied after all steps, in step order, so a
+    // score can update the best only if it is below b0 (the best when the steps start:
+    // later bests are lower) and below every score this step recorded before it; scores
+    // the fast sum puts at or above that are not recorded (score_below).
     void lo_step(Lane &L, int st, const std::vector<int> &sample_all, const Model &m_init, const double *thr,
-                 const double *upd, StepOut &out) {
+                 const double *upd, double b0, StepOut &out) {
         out.updates.clear();
         if (step_skipped(sample_all)) return;
+        double b = b0;
+        auto record = [&](const Model &mm) {
+            double e;
+            if (score_below(L, mm, b, &e)) {
+                out.updates.emplace_back(e, mm);
+                b = std::min(b, e);
+            }
+        };
         Model m = m_init;
         std::vector<int> smp[3];
         split(sample_all, n_, smp);
@@ -1093,7 +1117,7 @@ class Run {
         least_squares(L, smp, &m, true);
         out.nonmin_s = secs(t_nm);
         auto t_sc = Clock::now();
-        out.updates.emplace_back(score(L, m), m);
+        record(m);
         out.score_s = secs(t_sc);
         auto t_l = Clock::now();
         lsq_fit(L, thr_, st, &m, false);
@@ -1102,7 +1126,7 @@ class Run {
         auto t_it = Clock::now();
         for (int i = 0; i < o_.num_lsq_iterations; ++i) {
             lsq_fit(L, cur, st, &m, false);
-            out.updates.emplace_back(score(L, m), m);
+            record(m);
             for (int t = 0; t < 3; ++t) cur[t] -= upd[t];
         }
         out.iter_s = secs(t_it);
@@ -1129,8 +1153,9 @@ class Run {
         }
         Model m_init = *best_min;
         lsq_fit(L0, thr, st, &m_init, true);
-        double sc = score(L0, m_init);
-        update_best(sc, m_init, st, best_min_score, best_min, best_st);
+        double sc;
+        if (score_below(L0, m_init, *best_min_score, &sc)) update_best(sc, m_init, st, best_min_score, best_min, best_st);
+        const double b0 = *best_min_score; // (the steps' scores are decided against it, lo_step)
         std::vector<int> base[3];
         inliers(L0, m_init, thr_, base);
         std::vector<int> base_all;
@@ -1188,7 +1213,7 @@ class Run {
                     my.discard(start[r] - base_sel.draws());
                     Lane &L = lanes_[lane];
                     L.sel = &my;
-                    lo_step(L, st, r == 0 ? sample0 : sample1, m_init, thr, upd, outs[r]);
+                    lo_step(L, st, r == 0 ? sample0 : sample1, m_init, thr, upd, b0, outs[r]);
                     L.sel = lane == 0 ? &rs_.sel : nullptr;
                     outs[r].sel = my;
                     step_s[r] = secs(ts);
@@ -1223,7 +1248,7 @@ class Run {
             lo_t_[13] += R - first_serial; // steps recomputed in order
             for (int r = first_serial; r < R; ++r) {
                 L0.sel = &sel;
-                lo_step(L0, st, r == 0 ? sample0 : sample1, m_init, thr, upd, outs[r]);
+                lo_step(L0, st, r == 0 ? sample0 : sample1, m_init, thr, upd, b0, outs[r]);
                 L0.sel = &rs_.sel;
             }
             rs_.sel = sel;
@@ -1618,7 +1643,7 @@ void Run::run(Model *best, Stats *S) {
                         double e = kMax;
                         if (certain) {
                             m = fetch_model(Q, (int)j);
-                            e = exact_score(m);
+                            e = exact_score(m);  // (below best_min_score: the bounds say so)
                         } else {
                             resolve_tie(Q, j, &m, &e);
                         }
@@ -1644,17 +1669,27 @@ void Run::run(Model *best, Stats *S) {
                             ++S->number_lo_iterations;
                             double sc = best_min_score;
                             const uint32_t at = iter + 1;
-                            auto predicted = [&](const Mt19937 &sel_end) {
+                            // The hook runs on an LO worker beside the steps: it
+                            // gets copies of the loop state it reads -- the streams as rewound
+                            // (the LO draws only from its own copies of the selection stream
+                            // and writes rs_ after LoWorkers::run has returned), the free
+                            // slot, whether a continuation is pending, the pre-LO best (LO
+                            // leaves best_min_model_score alone, src/hybrid_ransac.h:149-155)
+                            // -- and writes only spec / spec_draws, read after the join.
+                            const IterationStream rs_at_lo = rs_;
+                            const int slot = cur ^ 1;
+                            const bool cont_pending = Bn > 0;
+                            const double bound = best_min_score;
+                            Batch *const gs = &gen[slot];
+                            auto predicted = [this, rs_at_lo, slot, cont_pending, bound, gs, at, max_total, speculate,
+                                              lo_start, &grow, &batch_size, &spec,
+                                              &spec_draws](const Mt19937 &sel_end) {
                                 if (!speculate || at >= max_total) return;
-                                if (Bn > 0) X_.sampler->cancel(); // the no-LO continuation
-                                IterationStream from = rs_;
+                                if (cont_pending) X_.sampler->cancel(); // the no-LO continuation
+                                IterationStream from = rs_at_lo;
                                 from.sel = sel_end;
                                 const uint32_t bc = grow(at);
-                                const int slot = cur ^ 1;
                                 slot_free(slot); // (an early continuation's samples are on the device)
-                                Batch *gs = &gen[slot];
-                                // LO leaves best_min_model_score alone (src/hybrid_ransac.h:149-155)
-                                const double bound = best_min_score;
                                 X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(slot),
                                                   [this, gs, bound, at, lo_start] {
                                                       // the sampler thread is not bound to the
@@ -1730,8 +1765,8 @@ void Run::run(Model *best, Stats *S) {
         auto t0 = Clock::now();
         Model refined = *best;
         least_squares(lanes_[0], S->inlier_indices, &refined, false);
-        const double sc = score(lanes_[0], refined);
-        if (sc < S->best_model_score) {
+        double sc;
+        if (score_below(lanes_[0], refined, S->best_model_score, &sc) && sc < S->best_model_score) {
             S->best_model_score = sc;
             *best = refined;
             termination(*best, max_per);
@@ -1881,7 +1916,7 @@ void debug_score_terms(const PairInput &in, const RansacOptions &opts, const Est
 }
 
 void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
-                     int nm, double *scores, double *errors) {
+                     int nm, double *scores, double *errors, double *fast_bounds) {
     validate(in, opts);
     Problem P = make_problem(in, opts, cfg);
     LoSweepData D;
@@ -1890,6 +1925,7 @@ void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const Estim
     for (int m = 0; m < nm; ++m) {
         scores[m] = lo_sweep(P.C, D, models[m], err.data());
         if (errors) std::memcpy(errors + (size_t)m * 3 * in.n, err.data(), sizeof(double) * 3 * in.n);
+        if (fast_bounds) lo_sweep_fast(P.C, D, models[m], err.data(), fast_bounds + 2 * m, fast_bounds + 2 * m + 1);
     }
 }
 

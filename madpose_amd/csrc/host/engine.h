@@ -64,7 +64,7 @@ void score_models(const PairInput &in, const RansacOptions &opts, const Estimato
 // The engine's host LO sweep (host/lo_sweep.h) over explicit models (problem units):
 // the errors and ScoreModel sums LO uses (mp_debug_lo_sweep, test hook; no device)
 void lo_sweep_models(const PairInput &in, const RansacOptions &opts, const EstimatorConfig &cfg, const Model *models,
-                     int nm, double *scores, double *errors);
+                     int nm, double *scores, double *errors, double *fast_bounds = nullptr);
 
 // score_batch's residuals of explicit models: errors nm x 3 x n, flags nm x n, taus nm x
 // 3 (per-term bounds), ties nm (margins) -- mp_debug_score_terms, test hook

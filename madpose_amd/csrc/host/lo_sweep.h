@@ -45,6 +45,18 @@ void lo_sweep_prepare(const PairConst &C, const double *x0, const double *x1, co
 // of model m (problem units); returns the ScoreModel sum
 double lo_sweep(const PairConst &C, const LoSweepData &D, const Model &m, double *err);
 
+// The same errors with a fast sum instead: ScoreModel's reference-order sum is one
+// chain of 3n dependent additions (about half of a sweep's time), and most of the LO's
+// scores only need to be compared with the best score.  The terms are the reference's
+// to the bit, so the two sums differ by their order alone: |fast - reference sum| <=
+// *bound (both within gamma_3n sum|term| of the exact sum).  A caller takes the
+// reference-order sum (lo_ordered_score, from the same errors) only when the fast sum
+// cannot decide its comparison.
+void lo_sweep_fast(const PairConst &C, const LoSweepData &D, const Model &m, double *err, double *fast, double *bound);
+
+// ScoreModel's sum (src/hybrid_ransac.h:274-281) over errors of lo_sweep / lo_sweep_fast
+double lo_ordered_score(const PairConst &C, const double *err, int n);
+
 // the instruction set lo_sweep dispatched to: 512 (AVX-512F) or 256 (AVX2)
 int lo_sweep_width();
 

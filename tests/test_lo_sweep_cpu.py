@@ -141,3 +141,28 @@ def test_host_lo_sweep_avx2_path_bit_identical():
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert all(a and b for a, b in res), res
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("case", ["example", "tiny", "negative"])
+def test_fast_sum_within_bound(variant, case):
+    """The LO decides most of its UpdateBestModel comparisons on a fast sum of the same
+    terms (lo_sweep.h lo_sweep_fast) and takes the reference-order sum only when the fast
+    one cannot decide: |fast - reference| <= bound for every model, at the example
+    thresholds, at tiny ones (subnormal-range sums) and with a negative weight."""
+    rng = np.random.default_rng(900 + variant)
+    p = synthetic.make_pair(900 + variant, n=1300)
+    kind = ["calibrated", "shared_focal", "two_focal"][variant]
+    o, c = synthetic.example_options(kind)
+    if case == "tiny":
+        o.squared_inlier_thresholds = [1e-300, 1e-300]
+    if case == "negative":
+        o.data_type_weights = [1.0, -0.5]
+    cam0, cam1 = (p["K0"], p["K1"]) if variant == 0 else (p["pp0"], p["pp1"])
+    ms = _models(p, rng, 40, variant)
+    fb = np.zeros((len(ms), 2))
+    ref = madpose.score_models(variant, p["x0"], p["x1"], p["depth0"], p["depth1"], cam0, cam1, o, c, ms,
+                               host_lo=True, fast_bounds=fb)
+    assert np.all(fb[:, 1] >= 0)
+    assert np.all(np.abs(fb[:, 0] - ref) <= fb[:, 1]), np.max(np.abs(fb[:, 0] - ref) / fb[:, 1])
+    assert np.all(fb[:, 1] <= 1e-11 * np.maximum(np.abs(ref), 1e-300) + 1e-300)
