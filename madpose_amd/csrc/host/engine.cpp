@@ -576,7 +576,7 @@ LmJob make_lm_job(const Problem &P, const EstimatorConfig &cfg, const int *sizes
 // score_margins): maxima of the rays' absolute sums, depths and coordinates.
 void pair_magnitudes(PairConst &C, const HostPair &H) {
     const bool cal = C.variant == kCal;
-    double ea = 0, eap = 0, exi = 0, eb = 0, ebp = 0, exj = 0, ed0 = 0, ed1 = 0, ex0 = 0, ex1 = 0;
+    double ea = 0, eap = 0, exi = 0, eb = 0, ebp = 0, exj = 0, ed0 = 0, ed1 = 0, ex0 = 0, ex1 = 0, eab2 = 0;
     for (int i = 0; i < H.n; ++i) {
         const double u0 = H.x0[2 * i], v0 = H.x0[2 * i + 1], u1 = H.x1[2 * i], v1 = H.x1[2 * i + 1];
         ex0 = std::max(ex0, std::max(std::fabs(u0), std::fabs(v0)));
@@ -596,9 +596,15 @@ void pair_magnitudes(PairConst &C, const HostPair &H) {
             };
             ray(C.K0i, u0, v0, &ea, &eap, &exi);
             ray(C.K1i, u1, v1, &eb, &ebp, &exj);
+            const double a0 = C.K0i[0] * u0 + C.K0i[1] * v0 + C.K0i[2], a1 = C.K0i[3] * u0 + C.K0i[4] * v0 + C.K0i[5];
+            const double b0 = C.K1i[0] * u1 + C.K1i[1] * v1 + C.K1i[2], b1 = C.K1i[3] * u1 + C.K1i[4] * v1 + C.K1i[5];
+            const double ab = (std::fabs(a0) + std::fabs(a1) + 1.0) * (std::fabs(b0) + std::fabs(b1) + 1.0);
+            eab2 = std::max(eab2, ab * ab);
         } else {
             ea = std::max(ea, std::fabs(u0) + std::fabs(v0));
             eb = std::max(eb, std::fabs(u1) + std::fabs(v1));
+            const double ab = (std::fabs(u0) + std::fabs(v0) + 1.0) * (std::fabs(u1) + std::fabs(v1) + 1.0);
+            eab2 = std::max(eab2, ab * ab);
         }
     }
     if (!cal) {
@@ -616,6 +622,7 @@ void pair_magnitudes(PairConst &C, const HostPair &H) {
     C.ed1 = ed1;
     C.ex0 = ex0;
     C.ex1 = ex1;
+    C.eab2 = eab2 * (1 + 1e-12);
 }
 
 Problem make_problem(const PairInput &in, const RansacOptions &o, const EstimatorConfig &cfg) {

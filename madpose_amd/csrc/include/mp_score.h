@@ -108,7 +108,9 @@ MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0)[
     // (the products of the rays' own errors, exi / exj, and of G's formation included).
     double g = 0.0;
     for (int i = 0; i < 9; ++i) g = fmax(g, fabs(r.G[i]));
-    r.kg2 = kSampsonKappa * g * g;
+    // (the floor with the pair's largest (alpha beta)^2: one uniform comparison per
+    // correspondence, and for each correspondence at least its own floor)
+    r.kg2 = kSampsonKappa * g * g * C.eab2;
     {
         const double Cc = 8.0 * (2.0 + 2.0 * C.exi + 2.0 * C.exj) + 60.0;
         const double isk = 1.0 / sqrt(kSampsonKappa);
@@ -206,11 +208,10 @@ MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r, do
 // One correspondence as the sweeps read it.  For the calibrated estimator the
 // model-independent rays are formed once per correspondence (corr_rays), outside the
 // loops over models: a = K0^-1 x0, b = K1^-1 x1 (xy; the Sampson terms) and the unit
-// bearings n0, n1 (the cheirality test).  ab2 = (alpha beta)^2 with alpha = |a_0| + |a_1|
-// + 1 (the Sampson conditioning test of score_margins; a = x0 for the uncalibrated).
+// bearings n0, n1 (the cheirality test).
 struct Corr {
     double x0u, x0v, x1u, x1v, d0, d1, r0, r1;
-    double a0, a1, b0, b1, n0[3], n1[3], ab2;
+    double a0, a1, b0, b1, n0[3], n1[3];
 };
 
 MP_HD void corr_rays(const PairConst &C, Corr &p) {
@@ -231,12 +232,6 @@ MP_HD void corr_rays(const PairConst &C, Corr &p) {
     p.n1[0] = b0 * p.r1;
     p.n1[1] = b1 * p.r1;
     p.n1[2] = b2 * p.r1;
-}
-MP_HD void corr_cond(Corr &p, bool cal) {
-    const double al = (cal ? fabs(p.a0) + fabs(p.a1) : fabs(p.x0u) + fabs(p.x0v)) + 1.0;
-    const double be = (cal ? fabs(p.b0) + fabs(p.b1) : fabs(p.x1u) + fabs(p.x1v)) + 1.0;
-    const double ab = al * be;
-    p.ab2 = ab * ab;
 }
 
 // Reciprocals of the sweeps.  On the device, the hardware reciprocal refined by two
@@ -278,7 +273,7 @@ MP_HD double reproj_err(const double *M, const double *k, double u, double v, do
     return ex * ex + ey * ey;
 }
 
-MP_HD double sampson_err(const ScoreRec &r, double au, double av, double bu, double bv, double ab2, bool &flag) {
+MP_HD double sampson_err(const ScoreRec &r, double au, double av, double bu, double bv, bool &flag) {
     const double *G = r.G;
     const double e0 = G[0] * au + G[1] * av + G[2];
     const double e1 = G[3] * au + G[4] * av + G[5];
@@ -287,7 +282,7 @@ MP_HD double sampson_err(const ScoreRec &r, double au, double av, double bu, dou
     const double f1 = G[1] * bu + G[4] * bv + G[7];
     const double c = bu * e0 + bv * e1 + e2;
     const double den = e0 * e0 + e1 * e1 + f0 * f0 + f1 * f1;
-    flag = flag || !(den >= r.kg2 * ab2);
+    flag = flag || !(den >= r.kg2);
     return div_nonneg(c * c, den);
 }
 
@@ -347,7 +342,7 @@ MP_HD void eval_corr_cal_ray(const PairConst &C, const ScoreRec &r, const Corr &
         e2 = DBL_MAX;
         return;
     }
-    e2 = sampson_err(r, p.a0, p.a1, p.b0, p.b1, p.ab2, flag) * C.loss_scale;
+    e2 = sampson_err(r, p.a0, p.a1, p.b0, p.b1, flag) * C.loss_scale;
 }
 
 // Squared errors of the three data types for one correspondence.
@@ -375,9 +370,9 @@ MP_HD void eval_corr(const PairConst &C, const ScoreRec &r, const Corr &p, bool 
             e2 = DBL_MAX;
             return;
         }
-        e2 = sampson_err(r, p.a0, p.a1, p.b0, p.b1, p.ab2, flag) * C.loss_scale;
+        e2 = sampson_err(r, p.a0, p.a1, p.b0, p.b1, flag) * C.loss_scale;
     } else {
-        e2 = sampson_err(r, p.x0u, p.x0v, p.x1u, p.x1v, p.ab2, flag);
+        e2 = sampson_err(r, p.x0u, p.x0v, p.x1u, p.x1v, flag);
     }
 }
 

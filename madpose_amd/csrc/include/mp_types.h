@@ -49,7 +49,7 @@ struct Model {
 //   wz0, wz1: half-widths of the z < 1e-2 gates (t = 0, 1) within which the device's
 //             and the reference's depth may fall on different sides
 //   wl:       the same for the calibrated cheirality test (l1, l2 against min_depth)
-//   kg2:      Sampson conditioning floor: den < kg2 (alpha beta)^2 flags the correspondence
+//   kg2:      Sampson conditioning floor: den < kg2 flags the correspondence
 struct ScoreRec {
     double M0[9], k0[3], M1[9], k1[3], G[9], R[9], t[3], nrt[3];
     double o0, s, o1s, tie, wz0, wz1, wl, kg2;
@@ -74,7 +74,9 @@ struct PairConst {
     // max_i eap_i / (|a_0| + |a_1| + 1); uncal: ea = eap = max_i |u_i| + |v_i| of the
     // normalized points, exi = 0.  eb, ebp, exj: the same for x1 / K1.  ed0, ed1: max
     // |depth|; ex0, ex1: max |coordinate| of x0, x1 (pixels, or normalized).
-    double ea, eap, exi, eb, ebp, exj, ed0, ed1, ex0, ex1;
+    // eab2: max_i (alpha_i beta_i)^2, alpha = |a_0| + |a_1| + 1 (a = K0^-1 x0, or x0),
+    // beta likewise (the Sampson conditioning floor, score_margins).
+    double ea, eap, exi, eb, ebp, exj, ed0, ed1, ex0, ex1, eab2;
     double tie_scale; // multiplies every margin (MADPOSE_TIE_SCALE: tests force the host resolution)
 };
 

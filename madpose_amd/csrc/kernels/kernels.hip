@@ -65,7 +65,6 @@ __device__ inline Corr load_corr(const PairConst &C, const PairData &D, int i, b
     p.r0 = cal ? D.r0[i] : 0.0;
     p.r1 = cal ? D.r1[i] : 0.0;
     if (cal) corr_rays(C, p);
-    corr_cond(p, cal);
     return p;
 }
 
