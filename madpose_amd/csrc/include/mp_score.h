@@ -59,14 +59,21 @@ MP_HD double clip_term_bound(double thr, double delta) {
 // reprojection t (0: x0 -> image 1 through K1; 1: x1 -> image 0 through K0): the
 // forward-error bound delta of the residual vector (pixels) of both forms, for the
 // correspondences the z gate lets through (z >= 1e-2 - wz) that are inliers on either
-// side.  Ks: max row |.|_1 of the target K's first two rows; Kis: |K^-1|_inf of the target;
-// X: max |coordinate| in the target image; Eq: bound on |q_dev - q| of the point q.
-MP_HD double reproj_delta(double thr, double Ks, double Kis, double X, double Bp, double Eq) {
+// side.  Ks: max row |.|_1 of the target K's first two rows; Kx(X): max over those rows
+// of (|Ki_r0| + |Ki_r1|) X + |Ki_r2| of the target's inverse, a bound of |K^-1 x| for
+// |x| <= X; X: max |coordinate| in the target image; Eq: bound on |q_dev - q| of the
+// point q.
+MP_HD double kinv_abs(const double (&Ki)[9], double X) {
+    const double a = (fabs(Ki[0]) + fabs(Ki[1])) * X + fabs(Ki[2]);
+    const double b = (fabs(Ki[3]) + fabs(Ki[4])) * X + fabs(Ki[5]);
+    return a > b ? a : b;
+}
+MP_HD double reproj_delta(double thr, double Ks, const double (&Ki)[9], double X, double Bp, double Eq) {
     const double zinv = 1.0 / (1e-2 - 2.0 * Eq);      // (Eq <= 1e-3 checked by the caller)
     const double U = X + sqrt(thr) + 1.0;              // |projection| of an inlier
-    const double Qn = Kis * (U + 1.0);                 // |q_xy / q_z| of an inlier
+    const double Qn = kinv_abs(Ki, U) + 1.0;           // |q_xy / q_z| of an inlier (and 1)
     return kSafe * (2.0 * zinv * Eq * (Ks + U + Ks * Qn) + gam(8) * (Ks * (Qn + Bp) + U) +
-                    8.0 * kU * Ks * Kis * (X + 1.0));
+                    8.0 * kU * Ks * kinv_abs(Ki, X + 1.0));
 }
 
 MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0)[9], const double (&K1)[9],
@@ -84,23 +91,15 @@ MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0)[
         const double a = fabs(K[0]) + fabs(K[1]) + fabs(K[2]), b = fabs(K[3]) + fabs(K[4]) + fabs(K[5]);
         return a > b ? a : b;
     };
-    auto inf_norm = [](const double (&K)[9]) {
-        double v = 0.0;
-        for (int i = 0; i < 3; ++i) {
-            const double rsum = fabs(K[3 * i]) + fabs(K[3 * i + 1]) + fabs(K[3 * i + 2]);
-            v = v > rsum ? v : rsum;
-        }
-        return v;
-    };
-    const double Ks1 = rows_abs(K1), Ks0 = rows_abs(K0), Ki1 = inf_norm(K1i), Ki0 = inf_norm(K0i);
+    const double Ks1 = rows_abs(K1), Ks0 = rows_abs(K0);
     // the point q before projection, each form within Eq of exact arithmetic
     const double Eq0 = gam(12) * ((A + Ap) * (C.ed0 + fabs(m.offset0)) + tinf);
     const double Eq1 = gam(14) * ((B + Bp) * (C.ed1 + fabs(m.offset1)) * fabs(m.scale) + t1);
     r.wz0 = kSafe * 2.0 * Eq0;
     r.wz1 = kSafe * 2.0 * Eq1;
     double tau0 = inf, tau1 = inf, tau2 = inf;
-    if (Eq0 <= 1e-3) tau0 = clip_term_bound(C.thr[0], reproj_delta(C.thr[0], Ks1, Ki1, C.ex1, Bp, Eq0));
-    if (Eq1 <= 1e-3) tau1 = clip_term_bound(C.thr[1], reproj_delta(C.thr[1], Ks0, Ki0, C.ex0, Ap, Eq1));
+    if (Eq0 <= 1e-3) tau0 = clip_term_bound(C.thr[0], reproj_delta(C.thr[0], Ks1, K1i, C.ex1, Bp, Eq0));
+    if (Eq1 <= 1e-3) tau1 = clip_term_bound(C.thr[1], reproj_delta(C.thr[1], Ks0, K0i, C.ex0, Ap, Eq1));
     // Sampson: g = max |G_ij|; for an unflagged correspondence (den >= kappa g^2 (alpha
     // beta)^2, alpha = |a_0| + |a_1| + 1, beta likewise) |c_dev - c_ref| / sqrt(den) <= rho
     // and den is known to a relative rel_den, so the distances sqrt(S) differ by at most

