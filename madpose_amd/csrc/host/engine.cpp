@@ -331,6 +331,10 @@ struct BatchBufs {
     int *d_counts = nullptr;
     IterResult *d_res = nullptr, *h_res = nullptr;
     int *d_work = nullptr, *h_work = nullptr; // score_batch's evaluated (model, trip) pairs per iteration
+    // device views of h_res / h_work (mapped, coherent): score_batch writes its
+    // per-iteration results straight to the host, no copy launch per batch
+    IterResult *m_res = nullptr;
+    int *m_work = nullptr;
     Model *d_models = nullptr;
     ScoreRec *d_recs = nullptr;
     double *d_scores = nullptr;
@@ -390,8 +394,8 @@ struct DeviceCtx {
                 if (p) hipFree(p);
             for (void *p : {(void *)q.h_res, (void *)q.h_work, (void *)q.h_recmodel})
                 if (p) hipHostFree(p);
-            q.d_counts = q.d_work = q.h_work = nullptr;
-            q.d_res = q.h_res = nullptr;
+            q.d_counts = q.d_work = q.h_work = q.m_work = nullptr;
+            q.d_res = q.h_res = q.m_res = nullptr;
             q.d_models = q.h_recmodel = q.d_recmodel = nullptr;
             q.d_recs = nullptr;
             q.d_scores = nullptr;
@@ -431,8 +435,10 @@ struct DeviceCtx {
             MP_HIP(hipMalloc(&q.d_models, sizeof(Model) * (size_t)bb_ * mm));
             MP_HIP(hipMalloc(&q.d_recs, sizeof(ScoreRec) * (size_t)bb_ * mm));
             MP_HIP(hipMalloc(&q.d_scores, sizeof(double) * (size_t)bb_ * mm));
-            MP_HIP(hipHostMalloc(&q.h_res, sizeof(IterResult) * bb_, hipHostMallocDefault));
-            MP_HIP(hipHostMalloc(&q.h_work, sizeof(int) * bb_, hipHostMallocDefault));
+            MP_HIP(hipHostMalloc(&q.h_res, sizeof(IterResult) * bb_, hipHostMallocMapped | hipHostMallocCoherent));
+            MP_HIP(hipHostMalloc(&q.h_work, sizeof(int) * bb_, hipHostMallocMapped | hipHostMallocCoherent));
+            MP_HIP(hipHostGetDevicePointer((void **)&q.m_res, q.h_res, 0));
+            MP_HIP(hipHostGetDevicePointer((void **)&q.m_work, q.h_work, 0));
             MP_HIP(hipHostMalloc(&q.h_recmodel, sizeof(Model) * (size_t)bb_,
                                  hipHostMallocMapped | hipHostMallocCoherent));
             MP_HIP(hipHostGetDevicePointer((void **)&q.d_recmodel, q.h_recmodel, 0));
@@ -1314,7 +1320,8 @@ class Run {
 
     // Solves and scores batch g on the GPU (asynchronous, X_.stream): sample upload,
     // MD solver on the side stream, the point-solver stages, score_batch, and the
-    // per-iteration best scores / slots / model counts back to pinned host memory.
+    // per-iteration best scores / slots / model counts, written by score_batch into
+    // mapped host memory.
     // best: best_min_model_score when the batch starts (the scoring's early exit).
     bool batch_prof_[2] = {false, false};
     double launch_s_ = 0.0; // main-thread time in launch_batch (MADPOSE_LO_TIMING)
@@ -1331,12 +1338,7 @@ class Run {
     }();
     bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
     int launch_n_ = 0;
-    // MADPOSE_MD_SAME_STREAM=1: the MD solver on the main stream ahead of the point
-    // chain instead of on the side stream (an experiment on the fork / join cost)
-    const bool md_same_stream_ = [] {
-        const char *e = std::getenv("MADPOSE_MD_SAME_STREAM");
-        return e && e[0] == '1';
-    }();
+
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
     // best runs LO and cuts it; score_batch then skips the iterations behind a record.
     // gate_prev: the batch is launched before the previous one's results were read (an
@@ -1361,29 +1363,32 @@ class Run {
         const int *d_md_list = X_.d_samples + 8 * (size_t)B, *d_pt_list = d_md_list + nmd;
         if (prof) MP_HIP(hipEventRecord(Q.ev[0], s));
         // MD iterations on the side stream, point iterations on the main one (they
-        // write disjoint model slots); scoring waits for both
-        if (nmd > 0 && md_same_stream_) {
-            MP_HIP(launch_md_solve(s, D, P_.C, d_md_list, nmd, X_.d_samples, Q.d_models, Q.d_recs, Q.d_counts, maxm_));
-        } else if (nmd > 0) {
-            MP_HIP(hipEventRecord(Q.ev_fork, s));
-            MP_HIP(hipStreamWaitEvent(X_.md_stream, Q.ev_fork, 0));
-            MP_HIP(launch_md_solve(X_.md_stream, D, P_.C, d_md_list, nmd, X_.d_samples, Q.d_models, Q.d_recs,
-                                   Q.d_counts, maxm_));
-            MP_HIP(hipEventRecord(Q.ev_join, X_.md_stream));
-        }
+        // write disjoint model slots); scoring waits for both -- or, calibrated, both in
+        // one launch on the main stream (launch_solve_fused)
         const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen};
-        MP_HIP(launch_pt_solve(s, D, P_.C, d_pt_list, npt, X_.d_samples, W, Q.d_models, Q.d_recs, Q.d_counts,
-                               maxm_));
-        if (nmd > 0 && !md_same_stream_) MP_HIP(hipStreamWaitEvent(s, Q.ev_join, 0));
+        const bool fused = solve_fusable(P_.C);
+        if (fused) {
+            MP_HIP(launch_solve_fused(s, D, P_.C, d_md_list, nmd, d_pt_list, npt, X_.d_samples, W, Q.d_models,
+                                      Q.d_recs, Q.d_counts, maxm_));
+        } else {
+            if (nmd > 0) {
+                MP_HIP(hipEventRecord(Q.ev_fork, s));
+                MP_HIP(hipStreamWaitEvent(X_.md_stream, Q.ev_fork, 0));
+                MP_HIP(launch_md_solve(X_.md_stream, D, P_.C, d_md_list, nmd, X_.d_samples, Q.d_models, Q.d_recs,
+                                       Q.d_counts, maxm_));
+                MP_HIP(hipEventRecord(Q.ev_join, X_.md_stream));
+            }
+            MP_HIP(launch_pt_solve(s, D, P_.C, d_pt_list, npt, X_.d_samples, W, Q.d_models, Q.d_recs, Q.d_counts,
+                                   maxm_));
+            if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, Q.ev_join, 0));
+        }
         if (prof) MP_HIP(hipEventRecord(Q.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
         Q.epoch_hi = epoch_hi;
-        MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.d_res, best,
-                                  prof ? Q.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
+        MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.m_res, best,
+                                  prof ? Q.m_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
                                   Q.d_models, Q.d_recmodel));
         if (prof) MP_HIP(hipEventRecord(Q.ev[2], s));
-        MP_HIP(hipMemcpyAsync(Q.h_res, Q.d_res, sizeof(IterResult) * B, hipMemcpyDeviceToHost, s));
-        if (prof) MP_HIP(hipMemcpyAsync(Q.h_work, Q.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
         MP_HIP(hipEventRecord(Q.ev_done, s));
     }
     // before host sample slot `slot` is redrawn: the last batch launched from it must

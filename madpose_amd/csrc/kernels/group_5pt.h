@@ -155,14 +155,16 @@ struct Group5Shared {
     double N[kS5][4][9];                          // null-space basis
 };
 
-// cand: 9 doubles per root (E, ascending roots), ncand: number of E written
-__global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
-                                                             const int *samples, double *cand, int *ncand,
-                                                             int cand_stride) {
+// cand: 9 doubles per root (E, ascending roots), ncand: number of E written.  The body
+// of workgroup `bid` (pt_roots5_group_kernel, and the fused MD + 5pt launch of
+// kernels.hip, which gives it the workgroups past the MD solver's)
+__device__ __forceinline__ void pt_roots5_group_body(int bid, const PairData &D, const PairConst &C, const int *list,
+                                                     int nlist, const int *samples, double *cand, int *ncand,
+                                                     int cand_stride) {
     if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     __shared__ Group5Shared sh;
     const int g = threadIdx.x / kG5, r = threadIdx.x % kG5;
-    const int idx = blockIdx.x * kS5 + g;
+    const int idx = bid * kS5 + g;
     const bool active = idx < nlist;
     const int *s = samples + (size_t)list[active ? idx : nlist - 1] * kSampleStride;
     G5_START;
@@ -313,6 +315,12 @@ __global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairCon
         }
         if (r == 0) ncand[idx] = nE;
     }
+}
+
+__global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                             const int *samples, double *cand, int *ncand,
+                                                             int cand_stride) {
+    pt_roots5_group_body(blockIdx.x, D, C, list, nlist, samples, cand, ncand, cand_stride);
 }
 
 } // namespace

@@ -33,10 +33,18 @@ struct PtWorkspace {
     int *valid;
     double *pen; // kPtPenStride doubles per point sample (shared focal)
 };
-// point minimal solver over the listed iterations (three launches, see kernels.hip).
+// point minimal solver over the listed iterations (three launches, see kernels.hip;
+// roots_done: the root stage ran in launch_solve_fused).
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
-                           int maxm);
+                           int maxm, bool roots_done = false);
+// Calibrated, default MD solver at 4 lanes per sample (MADPOSE_SOLVE_FUSE=0 turns it
+// off): the MD solver and the 5pt root stage in one launch, then the 5pt tails and
+// compaction -- both solvers on one stream, no fork / join.
+bool solve_fusable(const PairConst &C);
+hipError_t launch_solve_fused(hipStream_t s, const PairData &D, const PairConst &C, const int *md_list, int nmd,
+                              const int *pt_list, int npt, const int *samples, const PtWorkspace &W, Model *models,
+                              ScoreRec *recs, int *counts, int maxm);
 // scoring sweep: one workgroup per iteration, every model of the iteration scored
 // over all correspondences; per-iteration argmin (first minimum wins) into res[b] with
 // the screening bounds hi / lo and the kSlotAmbiguous / kSlotUncertain flags (each

@@ -207,10 +207,11 @@ template <> struct MdxSys<kTF> {
     static constexpr int K = 4;
 };
 
+// the body of workgroup `bid` (md_exact_kernel, and the fused MD + 5pt launch below)
 template <int V, int R>
-__global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, const int *list, int nlist,
-                                                      const int *samples, Model *models, ScoreRec *recs, int *counts,
-                                                      int maxm) {
+__device__ __forceinline__ void md_exact_body(int bid, const PairData &D, const PairConst &C, const int *list,
+                                              int nlist, const int *samples, Model *models, ScoreRec *recs,
+                                              int *counts, int maxm) {
     if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     using Sys = typename MdxSys<V>::S;
     constexpr int K = MdxSys<V>::K, NR = Sys::NR;
@@ -218,7 +219,7 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
     static_assert(NR % R == 0, "a sample's lanes take its roots in equal turns");
     __shared__ double scr[R == 1 ? NR * 64 : 1];
     const int g = threadIdx.x / R, r = threadIdx.x % R;
-    const int idx = blockIdx.x * (64 / R) + g;
+    const int idx = bid * (64 / R) + g;
     const bool active = idx < nlist;
     if (R == 1 && !active) return;
     const int b = list[active ? idx : nlist - 1];
@@ -299,6 +300,28 @@ __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, c
         }
         if (active && r == 0) counts[b] = n < maxm ? n : maxm;
     }
+}
+
+template <int V, int R>
+__global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                      const int *samples, Model *models, ScoreRec *recs, int *counts,
+                                                      int maxm) {
+    md_exact_body<V, R>(blockIdx.x, D, C, list, nlist, samples, models, recs, counts, maxm);
+}
+
+// The calibrated minimal solvers in one launch: workgroups [0, md_blocks) run the
+// exact MD solver (4 lanes per sample), the rest the 5pt root stage.  On two streams
+// the two needed a fork and a join per batch (four API calls and a cross-stream wait);
+// in one grid the MD solver, the longer of the two, still overlaps the root stage, and
+// the 5pt tails and the compaction follow on the same stream.
+__global__ void __launch_bounds__(64) md_pt5_kernel(PairData D, PairConst C, const int *md_list, int nmd,
+                                                    int md_blocks, const int *pt_list, int npt, const int *samples,
+                                                    double *cand, int *ncand, int cand_stride, Model *models,
+                                                    ScoreRec *recs, int *counts, int maxm) {
+    if ((int)blockIdx.x < md_blocks)
+        md_exact_body<kCal, 4>(blockIdx.x, D, C, md_list, nmd, samples, models, recs, counts, maxm);
+    else
+        pt_roots5_group_body(blockIdx.x - md_blocks, D, C, pt_list, npt, samples, cand, ncand, cand_stride);
 }
 
 template <int K>
@@ -917,6 +940,19 @@ hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D
     return hipGetLastError();
 }
 
+// the default MD solvers (shift on, no alternates) run md_exact
+static bool md_plain(const PairConst &C) {
+    return C.md_alt == 0 && (C.variant != kCal || (!C.scale_only && C.use_shift));
+}
+// md_exact's lanes per sample (MADPOSE_MDX_R=1|2|4 overrides the default)
+static int md_lanes(int v) {
+    static const int r_env = [] {
+        const char *e = std::getenv("MADPOSE_MDX_R");
+        return e ? std::atoi(e) : 0;
+    }();
+    return (r_env == 1 || r_env == 2 || r_env == 4) ? r_env : (v == kSF ? 2 : 4);
+}
+
 hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, Model *models, ScoreRec *recs, int *counts, int maxm) {
     if (nlist <= 0) return hipSuccess;
@@ -930,13 +966,8 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
         // 124 us, profiles/r04/mdxr/); tf and cal: one lane per root.
         // MADPOSE_MDX_R=1|2|4 overrides (results are the same: a lane's arithmetic never
         // depends on the others; tests/test_switch_invariance_gpu.py)
-        const bool plain = C.md_alt == 0 && (v != kCal || (!C.scale_only && C.use_shift));
-        if (plain) {
-            static const int r_env = [] {
-                const char *e = std::getenv("MADPOSE_MDX_R");
-                return e ? std::atoi(e) : 0;
-            }();
-            const int r = (r_env == 1 || r_env == 2 || r_env == 4) ? r_env : (v == kSF ? 2 : 4);
+        if (md_plain(C)) {
+            const int r = md_lanes(v);
             if (r == 1)
                 md_exact_kernel<v, 1><<<grid, 64, 0, s>>>(D, C, list, nlist, samples, models, recs, counts, maxm);
             else if (r == 2)
@@ -985,15 +1016,36 @@ static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int
                                                                          gate);
 }
 
+bool solve_fusable(const PairConst &C) {
+    static const bool off = [] {
+        const char *e = std::getenv("MADPOSE_SOLVE_FUSE");
+        return e && e[0] == '0';
+    }();
+    return !off && C.variant == kCal && md_plain(C) && md_lanes(kCal) == 4;
+}
+
+hipError_t launch_solve_fused(hipStream_t s, const PairData &D, const PairConst &C, const int *md_list, int nmd,
+                              const int *pt_list, int npt, const int *samples, const PtWorkspace &W, Model *models,
+                              ScoreRec *recs, int *counts, int maxm) {
+    if (!solve_fusable(C)) return hipErrorInvalidValue;
+    const int md_blocks = (nmd + 15) / 16, pt_blocks = (npt + kS5 - 1) / kS5;
+    if (md_blocks + pt_blocks > 0)
+        md_pt5_kernel<<<md_blocks + pt_blocks, 64, 0, s>>>(D, C, md_list, nmd, md_blocks, pt_list, npt, samples, W.cand,
+                                                          W.ncand, kCandStride, models, recs, counts, maxm);
+    return launch_pt_solve(s, D, C, pt_list, npt, samples, W, models, recs, counts, maxm, true);
+}
+
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
                            const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs, int *counts,
-                           int maxm) {
+                           int maxm, bool roots_done) {
     if (nlist <= 0) return hipSuccess;
     return by_variant(C.variant, [&](auto V) {
         constexpr int v = decltype(V)::value;
         // root stage: calibrated 5pt on 16-lane groups (group_5pt.h), shared-focal 6pt by
         // the deflated eigenproblem, two-focal 7pt one lane per sample
-        if (v == kSF)
+        if (roots_done)
+            ; // (launched by launch_solve_fused)
+        else if (v == kSF)
             launch_sf_eig(s, D, list, nlist, samples, W.cand, W.ncand, W.pen);
         else if (v == kCal)
             pt_roots5_group_kernel<<<(nlist + kS5 - 1) / kS5, 64, 0, s>>>(D, C, list, nlist, samples, W.cand, W.ncand,

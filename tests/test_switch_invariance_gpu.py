@@ -5,8 +5,9 @@ continuation on while alone and always (MADPOSE_EARLY_CONT, §2 step 7 of DESIGN
 exact MD solvers on one or two lanes per sample instead of the defaults (MADPOSE_MDX_R; cal
 and tf 4, sf 2), the scalar
 batch drawing instead of AVX-512 (MADPOSE_SAMPLER_SIMD), the 15x15 QR packed 16
-samples per wave instead of one sample per wave (MADPOSE_EIG_WAVES), and the
-draw-by-draw sampler (MADPOSE_SAMPLER_TWO_PASS)."""
+samples per wave instead of one sample per wave (MADPOSE_EIG_WAVES), the
+draw-by-draw sampler (MADPOSE_SAMPLER_TWO_PASS), and the calibrated MD and 5pt root
+stage on two streams instead of one fused launch (MADPOSE_SOLVE_FUSE)."""
 import json
 import os
 import subprocess
@@ -21,7 +22,8 @@ pytestmark = pytest.mark.gpu
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "switch_worker.py")
 SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOSE_EARLY_CONT": "2"},
             "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "mdx_two_lanes": {"MADPOSE_MDX_R": "2"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
-            "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"}}
+            "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"},
+            "solve_unfused": {"MADPOSE_SOLVE_FUSE": "0"}}
 
 
 def _run(extra):
