@@ -329,12 +329,14 @@ inline int lo_lanes_setting() {
 // slot while the host still reads this one's results (early continuation, Run::run).
 struct BatchBufs {
     int *d_counts = nullptr;
-    IterResult *d_res = nullptr, *h_res = nullptr;
+    IterResult *d_res = nullptr;
     int *d_work = nullptr, *h_work = nullptr; // score_batch's evaluated (model, trip) pairs per iteration
-    // device views of h_res / h_work (mapped, coherent): score_batch writes its
-    // per-iteration results straight to the host, no copy launch per batch
-    IterResult *m_res = nullptr;
-    int *m_work = nullptr;
+    // the walk's inputs (ScoreBound::flags8 / cand_out): one byte per iteration (model
+    // count | 0x80 for a possible new best), copied back; the IterResults of the marked
+    // iterations, written by score_batch into mapped memory
+    uint8_t *d_flags8 = nullptr, *h_flags8 = nullptr;
+    IterResult *h_cand = nullptr, *d_cand = nullptr;
+
     Model *d_models = nullptr;
     ScoreRec *d_recs = nullptr;
     double *d_scores = nullptr;
@@ -390,12 +392,13 @@ struct DeviceCtx {
             if (p) hipHostFree(p);
         for (BatchBufs &q : bb) {
             for (void *p : {(void *)q.d_counts, (void *)q.d_res, (void *)q.d_work, (void *)q.d_models,
-                            (void *)q.d_recs, (void *)q.d_scores})
+                            (void *)q.d_recs, (void *)q.d_scores, (void *)q.d_flags8})
                 if (p) hipFree(p);
-            for (void *p : {(void *)q.h_res, (void *)q.h_work, (void *)q.h_recmodel})
+            for (void *p : {(void *)q.h_flags8, (void *)q.h_cand, (void *)q.h_work, (void *)q.h_recmodel})
                 if (p) hipHostFree(p);
-            q.d_counts = q.d_work = q.h_work = q.m_work = nullptr;
-            q.d_res = q.h_res = q.m_res = nullptr;
+            q.d_counts = q.d_work = q.h_work = nullptr;
+            q.d_res = q.h_cand = q.d_cand = nullptr;
+            q.d_flags8 = q.h_flags8 = nullptr;
             q.d_models = q.h_recmodel = q.d_recmodel = nullptr;
             q.d_recs = nullptr;
             q.d_scores = nullptr;
@@ -435,10 +438,15 @@ struct DeviceCtx {
             MP_HIP(hipMalloc(&q.d_models, sizeof(Model) * (size_t)bb_ * mm));
             MP_HIP(hipMalloc(&q.d_recs, sizeof(ScoreRec) * (size_t)bb_ * mm));
             MP_HIP(hipMalloc(&q.d_scores, sizeof(double) * (size_t)bb_ * mm));
-            MP_HIP(hipHostMalloc(&q.h_res, sizeof(IterResult) * bb_, hipHostMallocMapped | hipHostMallocCoherent));
-            MP_HIP(hipHostMalloc(&q.h_work, sizeof(int) * bb_, hipHostMallocMapped | hipHostMallocCoherent));
-            MP_HIP(hipHostGetDevicePointer((void **)&q.m_res, q.h_res, 0));
-            MP_HIP(hipHostGetDevicePointer((void **)&q.m_work, q.h_work, 0));
+            // (score_batch writes a byte per iteration to device memory and one copy
+            // brings them over; writing every workgroup's result to mapped host memory
+            // made the kernel 51 -> 63 us per cal launch, profiles/r05/r5j -- only the
+            // few marked iterations write theirs there)
+            MP_HIP(hipMalloc(&q.d_flags8, (size_t)bb_));
+            MP_HIP(hipHostMalloc(&q.h_flags8, (size_t)bb_, hipHostMallocDefault));
+            MP_HIP(hipHostMalloc(&q.h_cand, sizeof(IterResult) * bb_, hipHostMallocMapped | hipHostMallocCoherent));
+            MP_HIP(hipHostGetDevicePointer((void **)&q.d_cand, q.h_cand, 0));
+            MP_HIP(hipHostMalloc(&q.h_work, sizeof(int) * bb_, hipHostMallocDefault));
             MP_HIP(hipHostMalloc(&q.h_recmodel, sizeof(Model) * (size_t)bb_,
                                  hipHostMallocMapped | hipHostMallocCoherent));
             MP_HIP(hipHostGetDevicePointer((void **)&q.d_recmodel, q.h_recmodel, 0));
@@ -1320,8 +1328,7 @@ class Run {
 
     // Solves and scores batch g on the GPU (asynchronous, X_.stream): sample upload,
     // MD solver on the side stream, the point-solver stages, score_batch, and the
-    // per-iteration best scores / slots / model counts, written by score_batch into
-    // mapped host memory.
+    // per-iteration best scores / slots / model counts back to pinned host memory.
     // best: best_min_model_score when the batch starts (the scoring's early exit).
     bool batch_prof_[2] = {false, false};
     double launch_s_ = 0.0; // main-thread time in launch_batch (MADPOSE_LO_TIMING)
@@ -1385,10 +1392,12 @@ class Run {
         if (prof) MP_HIP(hipEventRecord(Q.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
         Q.epoch_hi = epoch_hi;
-        MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.m_res, best,
-                                  prof ? Q.m_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
-                                  Q.d_models, Q.d_recmodel));
+        MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.d_res, best,
+                                  prof ? Q.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
+                                  Q.d_models, Q.d_recmodel, Q.d_flags8, Q.d_cand));
         if (prof) MP_HIP(hipEventRecord(Q.ev[2], s));
+        MP_HIP(hipMemcpyAsync(Q.h_flags8, Q.d_flags8, (size_t)B, hipMemcpyDeviceToHost, s));
+        if (prof) MP_HIP(hipMemcpyAsync(Q.h_work, Q.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
         MP_HIP(hipEventRecord(Q.ev_done, s));
     }
     // before host sample slot `slot` is redrawn: the last batch launched from it must
@@ -1414,8 +1423,8 @@ class Run {
     // bound S - T exceeds the smallest upper bound of the iteration cannot be the
     // reference's winner.  Rare (tests/test_ties_gpu.py forces it).
     void resolve_tie(const BatchBufs &Q, uint32_t j, Model *out, double *out_score) {
-        const int nm = Q.h_res[j].count;
-        const bool uncertain = (Q.h_res[j].slot & kSlotUncertain) != 0;
+        const int nm = Q.h_cand[j].count;
+        const bool uncertain = (Q.h_cand[j].slot & kSlotUncertain) != 0;
         std::vector<double> dsc(nm);
         std::vector<Model> ms(nm);
         std::vector<ScoreRec> rc(nm);
@@ -1639,9 +1648,10 @@ void Run::run(Model *best, Stats *S) {
             uint64_t h = 0, trips = 0, scored = 0;
             for (uint32_t q = 0; q < B; ++q) {
                 // (record-skipped iterations report their partial trips negated)
-                h += (uint64_t)Q.h_res[q].count;
+                const int c = Q.h_flags8[q] & 0x7f;
+                h += (uint64_t)c;
                 trips += (uint64_t)std::abs(Q.h_work[q]);
-                if (Q.h_work[q] > 0) scored += (uint64_t)Q.h_res[q].count;
+                if (Q.h_work[q] > 0) scored += (uint64_t)c;
             }
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.model_trips += trips;
@@ -1670,7 +1680,7 @@ void Run::run(Model *best, Stats *S) {
             const uint32_t iter = it + j;
             const int st = g.types[j];
             S->num_iterations_per_solver[st] += 1;
-            const int nm = Q.h_res[j].count;
+            const int nm = Q.h_flags8[j] & 0x7f;
             S->num_hypotheses += (uint64_t)nm;
             if (model_dump_) {
                 const int32_t hdr[2] = {(int32_t)iter, (int32_t)nm};
@@ -1689,15 +1699,19 @@ void Run::run(Model *best, Stats *S) {
                 // (exact_score) -- see resolve_tie.  `maybe`: the iteration could hold a new
                 // best (some model's lower bound is below the running best, or no bound
                 // holds); `certain`: it does, and its best model is the reference's winner.
-                const double bl = Q.h_res[j].best;
-                const int raw = Q.h_res[j].slot;
+                // Unmarked iterations (flag byte without 0x80) cannot: their lo is at or
+                // above the pre-batch best, which bounds the running best from above.
+                const bool marked = (Q.h_flags8[j] & 0x80) != 0;
+                const IterResult &res = Q.h_cand[j]; // (valid when marked)
+                const double bl = marked ? res.best : kMax;
+                const int raw = marked ? res.slot : 0;
                 const bool uncertain = (raw & kSlotUncertain) != 0;
-                const bool maybe = uncertain || (best_min_score == kMax ? bl < kMax : Q.h_res[j].lo < best_min_score);
+                const bool maybe = marked && (uncertain || (best_min_score == kMax ? bl < kMax : res.lo < best_min_score));
                 if (maybe || iter == lo_start) {
                     bool new_best = false;
                     if (maybe) {
                         const bool certain = !uncertain && !(raw & kSlotAmbiguous) &&
-                                             (best_min_score == kMax || Q.h_res[j].hi < best_min_score);
+                                             (best_min_score == kMax || res.hi < best_min_score);
                         Model m;
                         double e = kMax;
                         if (certain) {

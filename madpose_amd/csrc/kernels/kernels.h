@@ -61,7 +61,8 @@ hipError_t launch_solve_fused(hipStream_t s, const PairData &D, const PairConst 
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
                               int *work, unsigned long long *rec = nullptr, unsigned epoch_hi = 0,
-                              const Model *models = nullptr, Model *rec_out = nullptr);
+                              const Model *models = nullptr, Model *rec_out = nullptr, uint8_t *flags8 = nullptr,
+                              IterResult *cand_out = nullptr);
 // score_batch's per-correspondence errors (3 x n per model) and flags (n per model) of
 // nm explicit models (test hook)
 hipError_t launch_debug_terms(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,

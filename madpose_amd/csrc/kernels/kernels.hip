@@ -483,6 +483,12 @@ struct ScoreBound {
     // a new best's model without a copy round trip
     const Model *models;
     Model *rec_out;
+    // the host's walk (nullable): per iteration one byte, the model count | 0x80 when the
+    // iteration could hold a new best (uncertain, or lo below `best`: a superset of the
+    // walk's tests, whose running best only decreases), and for those the IterResult in
+    // cand_out[b] (mapped host memory) -- the walk reads B bytes, not B IterResults
+    uint8_t *flags8;
+    IterResult *cand_out;
 };
 
 // EXIT = false (no finite bound yet, or MADPOSE_SCORE_EXIT=0): the plain sweep,
@@ -499,6 +505,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         if (threadIdx.x == 0) {
             res[b] = IterResult{DBL_MAX, DBL_MAX, DBL_MAX, 0, 0};
             if (sb.work) sb.work[b] = 0;
+            if (sb.flags8) sb.flags8[b] = 0;
         }
         return;
     }
@@ -654,12 +661,16 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
             }
         }
         const int flags = (amb ? kSlotAmbiguous : 0) | (uncertain ? kSlotUncertain : 0);
-        res[b] = skipped ? IterResult{DBL_MAX, DBL_MAX, DBL_MAX, 0, nm} : IterResult{bs, hi, lo, bi | flags, nm};
+        const IterResult out = skipped ? IterResult{DBL_MAX, DBL_MAX, DBL_MAX, 0, nm} : IterResult{bs, hi, lo, bi | flags, nm};
+        res[b] = out;
         // (a record-skipped iteration reports its trips negated: profiling only)
         if (sb.work) sb.work[b] = skipped ? -work : work;
         if (sb.rec && !skipped && !uncertain && hi < sb.best)
             atomicMin(sb.rec, ((unsigned long long)sb.epoch_hi << 32) | (unsigned long long)(unsigned)b);
-        if (sb.rec_out && !skipped && (uncertain || lo < sb.best)) {
+        const bool cand = !skipped && (uncertain || lo < sb.best);
+        if (sb.flags8) sb.flags8[b] = (uint8_t)(nm | (cand ? 0x80 : 0));
+        if (cand && sb.cand_out) sb.cand_out[b] = out;
+        if (sb.rec_out && cand) {
             const double *src = (const double *)(sb.models + (size_t)b * MAXM + bi);
             double *dst = (double *)(sb.rec_out + b);
 #pragma unroll
@@ -1123,12 +1134,14 @@ static ScoreBound score_bound(const PairConst &C, double best, int *work, unsign
 hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs,
                               const int *counts, int nb, int maxm, double *scores, IterResult *res, double best,
                               int *work, unsigned long long *rec, unsigned epoch_hi, const Model *models,
-                              Model *rec_out) {
+                              Model *rec_out, uint8_t *flags8, IterResult *cand_out) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
     const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
     bool exit = false;
-    const ScoreBound sb = score_bound(C, best, work, rec, epoch_hi, models, rec_out, &exit);
+    ScoreBound sb = score_bound(C, best, work, rec, epoch_hi, models, rec_out, &exit);
+    sb.flags8 = flags8;
+    sb.cand_out = cand_out;
     auto go = [&](auto V, auto M, auto F) {
         constexpr int kV = decltype(V)::value, kM = decltype(M)::value;
         constexpr bool kF = decltype(F)::value;
