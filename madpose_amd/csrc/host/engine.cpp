@@ -837,8 +837,11 @@ class Run {
             long a;
         };
         std::vector<Ev> ev;
+        std::mutex mu; // (the sampler thread launches speculative batches)
         void mark(const char *what, long a = 0) {
-            if (on) ev.push_back({1e6 * std::chrono::duration<double>(Clock::now() - t0).count(), what, a});
+            if (!on) return;
+            std::lock_guard<std::mutex> lk(mu);
+            ev.push_back({1e6 * std::chrono::duration<double>(Clock::now() - t0).count(), what, a});
         }
     } tl_;
     PairData D_;
@@ -1365,6 +1368,7 @@ class Run {
         }
         // one upload: samples, then the MD list and the (descending) point list
         MP_HIP(hipMemcpyAsync(X_.d_samples, slot_ptr(g.slot), sizeof(int) * 9 * (size_t)B, hipMemcpyHostToDevice, s));
+        tl_.mark("  h2d");
         MP_HIP(hipEventRecord(Q.ev_h2d, s));
         Q.h2d_pending = true;
         const int *d_md_list = X_.d_samples + 8 * (size_t)B, *d_pt_list = d_md_list + nmd;
@@ -1377,6 +1381,7 @@ class Run {
         if (fused) {
             MP_HIP(launch_solve_fused(s, D, P_.C, d_md_list, nmd, d_pt_list, npt, X_.d_samples, W, Q.d_models,
                                       Q.d_recs, Q.d_counts, maxm_));
+            tl_.mark("  solve_launched");
         } else {
             if (nmd > 0) {
                 MP_HIP(hipEventRecord(Q.ev_fork, s));
@@ -1395,6 +1400,7 @@ class Run {
         MP_HIP(launch_score_batch(s, D, P_.C, Q.d_recs, Q.d_counts, (int)B, maxm_, Q.d_scores, Q.d_res, best,
                                   prof ? Q.d_work : nullptr, cut_on_record ? X_.d_recword : nullptr, epoch_hi,
                                   Q.d_models, Q.d_recmodel, Q.d_flags8, Q.d_cand));
+        tl_.mark("  score_launched");
         if (prof) MP_HIP(hipEventRecord(Q.ev[2], s));
         MP_HIP(hipMemcpyAsync(Q.h_flags8, Q.d_flags8, (size_t)B, hipMemcpyDeviceToHost, s));
         if (prof) MP_HIP(hipMemcpyAsync(Q.h_work, Q.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
@@ -1676,7 +1682,29 @@ void Run::run(Model *best, Stats *S) {
         bool spec = false; // the sampler holds the post-LO speculation, not the Bn batch
         uint64_t spec_draws = 0;
         uint32_t j = 0;
+        const bool dumping = model_dump_ || count_dump_;
         for (; j < B; ++j) {
+            // 64 iterations at a time while nothing happens in them: none marked, not
+            // lo_starting_iterations, no solver type reaching its cap (the counts only
+            // grow, so a cap reached inside the block is reached at its end)
+            while (!dumping && j + 64 <= B && !(lo_start >= it + j && lo_start < it + j + 64)) {
+                const uint8_t *f = Q.h_flags8 + j, *ty = g.types.data() + j;
+                unsigned mk = 0, n1 = 0, hy = 0;
+                for (int k = 0; k < 64; ++k) {
+                    mk |= f[k];
+                    n1 += ty[k];
+                    hy += f[k] & 0x7fu;
+                }
+                const uint32_t n0 = 64 - n1;
+                if ((mk & 0x80u) || S->num_iterations_per_solver[0] + n0 >= max_per[0] ||
+                    S->num_iterations_per_solver[1] + n1 >= max_per[1])
+                    break;
+                S->num_iterations_per_solver[0] += n0;
+                S->num_iterations_per_solver[1] += n1;
+                S->num_hypotheses += hy;
+                j += 64;
+            }
+            if (j >= B) break;
             const uint32_t iter = it + j;
             const int st = g.types[j];
             S->num_iterations_per_solver[st] += 1;
