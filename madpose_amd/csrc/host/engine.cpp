@@ -1579,8 +1579,48 @@ void Run::run(Model *best, Stats *S) {
     while (it < max_total && !done) {
         if (it == lo_start && best_min_score < kMax) {
             ++S->number_lo_iterations;
-            local_opt(S->best_solver_type, best, &S->best_model_score, &S->best_solver_type);
+            // post-LO speculation as after the LOs of the walk below: the batch from
+            // lo_starting_iterations on is drawn from the predicted end of the selection
+            // stream and launched while the LO steps run (no continuation is pending:
+            // batches stop at lo_start)
+            bool spec0 = false;
+            uint64_t spec0_draws = 0;
+            const IterationStream rs_at_lo = rs_;
+            const int slot = cur ^ 1;
+            const double bound = best_min_score;
+            Batch *const gs = &gen[slot];
+            const uint32_t at = it;
+            auto predicted = [this, rs_at_lo, slot, bound, gs, at, max_total, speculate, lo_start, &grow, &batch_size,
+                              &spec0, &spec0_draws](const Mt19937 &sel_end) {
+                if (!speculate || at >= max_total) return;
+                IterationStream from = rs_at_lo;
+                from.sel = sel_end;
+                slot_free(slot);
+                X_.sampler->start(from, gs, batch_size(at, sync_batch(grow(at))), slot, slot_ptr(slot),
+                                  [this, gs, bound, at, lo_start] {
+                                      MP_HIP(hipSetDevice(X_.device));
+                                      launch_batch(*gs, bound, at >= lo_start);
+                                  });
+                spec0 = true;
+                spec0_draws = sel_end.draws();
+            };
+            tl_.mark("lo", (long)it);
+            local_opt(S->best_solver_type, best, &S->best_model_score, &S->best_solver_type, predicted);
+            tl_.mark("lo_end", spec0 ? 1 : 0);
             termination(*best, max_per);
+            if (spec0) {
+                if (rs_.sel.draws() == spec0_draws) {
+                    tl_.mark("join_spec");
+                    have_next = X_.sampler->finish(&rs_);
+                    if (have_next) {
+                        cur ^= 1;
+                        launched = true;
+                    }
+                } else {
+                    X_.sampler->cancel();
+                    MP_HIP(hipStreamSynchronize(X_.stream)); // a launched speculation drains
+                }
+            }
         }
         // (drawn here only at the start and after LO / a cut batch: kept short so the
         // GPU starts early and the worker draws the big ones)
