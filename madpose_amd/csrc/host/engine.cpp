@@ -1344,10 +1344,23 @@ class Run {
     // 5.99 vs 5.80-5.86 ms, profiles/r04/hook2/)
     const int early_mode_ = [] {
         const char *e = std::getenv("MADPOSE_EARLY_CONT");
-        return e ? (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0)) : 0;
+        return e ? (e[0] == '3' ? 3 : (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0))) : 0;
     }();
-    bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
+    // =3: for continuations of at least kEarlyMinBatch iterations while alone on the
+    // device (the growth phase: new bests are rare there, and the continuation saves the
+    // host round trip between throughput-bound batches)
+    static constexpr uint32_t kEarlyMinBatch = 8192;
+    bool early_now(uint32_t Bn) const {
+        return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1) ||
+               (early_mode_ == 3 && Bn >= kEarlyMinBatch && active_runs(X_.device) <= 1);
+    }
     int launch_n_ = 0;
+    // the fused MD + 5pt launch up to this batch size (MADPOSE_SOLVE_FUSE_MAX; larger
+    // batches fill the GPU, where the fused kernel's register count costs occupancy)
+    const int64_t fuse_max_ = [] {
+        const char *e = std::getenv("MADPOSE_SOLVE_FUSE_MAX");
+        return e ? std::atoll(e) : (int64_t)1 << 40;
+    }();
 
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
     // best runs LO and cuts it; score_batch then skips the iterations behind a record.
@@ -1377,7 +1390,7 @@ class Run {
         // write disjoint model slots); scoring waits for both -- or, calibrated, both in
         // one launch on the main stream (launch_solve_fused)
         const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen};
-        const bool fused = solve_fusable(P_.C);
+        const bool fused = solve_fusable(P_.C) && (int64_t)B <= fuse_max_;
         if (fused) {
             MP_HIP(launch_solve_fused(s, D, P_.C, d_md_list, nmd, d_pt_list, npt, X_.d_samples, W, Q.d_models,
                                       Q.d_recs, Q.d_counts, maxm_));
@@ -1662,7 +1675,7 @@ void Run::run(Model *best, Stats *S) {
         const uint32_t Bn = (it_next < max_total && it_next != lo_start)
                                 ? batch_size(it_next, grow(it_next))
                                 : 0;
-        const bool early = Bn > 0 && early_now();
+        const bool early = Bn > 0 && early_now(Bn);
         if (Bn > 0) {
             slot_free(cur ^ 1);
             if (early) {
