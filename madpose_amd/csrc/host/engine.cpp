@@ -1342,24 +1342,21 @@ class Run {
     // continuation waits for the sampler thread to finish launching it (the speculation
     // hook 31-48 us instead of 4 us, the LO steps phase 221-233 vs 180-194 us, cal 5.90-
     // 5.99 vs 5.80-5.86 ms, profiles/r04/hook2/)
+    // (continuations of the big growth-phase batches only, >= 8192 iterations, measured
+    // slower too: cal 5.62 -> 5.86 ms per pair over 3 x 200 pairs, profiles/r05/r5o)
     const int early_mode_ = [] {
         const char *e = std::getenv("MADPOSE_EARLY_CONT");
-        return e ? (e[0] == '3' ? 3 : (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0))) : 0;
+        return e ? (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0)) : 0;
     }();
-    // =3: for continuations of at least kEarlyMinBatch iterations while alone on the
-    // device (the growth phase: new bests are rare there, and the continuation saves the
-    // host round trip between throughput-bound batches)
-    static constexpr uint32_t kEarlyMinBatch = 8192;
-    bool early_now(uint32_t Bn) const {
-        return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1) ||
-               (early_mode_ == 3 && Bn >= kEarlyMinBatch && active_runs(X_.device) <= 1);
-    }
+    bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
     int launch_n_ = 0;
-    // the fused MD + 5pt launch up to this batch size (MADPOSE_SOLVE_FUSE_MAX; larger
-    // batches fill the GPU, where the fused kernel's register count costs occupancy)
+    // the fused MD + 5pt launch up to this batch size (MADPOSE_SOLVE_FUSE_MAX): larger
+    // batches fill the GPU, where the fused kernel's 216 VGPRs (two waves per SIMD) cost
+    // the 5pt root stage its third wave -- cal 5.62 (always fused) -> 5.46 ms per pair
+    // (up to 8192), 3 x 200 pairs on one box, profiles/r05/r5o
     const int64_t fuse_max_ = [] {
         const char *e = std::getenv("MADPOSE_SOLVE_FUSE_MAX");
-        return e ? std::atoll(e) : (int64_t)1 << 40;
+        return e ? std::atoll(e) : (int64_t)8192;
     }();
 
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
@@ -1675,7 +1672,7 @@ void Run::run(Model *best, Stats *S) {
         const uint32_t Bn = (it_next < max_total && it_next != lo_start)
                                 ? batch_size(it_next, grow(it_next))
                                 : 0;
-        const bool early = Bn > 0 && early_now(Bn);
+        const bool early = Bn > 0 && early_now();
         if (Bn > 0) {
             slot_free(cur ^ 1);
             if (early) {
