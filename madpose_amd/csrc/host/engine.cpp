@@ -356,7 +356,7 @@ struct DeviceCtx {
     hipStream_t stream = nullptr;
     int64_t cap_n = 0;
     int cap_b = 0, cap_m = 0;
-    double *d_pair = nullptr; // 8 arrays of cap_n
+    double *d_pair = nullptr; // 12 arrays of cap_n (PairData)
     int *d_samples = nullptr; // a batch's samples + iteration lists (draw_batch layout; stream-ordered)
     // score_batch's record word (kernels.hip ScoreBound::rec) and the batch epoch
     unsigned long long *d_recword = nullptr;
@@ -426,7 +426,7 @@ struct DeviceCtx {
         MP_HIP(hipSetDevice(device));
         MP_HIP(hipDeviceSynchronize()); // (an early continuation may still use the old buffers)
         free_all();
-        MP_HIP(hipMalloc(&d_pair, sizeof(double) * 8 * nn));
+        MP_HIP(hipMalloc(&d_pair, sizeof(double) * 12 * nn));
         MP_HIP(hipMalloc(&d_err, sizeof(double) * 3 * nn));
         MP_HIP(hipMalloc(&d_samples, sizeof(int) * 9 * bb_));
         MP_HIP(hipMalloc(&d_recword, sizeof(unsigned long long)));
@@ -625,7 +625,7 @@ void pair_magnitudes(PairConst &C, const HostPair &H) {
         eap = ea;
         ebp = eb;
     }
-    // (a NaN coordinate makes every margin NaN, i.e. infinite: no screening)
+    // (a non-finite coordinate or depth turns screening off: make_problem)
     C.ea = ea * (1 + 1e-12);
     C.eap = eap * (1 + 1e-12);
     C.exi = exi * (1 + 1e-12);
@@ -710,6 +710,12 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
     {
         const char *ts = std::getenv("MADPOSE_TIE_SCALE");
         C.tie_scale = ts ? std::max(1.0, std::atof(ts)) : 1.0;
+        // a non-finite coordinate or depth: no screening at all (every margin infinite;
+        // the score kernel's residuals could be NaN where no gate flags them)
+        bool finite = true;
+        for (int i = 0; i < 2 * n && finite; ++i) finite = std::isfinite(H.x0[i]) && std::isfinite(H.x1[i]);
+        for (int i = 0; i < n && finite; ++i) finite = std::isfinite(H.d0[i]) && std::isfinite(H.d1[i]);
+        if (!finite) C.tie_scale = std::numeric_limits<double>::infinity();
     }
     std::memcpy(H.K0, C.K0, sizeof(H.K0));
     std::memcpy(H.K1, C.K1, sizeof(H.K1));
@@ -731,17 +737,17 @@ void upload_pair(DeviceCtx &X, const Problem &P, PairData *D) {
     const int64_t n = P.C.n;
     double *base = X.d_pair;
     const int64_t cn = X.cap_n;
-    std::vector<double> soa(6 * (size_t)n);
+    // (one upload: the six arrays at their device stride cap_n)
+    std::vector<double> soa(5 * (size_t)cn + (size_t)n, 0.0);
     for (int64_t i = 0; i < n; ++i) {
         soa[i] = P.H.x0[2 * i];
-        soa[n + i] = P.H.x0[2 * i + 1];
-        soa[2 * n + i] = P.H.x1[2 * i];
-        soa[3 * n + i] = P.H.x1[2 * i + 1];
-        soa[4 * n + i] = P.H.d0[i];
-        soa[5 * n + i] = P.H.d1[i];
+        soa[cn + i] = P.H.x0[2 * i + 1];
+        soa[2 * cn + i] = P.H.x1[2 * i];
+        soa[3 * cn + i] = P.H.x1[2 * i + 1];
+        soa[4 * cn + i] = P.H.d0[i];
+        soa[5 * cn + i] = P.H.d1[i];
     }
-    for (int a = 0; a < 6; ++a)
-        MP_HIP(hipMemcpyAsync(base + a * cn, soa.data() + a * n, sizeof(double) * n, hipMemcpyHostToDevice, X.stream));
+    MP_HIP(hipMemcpyAsync(base, soa.data(), sizeof(double) * soa.size(), hipMemcpyHostToDevice, X.stream));
     D->x0u = base;
     D->x0v = base + cn;
     D->x1u = base + 2 * cn;
@@ -750,7 +756,12 @@ void upload_pair(DeviceCtx &X, const Problem &P, PairData *D) {
     D->d1 = base + 5 * cn;
     D->r0 = base + 6 * cn;
     D->r1 = base + 7 * cn;
-    MP_HIP(launch_prep_pair(X.stream, P.C, *D, base + 6 * cn, base + 7 * cn));
+    D->a0 = base + 8 * cn;
+    D->a1 = base + 9 * cn;
+    D->b0 = base + 10 * cn;
+    D->b1 = base + 11 * cn;
+    MP_HIP(launch_prep_pair(X.stream, P.C, *D, base + 6 * cn, base + 7 * cn, base + 8 * cn, base + 9 * cn,
+                            base + 10 * cn, base + 11 * cn));
     // the staging vector dies here: make the copies complete first
     MP_HIP(hipStreamSynchronize(X.stream));
 }

@@ -171,7 +171,12 @@ MP_HD void score_margins(const PairConst &C, const Model &m, const double (&K0i)
     r.wl = cal ? kSafe * gam(16) * (8.0 * t1 + 0.1) : 0.0;
     const double terms = C.n * (fabs(C.w[0]) * tau0 + fabs(C.w[1]) * tau1 + fabs(C.w[2]) * tau2);
     const double T = (kSafe * terms + C.mg_fixed) * (C.tie_scale > 1.0 ? C.tie_scale : 1.0);
-    r.tie = (T == T) ? T : inf; // (NaN: no screening)
+    // a non-finite model constant: no screening (its residuals may be NaN where no gate
+    // flags them, and the score kernel's minimum would drop the NaN)
+    double fin = r.o0 + r.s + r.o1s + m.focal0 + m.focal1;
+    for (int i = 0; i < 9; ++i) fin += r.R[i] + r.M0[i] + r.M1[i] + r.G[i];
+    for (int i = 0; i < 3; ++i) fin += r.t[i] + r.k0[i] + r.k1[i] + r.nrt[i];
+    r.tie = (T == T && fin - fin == 0.0) ? T : inf; // (NaN: no screening)
 }
 
 // Prepare the sweep constants of a model (host or device).  taus (nullable): the
@@ -302,7 +307,7 @@ MP_HD double reproj_err(const double *M, const double *k, double u, double v, do
     const double px = (M[0] * u + M[1] * v + M[2]) * a + k[0];
     const double py = (M[3] * u + M[4] * v + M[5]) * a + k[1];
     const double pz = (M[6] * u + M[7] * v + M[8]) * a + k[2];
-    flag = flag || fabs(pz - 1e-2) <= wz;
+    flag = flag || !(fabs(pz - 1e-2) > wz); // (NaN: flagged)
     if (pz < 1e-2) return DBL_MAX;
     const double iz = rcp_depth(pz);
     const double ex = px * iz - tu, ey = py * iz - tv;
@@ -345,7 +350,7 @@ MP_HD bool cheirality_rn(const double *rn, const double *n1, const double *t, do
 // (R a) r0) -- fewer FP64 instructions per (correspondence, model) than the matrix
 // form M0 = K1 R K0^-1 of reproj_err.
 MP_HD double reproj_ray(const double *q, const double *K, double bu, double bv, double wz, bool &flag) {
-    flag = flag || fabs(q[2] - 1e-2) <= wz;
+    flag = flag || !(fabs(q[2] - 1e-2) > wz); // (NaN: flagged)
     if (q[2] < 1e-2) return DBL_MAX;
     const double iz = rcp_depth(q[2]);
     const double dx = fma(q[0], iz, -bu), dy = fma(q[1], iz, -bv);

@@ -89,6 +89,9 @@ struct PairConst {
 struct PairData {
     const double *x0u, *x0v, *x1u, *x1v, *d0, *d1; // pixels (CAL) or normalized pixels (SF/TF)
     const double *r0, *r1;                          // 1/|K^-1 x| (CAL bearings), else unused
+    // CAL: the rays' first two components a = K0^-1 x0, b = K1^-1 x1 (prep_pair_kernel;
+    // the score kernel's ray form reads them instead of forming them per trip)
+    const double *a0 = nullptr, *a1 = nullptr, *b0 = nullptr, *b1 = nullptr;
     // Batch gate (nullable): the kernels of a batch launched before the previous batch's
     // results were read leave at once when that batch published a record (score_batch's
     // record word holds ~its epoch, gate_hi), i.e. when the host is bound to run LO and

@@ -16,8 +16,10 @@ __device__ inline bool batch_cancelled(const unsigned long long *word, unsigned 
            (unsigned)(__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == hi;
 }
 
-// r0/r1 = 1 / |K^-1 x| for the calibrated bearings
-hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1);
+// r0/r1 = 1 / |K^-1 x| for the calibrated bearings; a0 .. b1 (nullable, calibrated):
+// the rays' first two components, a = K0^-1 x0 and b = K1^-1 x1 (PairData::a0 .. b1)
+hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1,
+                            double *a0 = nullptr, double *a1 = nullptr, double *b0 = nullptr, double *b1 = nullptr);
 
 // MD minimal solver over the listed iterations (md_exact: R lanes per sample).
 hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,

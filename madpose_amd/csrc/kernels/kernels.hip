@@ -69,11 +69,21 @@ __device__ inline Corr load_corr(const PairConst &C, const PairData &D, int i, b
 }
 
 __device__ inline double msac(double e, double thr, double w) { return ((thr < e) ? thr : e) * w; }
-// the same term with thr * w precomputed (tw): the uniform value is selected directly
-// instead of being moved into a vector register first; bit-identical to msac
-__device__ inline double msac_tw(double e, double thr, double tw, double w) { return (thr < e) ? tw : e * w; }
+// the score kernel's term: min(e, thr) w by the hardware minimum (two instructions
+// instead of a compare, a product and two selects).  It differs from msac only for
+// e = NaN (std::min keeps the NaN, the hardware minimum returns thr), and every NaN
+// error of the kernel's residuals comes with a flag (eval_corr*), so its iteration is
+// decided on the host's reference-order sums
+__device__ inline double msac_min(double e, double thr, double w) {
+    // (v_min_f64 directly: fmin() would canonicalize both operands first, two more
+    // instructions per term)
+    double m;
+    asm("v_min_f64 %0, %1, %2" : "=v"(m) : "v"(e), "s"(thr));
+    return m * w;
+}
 
-__global__ void prep_pair_kernel(PairConst C, PairData D, double *r0, double *r1) {
+__global__ void prep_pair_kernel(PairConst C, PairData D, double *r0, double *r1, double *ra0, double *ra1,
+                                 double *rb0, double *rb1) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= C.n) return;
     const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
@@ -82,6 +92,39 @@ __global__ void prep_pair_kernel(PairConst C, PairData D, double *r0, double *r1
     matvec3(C.K1i, xb, b);
     r0[i] = 1.0 / sqrt(dot3(a, a));
     r1[i] = 1.0 / sqrt(dot3(b, b));
+    if (ra0) { // the rays as corr_rays forms them
+        Corr p;
+        p.x0u = xa[0];
+        p.x0v = xa[1];
+        p.x1u = xb[0];
+        p.x1v = xb[1];
+        p.r0 = p.r1 = 1.0;
+        corr_rays(C, p);
+        ra0[i] = p.a0;
+        ra1[i] = p.a1;
+        rb0[i] = p.b0;
+        rb1[i] = p.b1;
+    }
+}
+
+// the calibrated ray form's correspondence (eval_corr_cal_ray): the rays from
+// prep_pair_kernel, the unit bearing n1 = b r1 (b_2 = 1); x and n0 are not read
+__device__ inline Corr load_corr_ray(const PairData &D, int i) {
+    Corr p;
+    p.x0u = p.x0v = p.x1u = p.x1v = 0.0;
+    p.d0 = D.d0[i];
+    p.d1 = D.d1[i];
+    p.r0 = D.r0[i];
+    p.r1 = D.r1[i];
+    p.a0 = D.a0[i];
+    p.a1 = D.a1[i];
+    p.b0 = D.b0[i];
+    p.b1 = D.b1[i];
+    p.n0[0] = p.n0[1] = p.n0[2] = 0.0;
+    p.n1[0] = p.b0 * p.r1;
+    p.n1[1] = p.b1 * p.r1;
+    p.n1[2] = p.r1;
+    return p;
 }
 
 // estimator-level min-depth filter of the MD branch (src/hybrid_pose_estimator.cpp:80-85)
@@ -525,7 +568,6 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     for (int m = 0; m < MAXM; ++m) acc[m] = 0.0;
     const double t0 = C.thr[0], t1 = C.thr[1], t2 = C.thr[2];
     const double w0 = C.w[0], w1 = C.w[1], w2 = C.w[2];
-    const double tw0 = t0 * w0, tw1 = t1 * w1, tw2 = t2 * w2;
     __shared__ double part[2][kBlock / 64][MAXM];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned live = (nm >= 32) ? ~0u : ((1u << nm) - 1u); // uniform
@@ -533,7 +575,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     const int ntrip = (C.n + kBlock - 1) / kBlock;
     if (!EXIT) {
         for (int i = threadIdx.x; i < C.n; i += kBlock) {
-            Corr p = load_corr(C, D, i, V == kCal);
+            Corr p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
 #pragma unroll
             for (int m = 0; m < MAXM; ++m) {
                 if (m < nm) {
@@ -542,7 +584,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                         eval_corr_cal_ray(C, R[m], p, e0, e1, e2, flag);
                     else
                         eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2, flag);
-                    acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
+                    acc[m] += msac_min(e0, t0, w0) + msac_min(e1, t1, w1) + msac_min(e2, t2, w2);
                 }
             }
         }
@@ -551,7 +593,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     for (int trip = 0; EXIT && trip < ntrip; ++trip) {
         const int i = trip * kBlock + threadIdx.x;
         if (i < C.n) {
-            Corr p = load_corr(C, D, i, V == kCal);
+            Corr p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
 #pragma unroll
             for (int m = 0; m < MAXM; ++m) {
                 if ((live >> m) & 1u) {
@@ -560,7 +602,7 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                         eval_corr_cal_ray(C, R[m], p, e0, e1, e2, flag);
                     else
                         eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2, flag);
-                    acc[m] += msac_tw(e0, t0, tw0, w0) + msac_tw(e1, t1, tw1, w1) + msac_tw(e2, t2, tw2, w2);
+                    acc[m] += msac_min(e0, t0, w0) + msac_min(e1, t1, w1) + msac_min(e2, t2, w2);
                 }
             }
         }
@@ -688,7 +730,7 @@ __global__ void __launch_bounds__(kBlock) debug_terms_kernel(PairData D, PairCon
     const ScoreRec &r = recs[blockIdx.x];
     double *e = err + (size_t)blockIdx.x * 3 * C.n;
     for (int i = threadIdx.x; i < C.n; i += kBlock) {
-        const Corr p = load_corr(C, D, i, V == kCal);
+        const Corr p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
         double e0, e1, e2;
         bool flag = false;
         if (FAST && V == kCal)
@@ -945,9 +987,11 @@ template <class F> hipError_t by_variant(int v, F f) {
 
 } // namespace
 
-hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1) {
+hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D, double *r0, double *r1, double *a0,
+                            double *a1, double *b0, double *b1) {
     if (C.n <= 0) return hipSuccess;
-    prep_pair_kernel<<<(C.n + 255) / 256, 256, 0, s>>>(C, D, r0, r1);
+    const bool rays = C.variant == kCal && a0 && a1 && b0 && b1;
+    prep_pair_kernel<<<(C.n + 255) / 256, 256, 0, s>>>(C, D, r0, r1, rays ? a0 : nullptr, a1, b0, b1);
     return hipGetLastError();
 }
 
@@ -1137,7 +1181,7 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
                               Model *rec_out, uint8_t *flags8, IterResult *cand_out) {
     if (nb <= 0) return hipSuccess;
     if (maxm != max_models(C.variant)) return hipErrorInvalidValue;
-    const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
+    const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || (C.kstd && D.a0));
     bool exit = false;
     ScoreBound sb = score_bound(C, best, work, rec, epoch_hi, models, rec_out, &exit);
     sb.flags8 = flags8;
@@ -1187,7 +1231,7 @@ hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C,
 hipError_t launch_debug_terms(hipStream_t s, const PairData &D, const PairConst &C, const ScoreRec *recs, int nm,
                               double *err, int *flags) {
     if (nm <= 0) return hipSuccess;
-    const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || C.kstd);
+    const bool fast = C.score_type == 0 && !C.scale_only && (C.variant != kCal || (C.kstd && D.a0));
     return by_variant(C.variant, [&](auto V) {
         constexpr int v = decltype(V)::value;
         if (fast)
