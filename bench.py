@@ -211,6 +211,7 @@ def dist_info(world):
         info["lo_spin_us"] = None
     # rank 0's CPU share (pin_rank; empty when one rank has the node's share)
     info["cpu_share"] = {k: v for k, v in PIN_INFO.items() if k != "cpu_list"} or None
+    info["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
     return info
 
 
@@ -655,6 +656,9 @@ def pin_rank(local_rank, local_world):
     would let eight LM pools, LO lanes and samplers migrate across both sockets), and
     size the LM pool and its spin from the share.  MADPOSE_BENCH_PIN=0: no pinning."""
     if local_world <= 1 or os.environ.get("MADPOSE_BENCH_PIN") == "0" or not hasattr(os, "sched_setaffinity"):
+        # (one rank keeps the CPUs it was given; reported as unpinned)
+        if hasattr(os, "sched_getaffinity"):
+            PIN_INFO.update({"cpus": len(os.sched_getaffinity(0)), "pinned": False})
         return
     allowed = sorted(os.sched_getaffinity(0))
     bench_dev = os.environ.get("MADPOSE_BENCH_DEVICE")
@@ -666,7 +670,7 @@ def pin_rank(local_rank, local_world):
     # sampler and the LO lanes their cores; spin only on a share of its own
     os.environ.setdefault("MADPOSE_LO_THREADS", str(max(1, min(8, len(share) - 4))))
     os.environ.setdefault("MADPOSE_LO_SPIN", "300" if len(share) >= 12 else "0")
-    PIN_INFO.update({"cpus": len(share), "cpu_list": share, "gpu_local": bool(local),
+    PIN_INFO.update({"cpus": len(share), "cpu_list": share, "gpu_local": bool(local), "pinned": True,
                      "lo_threads": int(os.environ["MADPOSE_LO_THREADS"])})
 
 
@@ -726,6 +730,12 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    # hardware queues of the HIP runtime (read once, at its start): every estimator in
+    # flight drives two streams (main + MD side stream), and with HIP's default of 4
+    # queues the kernels of different pairs serialize behind each other -- ScanNet
+    # stand-in 943-946 pairs/s at 4 queues, 1302-1309 at 8, 1281-1337 at 16, 1232-1271
+    # at 24 (8 pairs in flight, profiles/r05/r5r)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
     import torch
     import torch.distributed as dist
