@@ -140,7 +140,14 @@ namespace {
 // (profiles/r04/lotab, tflo).  The wide workers wait on a counter of their own, so a
 // narrow job neither wakes them nor keeps them spinning.
 constexpr int kNarrow = 4;
-constexpr size_t kPoolWide = 8192;
+// (MADPOSE_LM_WIDE overrides the wide threshold, in blocks: an A/B knob)
+size_t pool_wide() {
+    static const size_t v = [] {
+        const char *e = std::getenv("MADPOSE_LM_WIDE");
+        return e ? (size_t)std::max(1L, std::atol(e)) : (size_t)8192;
+    }();
+    return v;
+}
 class Pool {
   public:
     explicit Pool(int n) {
@@ -318,7 +325,7 @@ double evaluate(const Ctx &C, const Params &p, double *H, double *g) {
             range(k * kChunk, std::min(nb, (k + 1) * kChunk), parts[k]);
         };
         if (nb >= kPoolBlocks)
-            lo_pool().run(nchunks, chunk, nb >= kPoolWide);
+            lo_pool().run(nchunks, chunk, nb >= pool_wide());
         else
             for (size_t k = 0; k < nchunks; ++k) chunk(k);
         for (size_t k = 0; k < nchunks; ++k) total.merge(parts[k]);
