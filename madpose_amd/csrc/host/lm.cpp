@@ -140,11 +140,14 @@ namespace {
 // (profiles/r04/lotab, tflo).  The wide workers wait on a counter of their own, so a
 // narrow job neither wakes them nor keeps them spinning.
 constexpr int kNarrow = 4;
-// (MADPOSE_LM_WIDE overrides the wide threshold, in blocks: an A/B knob)
+// every pool-sized problem is wide since round 5: the LO's serial all-inlier fit (the
+// prefix) 90-93 -> 82-88 us per calibrated LO with 8 threads instead of 4 (3 x 100
+// pairs on one box, profiles/r05/r5t); 12 threads oversubscribe the 16-CPU share
+// (prefix 132-134 us).  MADPOSE_LM_WIDE overrides the threshold, in blocks.
 size_t pool_wide() {
     static const size_t v = [] {
         const char *e = std::getenv("MADPOSE_LM_WIDE");
-        return e ? (size_t)std::max(1L, std::atol(e)) : (size_t)8192;
+        return e ? (size_t)std::max(1L, std::atol(e)) : (size_t)2048;
     }();
     return v;
 }
