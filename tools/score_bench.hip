@@ -44,7 +44,7 @@ static void bench(int B, std::mt19937 &rng) {
     const double ax[3] = {0.3, 1.0, 0.2};
     rot(ax, 0.25, Rg);
     const double tg[3] = {0.6, 0.05, 0.1};
-    std::vector<double> x0u(n), x0v(n), x1u(n), x1v(n), d0(n), d1(n), r0(n), r1(n);
+    std::vector<double> x0u(n), x0v(n), x1u(n), x1v(n), d0(n), d1(n), r0(n), r1(n), ra0(n), ra1(n), rb0(n), rb1(n);
     for (int i = 0; i < n; ++i) {
         const double X[3] = {2 * U(rng), 1.5 * U(rng), 4.5 + 3.5 * U(rng)};
         double Y[3];
@@ -58,6 +58,10 @@ static void bench(int B, std::mt19937 &rng) {
         d1[i] = Y[2] * std::exp(0.05 * G(rng));
         const double a[3] = {(x0u[i] - cx) / f, (x0v[i] - cy) / f, 1}, b[3] = {(x1u[i] - cx) / f, (x1v[i] - cy) / f, 1};
         r0[i] = 1 / std::sqrt(a[0] * a[0] + a[1] * a[1] + 1);
+        ra0[i] = a[0];
+        ra1[i] = a[1];
+        rb0[i] = b[0];
+        rb1[i] = b[1];
         r1[i] = 1 / std::sqrt(b[0] * b[0] + b[1] * b[1] + 1);
         if (V != kCal) { // normalized, pp-centred pixels
             x0u[i] = (x0u[i] - cx) / f;
@@ -73,6 +77,10 @@ static void bench(int B, std::mt19937 &rng) {
         return p;
     };
     PairData D{up(x0u), up(x0v), up(x1u), up(x1v), up(d0), up(d1), up(r0), up(r1)};
+    D.a0 = up(ra0); // (the calibrated ray form's precomputed rays, prep_pair_kernel)
+    D.a1 = up(ra1);
+    D.b0 = up(rb0);
+    D.b1 = up(rb1);
     PairConst C{};
     C.variant = V;
     C.n = n;
@@ -89,6 +97,8 @@ static void bench(int B, std::mt19937 &rng) {
     C.w[0] = C.w[1] = 1.0;
     C.w[2] = 2.0 * thr / thr2;
     C.loss_scale = 1.0 / ((1.0 / (2 * f) + 1.0 / (2 * f)) * (1.0 / (2 * f) + 1.0 / (2 * f)));
+    C.tie_scale = 1.0;
+    margin_consts(C); // (magnitudes left at zero: the margins are only placeholders here)
     std::vector<ScoreRec> recs((size_t)B * M);
     std::vector<int> counts(B);
     std::uniform_int_distribution<int> nmd(1, 4);
@@ -125,6 +135,7 @@ static void bench(int B, std::mt19937 &rng) {
     const int ntrip = (n + kBlock - 1) / kBlock;
     auto launch = [&](bool exit, double cut, int first, int every) {
         ScoreBound sb{cut, first, every, d_work};
+        sb.nb = B;
         if (exit)
             score_batch_kernel<V, M, true, true><<<B, kBlock>>>(D, C, d_recs, d_counts, d_scores, d_res, sb);
         else
