@@ -532,16 +532,17 @@ struct ScoreBound {
     // cand_out[b] (mapped host memory) -- the walk reads B bytes, not B IterResults
     uint8_t *flags8;
     IterResult *cand_out;
-    int nb; // iterations of the batch
 };
 
 // EXIT = false (no finite bound yet, or MADPOSE_SCORE_EXIT=0): the plain sweep,
-// without the trip-boundary checks and their barriers.  One iteration b of the batch
-// (the workgroup's; score_batch_kernel runs one or several per workgroup).
+// without the trip-boundary checks and their barriers.
 template <int V, int MAXM, bool FAST, bool EXIT>
-__device__ __forceinline__ void score_iteration(int b, const PairData &D, const PairConst &C,
-                                                const ScoreRec *__restrict__ recs, const int *__restrict__ counts,
-                                                double *scores, IterResult *res, const ScoreBound &sb) {
+__global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairConst C,
+                                                             const ScoreRec *__restrict__ recs,
+                                                             const int *__restrict__ counts, double *scores,
+                                                             IterResult *res, ScoreBound sb) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
+    const int b = blockIdx.x;
     const int nm = counts[b];
     if (nm == 0) {
         if (threadIdx.x == 0) {
@@ -717,21 +718,6 @@ __device__ __forceinline__ void score_iteration(int b, const PairData &D, const 
 #pragma unroll
             for (int q = 0; q < (int)(sizeof(Model) / sizeof(double)); ++q) dst[q] = src[q];
         }
-    }
-}
-
-// sb.nb iterations; a workgroup takes iterations blockIdx.x, + gridDim.x, ... (one each
-// when the grid covers the batch), with a barrier between them (the shared partials
-// are reused)
-template <int V, int MAXM, bool FAST, bool EXIT>
-__global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairConst C,
-                                                             const ScoreRec *__restrict__ recs,
-                                                             const int *__restrict__ counts, double *scores,
-                                                             IterResult *res, ScoreBound sb) {
-    if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
-    for (int b = blockIdx.x; b < sb.nb; b += gridDim.x) {
-        score_iteration<V, MAXM, FAST, EXIT>(b, D, C, recs, counts, scores, res, sb);
-        if (b + (int)gridDim.x < sb.nb) __syncthreads();
     }
 }
 
@@ -1200,20 +1186,13 @@ hipError_t launch_score_batch(hipStream_t s, const PairData &D, const PairConst 
     ScoreBound sb = score_bound(C, best, work, rec, epoch_hi, models, rec_out, &exit);
     sb.flags8 = flags8;
     sb.cand_out = cand_out;
-    sb.nb = nb;
-    // workgroups: one per iteration, or at most MADPOSE_SCORE_WGS (several iterations each)
-    static const int wgs_cap = [] {
-        const char *e = std::getenv("MADPOSE_SCORE_WGS");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    const int grid = (wgs_cap > 0 && nb > wgs_cap) ? wgs_cap : nb;
     auto go = [&](auto V, auto M, auto F) {
         constexpr int kV = decltype(V)::value, kM = decltype(M)::value;
         constexpr bool kF = decltype(F)::value;
         if (exit)
-            score_batch_kernel<kV, kM, kF, true><<<grid, kBlock, 0, s>>>(D, C, recs, counts, scores, res, sb);
+            score_batch_kernel<kV, kM, kF, true><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res, sb);
         else
-            score_batch_kernel<kV, kM, kF, false><<<grid, kBlock, 0, s>>>(D, C, recs, counts, scores, res, sb);
+            score_batch_kernel<kV, kM, kF, false><<<nb, kBlock, 0, s>>>(D, C, recs, counts, scores, res, sb);
     };
     using T = std::true_type;
     using F = std::false_type;

@@ -135,7 +135,6 @@ static void bench(int B, std::mt19937 &rng) {
     const int ntrip = (n + kBlock - 1) / kBlock;
     auto launch = [&](bool exit, double cut, int first, int every) {
         ScoreBound sb{cut, first, every, d_work};
-        sb.nb = B;
         if (exit)
             score_batch_kernel<V, M, true, true><<<B, kBlock>>>(D, C, d_recs, d_counts, d_scores, d_res, sb);
         else
