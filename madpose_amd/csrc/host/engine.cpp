@@ -1055,6 +1055,17 @@ class Run {
         S.nonmonotonic = cfg_.nonmonotonic;
         auto t_lm = Clock::now();
         lm_refine(P_.H, sample, S, m);
+        if (lo_timing_) {
+            const size_t nb = (S.use_reproj ? sample[0].size() + sample[1].size() : 0) +
+                              (S.use_sampson ? sample[2].size() : 0);
+            if (nb >= kBigLM) {
+                std::lock_guard<std::mutex> lk(lm_stat_mu_);
+                lm_stat_[0] += 1.0;
+                lm_stat_[1] += lm_last_evals;
+                lm_stat_[2] += secs(t_lm);
+                lm_stat_[3] += (double)nb;
+            }
+        }
         if (g_prof_on.load(std::memory_order_relaxed)) {
             const double dt = secs(t_lm);
             const size_t nb = (S.use_reproj ? sample[0].size() + sample[1].size() : 0) +
@@ -1361,6 +1372,11 @@ class Run {
     }();
     bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
     int launch_n_ = 0;
+    // big LM solves (>= kBigLM blocks) under MADPOSE_LO_TIMING: count, evaluations,
+    // seconds, blocks
+    const bool lo_timing_ = std::getenv("MADPOSE_LO_TIMING") != nullptr;
+    std::mutex lm_stat_mu_;
+    double lm_stat_[4] = {0, 0, 0, 0};
     // the fused MD + 5pt launch up to this batch size (MADPOSE_SOLVE_FUSE_MAX): larger
     // batches fill the GPU, where the fused kernel's 216 VGPRs (two waves per SIMD) cost
     // the 5pt root stage its third wave -- cal 5.62 (always fused) -> 5.46 ms per pair
@@ -1965,6 +1981,9 @@ void Run::run(Model *best, Stats *S) {
                      1e6 * lo_t_[5] / lo_t_[2], 1e6 * lo_t_[4], 1e6 * lo_t_[6] / lo_t_[2], 1e6 * lo_t_[7] / lo_t_[2],
                      1e6 * lo_t_[8] / lo_t_[2], 1e6 * lo_t_[9] / lo_t_[2], 1e6 * lo_t_[10] / lo_t_[2],
                      1e6 * lo_t_[11] / lo_t_[2], 1e6 * lo_t_[12] / lo_t_[2], lo_t_[13] / lo_t_[2]);
+    if (lo_timing_ && lm_stat_[0] > 0)
+        std::fprintf(stderr, "[engine] %d big LM solves: %.1f evaluations, %.0f blocks, %.1f us each (avg)\n",
+                     (int)lm_stat_[0], lm_stat_[1] / lm_stat_[0], lm_stat_[3] / lm_stat_[0], 1e6 * lm_stat_[2] / lm_stat_[0]);
     if (std::getenv("MADPOSE_LO_TIMING") && lo_t_[2] > 0)
         std::fprintf(stderr, "[engine] LO steps phase: before the parallel run %.1f us, the run %.1f us, the speculation "
                      "hook %.1f us (avg per LO)\n",

@@ -410,7 +410,10 @@ void quat_to_rot(const double *q0, double *R) {
     R[8] = 1 - 2 * (x * x + y * y);
 }
 
+thread_local int lm_last_evals = 0;
+
 bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettings &S, Model *m) {
+    lm_last_evals = 0;
     Ctx C;
     C.P = &P;
     C.sample = sample;
@@ -468,6 +471,7 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
     double Hbuf[2][kNFull * kNFull], gbuf[2][kNFull];
     double *H = Hbuf[0], *g = gbuf[0], *Hc = Hbuf[1], *gc = gbuf[1];
     double cost = evaluate(C, x, H, g);
+    lm_last_evals = 1;
     auto gmax = [&]() {
         double v = 0;
         for (int a = 0; a < n; ++a) v = std::max(v, std::fabs(g[a]));
@@ -542,6 +546,7 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
             // the candidate is evaluated with its normal equations: accepted steps
             // (the common case) then need no second pass
             const double cand_cost = evaluate(C, c, Hc, gc);
+            ++lm_last_evals;
             if (step_norm <= S.ptol * (xnorm + S.ptol)) break;
             if (std::fabs(cost - cand_cost) <= S.ftol * cost) break;
             double gd = 0, jd2 = 0;

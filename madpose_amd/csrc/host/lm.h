@@ -39,6 +39,8 @@ struct LMSettings {
 // sample[2] (Sampson).  Returns false when the problem has no residuals (Ceres
 // Solve() returning false); m is left unchanged in that case.
 bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettings &S, Model *m);
+// normal-equation evaluations of this thread's last lm_refine (MADPOSE_LO_TIMING)
+extern thread_local int lm_last_evals;
 
 // the LM pool's spin before blocking, in microseconds (MADPOSE_LO_SPIN, or the
 // affinity-based default of lm.cpp)
