@@ -3,10 +3,13 @@ all-inlier problem of every data type started near the ground truth, solved by t
 engine's host LM (`lm_refine_batch(..., on_host=True)`, the ctypes call included)
 `reps` times; prints microseconds per solve.  Run under MADPOSE_LO_THREADS=1/4/8 or
 MADPOSE_LM_ISA=avx2 for the pool / ISA split.  usage: python tools/lm_host_bench.py [reps]"""
+import os
 import sys
 import time
 
 import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import madpose
 from madpose_amd import synthetic
