@@ -655,6 +655,12 @@ def pin_rank(local_rank, local_world):
     share them (the estimator's host LO runs on these cores -- an unpinned 8-rank run
     would let eight LM pools, LO lanes and samplers migrate across both sockets), and
     size the LM pool and its spin from the share.  MADPOSE_BENCH_PIN=0: no pinning."""
+    explicit = os.environ.get("MADPOSE_BENCH_CPUS")  # an explicit CPU list for this process (A/B)
+    if explicit and hasattr(os, "sched_setaffinity"):
+        share = parse_cpulist(explicit)
+        os.sched_setaffinity(0, share)
+        PIN_INFO.update({"cpus": len(share), "cpu_list": share, "pinned": True, "explicit": True})
+        return
     if local_world <= 1 or os.environ.get("MADPOSE_BENCH_PIN") == "0" or not hasattr(os, "sched_setaffinity"):
         # (one rank keeps the CPUs it was given; reported as unpinned)
         if hasattr(os, "sched_getaffinity"):
