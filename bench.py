@@ -624,11 +624,27 @@ def cpu_siblings(cpus):
     return first
 
 
-def partition_cpus(local, allowed, core_of, devices):
+def cpu_l3(cpus):
+    """cpu -> the smallest CPU sharing its last-level cache (an EPYC CCD), from sysfs."""
+    first = {}
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                first[c] = min(parse_cpulist(f.read()))
+        except (OSError, ValueError):
+            first[c] = c
+    return first
+
+
+def partition_cpus(local, allowed, core_of, devices, l3_of=None):
     """Host CPUs for the ranks of one node: rank r runs on devices[r]; its candidates are
-    the allowed CPUs local to that GPU (all allowed CPUs when none is), and the ranks with
-    the same candidates split them into contiguous runs of whole cores.  local: CPU lists
-    per device (or None); core_of: cpu -> core id.  Returns one sorted CPU list per rank."""
+    the allowed CPUs local to that GPU (all allowed CPUs when none is).  With l3_of (cpu
+    -> last-level-cache id) and at least as many complete L3 domains among the candidates
+    as ranks sharing them, each rank gets one L3 domain (spread evenly over them): the
+    estimator's LO threads and LM pool synchronize through that cache.  Otherwise the
+    ranks with the same candidates split them into contiguous runs of whole cores.
+    local: CPU lists per device (or None); core_of: cpu -> core id.  Returns one sorted
+    CPU list per rank."""
     allowed = sorted(set(allowed))
     cand = []
     for d in devices:
@@ -637,8 +653,19 @@ def partition_cpus(local, allowed, core_of, devices):
     out = [None] * len(devices)
     for key in dict.fromkeys(cand):
         ranks = [r for r in range(len(devices)) if cand[r] == key]
-        cores = sorted(dict.fromkeys(core_of.get(c, c) for c in key))
         k = len(ranks)
+        if l3_of:
+            groups = {}
+            for c in key:
+                groups.setdefault(l3_of.get(c, c), []).append(c)
+            # complete domains only (every CPU of the domain allowed), largest first
+            full = [sorted(g) for g in groups.values() if len(g) >= max(len(v) for v in groups.values())]
+            full.sort(key=lambda g: g[0])
+            if len(full) >= k and len(full[0]) >= 2:
+                for j, r in enumerate(ranks):
+                    out[r] = full[j * len(full) // k]
+                continue
+        cores = sorted(dict.fromkeys(core_of.get(c, c) for c in key))
         for j, r in enumerate(ranks):
             lo, hi = len(cores) * j // k, len(cores) * (j + 1) // k
             mine = set(cores[lo:hi]) if hi > lo else {cores[j % len(cores)]}
@@ -650,19 +677,20 @@ PIN_INFO = {}  # this rank's CPU share (reported under "dist")
 
 
 def pin_rank(local_rank, local_world):
-    """One rank of several on this node: pin the process, before any GPU call and before
-    the engine's threads exist, to the CPUs local to its GPU, split with the ranks that
-    share them (the estimator's host LO runs on these cores -- an unpinned 8-rank run
-    would let eight LM pools, LO lanes and samplers migrate across both sockets), and
-    size the LM pool and its spin from the share.  MADPOSE_BENCH_PIN=0: no pinning."""
+    """Pin this rank (one of local_world on the node, possibly the only one), before any
+    GPU call and before the engine's threads exist, to the CPUs local to its GPU -- one
+    last-level-cache domain when there are enough of them, else a split of whole cores
+    with the ranks that share them (the estimator's host LO runs on these cores: unpinned
+    ranks let their LM pools, LO lanes and samplers migrate across CCDs and sockets) --
+    and size the LM pool and its spin from the share.  MADPOSE_BENCH_PIN=0: no pinning;
+    MADPOSE_BENCH_CPUS=list: exactly these CPUs."""
     explicit = os.environ.get("MADPOSE_BENCH_CPUS")  # an explicit CPU list for this process (A/B)
     if explicit and hasattr(os, "sched_setaffinity"):
         share = parse_cpulist(explicit)
         os.sched_setaffinity(0, share)
         PIN_INFO.update({"cpus": len(share), "cpu_list": share, "pinned": True, "explicit": True})
         return
-    if local_world <= 1 or os.environ.get("MADPOSE_BENCH_PIN") == "0" or not hasattr(os, "sched_setaffinity"):
-        # (one rank keeps the CPUs it was given; reported as unpinned)
+    if os.environ.get("MADPOSE_BENCH_PIN") == "0" or not hasattr(os, "sched_setaffinity"):
         if hasattr(os, "sched_getaffinity"):
             PIN_INFO.update({"cpus": len(os.sched_getaffinity(0)), "pinned": False})
         return
@@ -670,13 +698,18 @@ def pin_rank(local_rank, local_world):
     bench_dev = os.environ.get("MADPOSE_BENCH_DEVICE")
     devices = [int(bench_dev) if bench_dev is not None else r for r in range(local_world)]
     local = gpu_local_cpus()
-    share = partition_cpus(local, allowed, cpu_siblings(allowed), devices)[local_rank]
+    # one rank too: unpinned, its threads float over the host (a 16-CPU quota on 256
+    # CPUs on the MI355X boxes) and the LO's pool synchronizes across CCDs and sockets --
+    # big LM solves 77-86 us unpinned, 28 us pinned to one CCD (8 cores + SMT), cal
+    # 5.68-5.91 -> 4.71-4.92 ms per pair (profiles/r05/r5pa)
+    share = partition_cpus(local, allowed, cpu_siblings(allowed), devices, cpu_l3(allowed))[local_rank]
     os.sched_setaffinity(0, share)
     # the LM pool: the calling thread plus up to 7 workers, leaving the estimator, the
     # sampler and the LO lanes their cores; spin only on a share of its own
     os.environ.setdefault("MADPOSE_LO_THREADS", str(max(1, min(8, len(share) - 4))))
     os.environ.setdefault("MADPOSE_LO_SPIN", "300" if len(share) >= 12 else "0")
     PIN_INFO.update({"cpus": len(share), "cpu_list": share, "gpu_local": bool(local), "pinned": True,
+                     "l3_domains": len(set(cpu_l3(share).values())),
                      "lo_threads": int(os.environ["MADPOSE_LO_THREADS"])})
 
 
