@@ -662,8 +662,12 @@ def partition_cpus(local, allowed, core_of, devices, l3_of=None):
             full = [sorted(g) for g in groups.values() if len(g) >= max(len(v) for v in groups.values())]
             full.sort(key=lambda g: g[0])
             if len(full) >= k and len(full[0]) >= 2:
+                # (from the last domain down: the first CCD of a host is where its system
+                # work runs -- a single pair pinned there once took 20.6 ms instead of
+                # 4.8, profiles/r05/r5pb; the last CCD of either socket gave 4.75-5.02,
+                # r5pc)
                 for j, r in enumerate(ranks):
-                    out[r] = full[j * len(full) // k]
+                    out[r] = full[len(full) - 1 - j * len(full) // k]
                 continue
         cores = sorted(dict.fromkeys(core_of.get(c, c) for c in key))
         for j, r in enumerate(ranks):
@@ -676,7 +680,7 @@ def partition_cpus(local, allowed, core_of, devices, l3_of=None):
 PIN_INFO = {}  # this rank's CPU share (reported under "dist")
 
 
-def pin_rank(local_rank, local_world):
+def pin_rank(local_rank, local_world, per_ccd=True):
     """Pin this rank (one of local_world on the node, possibly the only one), before any
     GPU call and before the engine's threads exist, to the CPUs local to its GPU -- one
     last-level-cache domain when there are enough of them, else a split of whole cores
@@ -702,7 +706,13 @@ def pin_rank(local_rank, local_world):
     # CPUs on the MI355X boxes) and the LO's pool synchronizes across CCDs and sockets --
     # big LM solves 77-86 us unpinned, 28 us pinned to one CCD (8 cores + SMT), cal
     # 5.68-5.91 -> 4.71-4.92 ms per pair (profiles/r05/r5pa)
-    share = partition_cpus(local, allowed, cpu_siblings(allowed), devices, cpu_l3(allowed))[local_rank]
+    if local_world <= 1 and not per_ccd:
+        # (a single rank with many pairs in flight, the ScanNet stand-in, wants cores more
+        # than one cache: 960 pairs/s unpinned against 883 on one CCD, r5pb)
+        PIN_INFO.update({"cpus": len(allowed), "pinned": False})
+        return
+    share = partition_cpus(local, allowed, cpu_siblings(allowed), devices,
+                           cpu_l3(allowed) if per_ccd else None)[local_rank]
     os.sched_setaffinity(0, share)
     # the LM pool: the calling thread plus up to 7 workers, leaving the estimator, the
     # sampler and the LO lanes their cores; spin only on a share of its own
@@ -768,7 +778,7 @@ def main(argv=None):
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)), per_ccd=a.workload != "scannet")
     # hardware queues of the HIP runtime (read once, at its start): every estimator in
     # flight drives two streams (main + MD side stream), and with HIP's default of 4
     # queues the kernels of different pairs serialize behind each other -- ScanNet

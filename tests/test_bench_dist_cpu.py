@@ -229,9 +229,9 @@ def test_forced_one_rank_group_gathers_through_the_collective():
 
 def test_cpu_partition_one_l3_domain_per_rank():
     """A two-socket host with 16 CCDs of 8 cores (CPU c and c + 128 are SMT siblings,
-    CCD = c // 8 of the core): a single rank gets one whole CCD with its siblings; 8 ranks
-    without GPU locality get 8 distinct CCDs spread over the host; 20 ranks (more than
-    the domains) fall back to splitting whole cores."""
+    CCD = c // 8 of the core): a single rank gets one whole CCD with its siblings (the
+    last one); 8 ranks without GPU locality get 8 distinct CCDs spread over the host; 20
+    ranks (more than the domains) fall back to splitting whole cores."""
     sys.path.insert(0, ROOT)
     import bench
 
@@ -239,12 +239,12 @@ def test_cpu_partition_one_l3_domain_per_rank():
     core_of = {c: c % 128 for c in cpus}
     l3_of = {c: (c % 128) // 8 * 8 for c in cpus}
     one = bench.partition_cpus(None, cpus, core_of, [0], l3_of)[0]
-    assert one == list(range(0, 8)) + list(range(128, 136))
+    assert one == list(range(120, 128)) + list(range(248, 256))  # the last CCD
     parts = bench.partition_cpus(None, cpus, core_of, list(range(8)), l3_of)
     doms = [{l3_of[c] for c in p} for p in parts]
     assert all(len(d) == 1 and len(p) == 16 for d, p in zip(doms, parts))
     assert len({next(iter(d)) for d in doms}) == 8
-    assert {next(iter(d)) for d in doms} == {16 * j for j in range(8)}  # every other CCD
+    assert {next(iter(d)) for d in doms} == {120 - 16 * j for j in range(8)}  # every other CCD from the top
     parts = bench.partition_cpus(None, cpus, core_of, list(range(20)), l3_of)
     seen = set()
     for p in parts:
