@@ -783,8 +783,9 @@ def main(argv=None):
     # flight drives two streams (main + MD side stream), and with HIP's default of 4
     # queues the kernels of different pairs serialize behind each other -- ScanNet
     # stand-in 943-946 pairs/s at 4 queues, 1302-1309 at 8, 1281-1337 at 16, 1232-1271
-    # at 24 (8 pairs in flight, profiles/r05/r5r)
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    # at 24 (8 pairs in flight, profiles/r05/r5r).  The boxes export 4, so it is set, not
+    # defaulted; MADPOSE_HW_QUEUES overrides the 16.
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MADPOSE_HW_QUEUES", "16")
 
     import torch
     import torch.distributed as dist
