@@ -796,13 +796,14 @@ class Run {
         // 903 / 982 / 998 pairs/s at 128 / 512 / 1000 on one box, profiles/r03/s6)
         min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 1024;
         min_batch_ = std::min(min_batch_, max_batch_);
-        // growth: 1, and 2 for the shared focal, whose pair waits on the GPU (≈ 380 us of
-        // latency-bound point chain per batch, flat in the batch size): fewer, larger
-        // batches -- sf 11.48 / 11.48 / 11.49 ms at 1, 11.20 / 10.97 / 11.18 at 2, 10.88 /
-        // 11.16 / 11.13 at 3 on one box (profiles/r04/gab2); for cal, 0.5 and the
-        // waste it saves cost more round trips than they save work (gab)
+        // growth 1 for every variant: round 4 ran the shared focal at 2 (fewer, larger
+        // batches for its latency-bound chain: 11.48 -> 10.97-11.20 ms, profiles/r04/gab2)
+        // at 1.49 solved per accepted hypothesis; with the round-5 host the difference is
+        // 10.62 (1.33) against 10.39 ms (1.42), 1.5: 10.50 (1.38), 3 x 60 pairs on one
+        // box (profiles/r05/r5sg).  For cal, 0.5 and the waste it saves cost more round
+        // trips than they save work (r04 gab)
         const char *env3 = std::getenv("MADPOSE_BATCH_GROWTH");
-        growth_ = env3 ? std::max(0.01, std::atof(env3)) : (variant_ == kSF ? 2.0 : 1.0);
+        growth_ = env3 ? std::max(0.01, std::atof(env3)) : 1.0;
         trace_ = std::getenv("MADPOSE_TRACE") != nullptr;
     }
 
