@@ -590,16 +590,10 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         }
         work = nm * ntrip;
     }
-    // the next trip's correspondence is loaded before this trip's models are evaluated
-    // (its L2 latency then overlaps them instead of stalling the wave at the trip's start)
-    auto load = [&](int i) { return (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal); };
-    Corr p_next{};
-    if (EXIT && (int)threadIdx.x < C.n) p_next = load(threadIdx.x);
     for (int trip = 0; EXIT && trip < ntrip; ++trip) {
         const int i = trip * kBlock + threadIdx.x;
-        const Corr p = p_next;
-        if (trip + 1 < ntrip && i + kBlock < C.n) p_next = load(i + kBlock);
         if (i < C.n) {
+            Corr p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
 #pragma unroll
             for (int m = 0; m < MAXM; ++m) {
                 if ((live >> m) & 1u) {
