@@ -346,7 +346,14 @@ struct BatchBufs {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr}; // solve start / score start / score end
     hipEvent_t ev_fork = nullptr, ev_join = nullptr; // MD side stream fork / join
     hipEvent_t ev_h2d = nullptr;                    // the batch's samples have been copied
+    hipEvent_t ev_solved = nullptr;                 // the batch's solver kernels are done
     hipEvent_t ev_done = nullptr;                   // the batch's results are on the host
+    // each slot's batches run on the slot's stream from the slot's sample buffer: a
+    // continuation in the other slot solves while this slot's batch is scored (it waits
+    // for this slot's ev_solved first: the point solvers' workspace and the MD side
+    // stream are shared)
+    hipStream_t stream = nullptr;
+    int *d_samples = nullptr;
     unsigned epoch_hi = 0;                          // ~epoch of the batch last launched here
     bool h2d_pending = false;                       // launched, ev_h2d not yet waited for
 };
@@ -357,7 +364,6 @@ struct DeviceCtx {
     int64_t cap_n = 0;
     int cap_b = 0, cap_m = 0;
     double *d_pair = nullptr; // 12 arrays of cap_n (PairData)
-    int *d_samples = nullptr; // a batch's samples + iteration lists (draw_batch layout; stream-ordered)
     // score_batch's record word (kernels.hip ScoreBound::rec) and the batch epoch
     unsigned long long *d_recword = nullptr;
     uint32_t epoch = 0;
@@ -384,7 +390,7 @@ struct DeviceCtx {
 
     void free_all() {
         hipSetDevice(device);
-        for (void *p : {(void *)d_pair, (void *)d_samples, (void *)d_recword, (void *)d_rec1, (void *)d_err,
+        for (void *p : {(void *)d_pair, (void *)bb[0].d_samples, (void *)bb[1].d_samples, (void *)d_recword, (void *)d_rec1, (void *)d_err,
                         (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_pen, (void *)d_pt_ncand, (void *)d_pt_valid,
                         (void *)d_pt_slots})
             if (p) hipFree(p);
@@ -405,7 +411,7 @@ struct DeviceCtx {
             q.h2d_pending = false;
         }
         d_pair = d_err = d_score1 = nullptr;
-        d_samples = nullptr;
+        bb[0].d_samples = bb[1].d_samples = nullptr;
         d_recword = nullptr;
         d_rec1 = nullptr;
         d_pt_cand = d_pt_pen = nullptr;
@@ -428,7 +434,7 @@ struct DeviceCtx {
         free_all();
         MP_HIP(hipMalloc(&d_pair, sizeof(double) * 12 * nn));
         MP_HIP(hipMalloc(&d_err, sizeof(double) * 3 * nn));
-        MP_HIP(hipMalloc(&d_samples, sizeof(int) * 9 * bb_));
+        for (BatchBufs &q : bb) MP_HIP(hipMalloc(&q.d_samples, sizeof(int) * 9 * bb_));
         MP_HIP(hipMalloc(&d_recword, sizeof(unsigned long long)));
         MP_HIP(hipMemset(d_recword, 0xff, sizeof(unsigned long long)));
         for (BatchBufs &q : bb) {
@@ -509,8 +515,11 @@ struct CtxLease {
             MP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             MP_HIP(hipStreamCreateWithFlags(&c->md_stream, hipStreamNonBlocking));
             MP_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+            c->bb[0].stream = c->stream;
+            MP_HIP(hipStreamCreateWithFlags(&c->bb[1].stream, hipStreamNonBlocking));
             for (BatchBufs &q : c->bb) {
                 for (auto &e : q.ev) MP_HIP(hipEventCreate(&e));
+                MP_HIP(hipEventCreateWithFlags(&q.ev_solved, hipEventDisableTiming));
                 MP_HIP(hipEventCreateWithFlags(&q.ev_fork, hipEventDisableTiming));
                 MP_HIP(hipEventCreateWithFlags(&q.ev_join, hipEventDisableTiming));
                 MP_HIP(hipEventCreateWithFlags(&q.ev_h2d, hipEventDisableTiming));
@@ -1365,13 +1374,19 @@ class Run {
     // continuation waits for the sampler thread to finish launching it (the speculation
     // hook 31-48 us instead of 4 us, the LO steps phase 221-233 vs 180-194 us, cal 5.90-
     // 5.99 vs 5.80-5.86 ms, profiles/r04/hook2/)
-    // (continuations of the big growth-phase batches only, >= 8192 iterations, measured
-    // slower too: cal 5.62 -> 5.86 ms per pair over 3 x 200 pairs, profiles/r05/r5o)
+    // =3: continuations of at least kEarlyMinBatch iterations while alone on the device
+    // (the growth phase, where new bests are rare): each slot has its own stream, so the
+    // continuation's solvers run while this batch is scored.  (On one stream, round 5's
+    // first form, it measured slower: cal 5.62 -> 5.86 ms per pair, profiles/r05/r5o.)
     const int early_mode_ = [] {
         const char *e = std::getenv("MADPOSE_EARLY_CONT");
-        return e ? (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0)) : 0;
+        return e ? (e[0] == '3' ? 3 : (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0))) : 0;
     }();
-    bool early_now() const { return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1); }
+    static constexpr uint32_t kEarlyMinBatch = 4096;
+    bool early_now(uint32_t Bn) const {
+        return early_mode_ == 2 || (early_mode_ == 1 && active_runs(X_.device) <= 1) ||
+               (early_mode_ == 3 && Bn >= kEarlyMinBatch && active_runs(X_.device) <= 1);
+    }
     int launch_n_ = 0;
     // big LM solves (>= kBigLM blocks) under MADPOSE_LO_TIMING: count, evaluations,
     // seconds, blocks
@@ -1395,8 +1410,9 @@ class Run {
     void launch_batch(const Batch &g, double best, bool cut_on_record, const BatchBufs *gate_prev = nullptr) {
         const uint32_t B = g.B;
         const int nmd = g.nmd, npt = g.npt;
-        hipStream_t s = X_.stream;
         BatchBufs &Q = X_.bb[g.slot];
+        const BatchBufs &O = X_.bb[g.slot ^ 1];
+        hipStream_t s = Q.stream;
         const bool prof = g_prof_on.load(std::memory_order_relaxed);
         batch_prof_[g.slot] = prof;
         PairData D = D_;
@@ -1405,11 +1421,13 @@ class Run {
             D.gate_hi = gate_prev->epoch_hi;
         }
         // one upload: samples, then the MD list and the (descending) point list
-        MP_HIP(hipMemcpyAsync(X_.d_samples, slot_ptr(g.slot), sizeof(int) * 9 * (size_t)B, hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(Q.d_samples, slot_ptr(g.slot), sizeof(int) * 9 * (size_t)B, hipMemcpyHostToDevice, s));
         tl_.mark("  h2d");
         MP_HIP(hipEventRecord(Q.ev_h2d, s));
         Q.h2d_pending = true;
-        const int *d_md_list = X_.d_samples + 8 * (size_t)B, *d_pt_list = d_md_list + nmd;
+        const int *d_md_list = Q.d_samples + 8 * (size_t)B, *d_pt_list = d_md_list + nmd;
+        // (the other slot's batch may still be solving: the solvers' workspace is shared)
+        MP_HIP(hipStreamWaitEvent(s, O.ev_solved, 0));
         if (prof) MP_HIP(hipEventRecord(Q.ev[0], s));
         // MD iterations on the side stream, point iterations on the main one (they
         // write disjoint model slots); scoring waits for both -- or, calibrated, both in
@@ -1417,21 +1435,22 @@ class Run {
         const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen};
         const bool fused = solve_fusable(P_.C) && (int64_t)B <= fuse_max_;
         if (fused) {
-            MP_HIP(launch_solve_fused(s, D, P_.C, d_md_list, nmd, d_pt_list, npt, X_.d_samples, W, Q.d_models,
+            MP_HIP(launch_solve_fused(s, D, P_.C, d_md_list, nmd, d_pt_list, npt, Q.d_samples, W, Q.d_models,
                                       Q.d_recs, Q.d_counts, maxm_));
             tl_.mark("  solve_launched");
         } else {
             if (nmd > 0) {
                 MP_HIP(hipEventRecord(Q.ev_fork, s));
                 MP_HIP(hipStreamWaitEvent(X_.md_stream, Q.ev_fork, 0));
-                MP_HIP(launch_md_solve(X_.md_stream, D, P_.C, d_md_list, nmd, X_.d_samples, Q.d_models, Q.d_recs,
+                MP_HIP(launch_md_solve(X_.md_stream, D, P_.C, d_md_list, nmd, Q.d_samples, Q.d_models, Q.d_recs,
                                        Q.d_counts, maxm_));
                 MP_HIP(hipEventRecord(Q.ev_join, X_.md_stream));
             }
-            MP_HIP(launch_pt_solve(s, D, P_.C, d_pt_list, npt, X_.d_samples, W, Q.d_models, Q.d_recs, Q.d_counts,
+            MP_HIP(launch_pt_solve(s, D, P_.C, d_pt_list, npt, Q.d_samples, W, Q.d_models, Q.d_recs, Q.d_counts,
                                    maxm_));
             if (nmd > 0) MP_HIP(hipStreamWaitEvent(s, Q.ev_join, 0));
         }
+        MP_HIP(hipEventRecord(Q.ev_solved, s));
         if (prof) MP_HIP(hipEventRecord(Q.ev[1], s));
         const unsigned epoch_hi = ~(++X_.epoch);
         Q.epoch_hi = epoch_hi;
@@ -1443,6 +1462,12 @@ class Run {
         MP_HIP(hipMemcpyAsync(Q.h_flags8, Q.d_flags8, (size_t)B, hipMemcpyDeviceToHost, s));
         if (prof) MP_HIP(hipMemcpyAsync(Q.h_work, Q.d_work, sizeof(int) * B, hipMemcpyDeviceToHost, s));
         MP_HIP(hipEventRecord(Q.ev_done, s));
+    }
+    // every batch launched from this run has finished (both slots' streams and the MD
+    // side stream)
+    void drain_batches() {
+        for (const BatchBufs &q : X_.bb) MP_HIP(hipStreamSynchronize(q.stream));
+        MP_HIP(hipStreamSynchronize(X_.md_stream));
     }
     // before host sample slot `slot` is redrawn: the last batch launched from it must
     // have been copied to the device (an early continuation may still be queued)
@@ -1656,7 +1681,7 @@ void Run::run(Model *best, Stats *S) {
                     }
                 } else {
                     X_.sampler->cancel();
-                    MP_HIP(hipStreamSynchronize(X_.stream)); // a launched speculation drains
+                    drain_batches(); // a launched speculation drains
                 }
             }
         }
@@ -1700,7 +1725,7 @@ void Run::run(Model *best, Stats *S) {
         const uint32_t Bn = (it_next < max_total && it_next != lo_start)
                                 ? batch_size(it_next, grow(it_next))
                                 : 0;
-        const bool early = Bn > 0 && early_now();
+        const bool early = Bn > 0 && early_now(Bn);
         if (Bn > 0) {
             slot_free(cur ^ 1);
             if (early) {
@@ -1934,7 +1959,7 @@ void Run::run(Model *best, Stats *S) {
                 }
             } else {
                 X_.sampler->cancel();
-                MP_HIP(hipStreamSynchronize(X_.stream)); // a launched speculation drains
+                drain_batches(); // a launched speculation drains
             }
         } else {
             if (Bn > 0) X_.sampler->cancel();
@@ -1943,6 +1968,10 @@ void Run::run(Model *best, Stats *S) {
         bcur = (int)grow(it);
     }
     if (!done) S->num_iterations_total = it;
+    // (a continuation launched past the end may still be in flight: the next run reuses
+    // the buffers)
+    X_.sampler->cancel();
+    drain_batches();
 
     if (S->num_iterations_total <= lo_start && S->best_model_score < kMax) {
         ++S->number_lo_iterations;
