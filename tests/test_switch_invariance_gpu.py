@@ -23,7 +23,7 @@ WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "switch_worker
 SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOSE_EARLY_CONT": "2"},
             "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "mdx_two_lanes": {"MADPOSE_MDX_R": "2"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
             "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"},
-            "solve_unfused": {"MADPOSE_SOLVE_FUSE": "0"}}
+            "solve_unfused": {"MADPOSE_SOLVE_FUSE": "0"}, "early_big": {"MADPOSE_EARLY_CONT": "3"}}
 
 
 def _run(extra):
