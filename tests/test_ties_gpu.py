@@ -109,6 +109,35 @@ def test_score_batch_flags_duplicated_model_as_ambiguous():
     assert not (s[1] & AMB)
 
 
+def test_ambiguity_is_two_sided(monkeypatch):
+    """Two models whose device scores differ by d: the best one's reference score can be
+    up to S1 + T1 and the other's as low as S2 - T2, so the iteration is ambiguous when
+    d <= T1 + T2 -- also when each margin alone is below d -- and not when
+    T1 + T2 < d.  The margins are scaled by MADPOSE_TIE_SCALE around d."""
+    rng = np.random.default_rng(11)
+    p = synthetic.make_pair(11, n=800)
+    o, c = synthetic.example_options("calibrated")
+    ms = _models_near_gt(p, rng, 6, 0)
+    args = (0, p["x0"], p["x1"], p["depth0"], p["depth1"], p["K0"], p["K1"], o, c)
+    big = np.finfo(np.float64).max
+    sc, _, _, bd = api.debug_score_batch(*args, [[m] for m in ms], best=big, exit=False, record_skip=False)
+    t = np.array([x[0] for x in bd["tie"]])
+    order = np.argsort(sc)
+    i, j = int(order[0]), int(order[1])  # the two best, scores s_i < s_j
+    d = sc[j] - sc[i]
+    assert d > 0
+    tbar = 0.5 * (t[i] + t[j])
+    for frac, amb in ((0.75, True), (0.4, False)):
+        k = frac * d / tbar
+        assert k > 1.0  # (the scale only widens)
+        monkeypatch.setenv("MADPOSE_TIE_SCALE", repr(k))
+        _, slots, _, bd2 = api.debug_score_batch(*args, [[ms[i], ms[j]]], best=big, exit=False, record_skip=False)
+        T = bd2["tie"][0]
+        assert T[0] < d and T[1] < d  # each margin alone below the gap
+        assert bool(slots[0] & AMB) == amb, (frac, T, d)
+        assert (slots[0] & 0xffff) == 0  # the first model is the device's best
+
+
 @pytest.mark.parametrize("variant,seed", [(0, 0), (0, 3), (1, 1), (2, 2)])
 def test_tie_margin_inflated_parity(variant, seed, monkeypatch):
     """MADPOSE_TIE_SCALE=1e7 widens the margins (about 1e-9 of a score by default) to a
