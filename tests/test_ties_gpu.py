@@ -130,7 +130,7 @@ def test_ambiguity_is_two_sided(monkeypatch):
     for frac, amb in ((0.75, True), (0.4, False)):
         k = frac * d / tbar
         assert k > 1.0  # (the scale only widens)
-        monkeypatch.setenv("MADPOSE_TIE_SCALE", repr(k))
+        monkeypatch.setenv("MADPOSE_TIE_SCALE", repr(float(k)))
         _, slots, _, bd2 = api.debug_score_batch(*args, [[ms[i], ms[j]]], best=big, exit=False, record_skip=False)
         T = bd2["tie"][0]
         assert T[0] < d and T[1] < d  # each margin alone below the gap
