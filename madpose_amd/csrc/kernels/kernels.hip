@@ -590,63 +590,73 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
         }
         work = nm * ntrip;
     }
-    for (int trip = 0; EXIT && trip < ntrip; ++trip) {
-        const int i = trip * kBlock + threadIdx.x;
-        if (i < C.n) {
-            Corr p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
+    // the trip loop over the first NM model slots: a separate instance for iterations with
+    // one model (most of them), whose model constants then stay in scalar registers
+    // across the trips instead of being reloaded with every trip
+    auto trips = [&](auto nmc) {
+        constexpr int NM = decltype(nmc)::value;
+        for (int trip = 0; EXIT && trip < ntrip; ++trip) {
+            const int i = trip * kBlock + threadIdx.x;
+            if (i < C.n) {
+                Corr p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
 #pragma unroll
-            for (int m = 0; m < MAXM; ++m) {
-                if ((live >> m) & 1u) {
-                    double e0, e1, e2;
-                    if (FAST && V == kCal)
-                        eval_corr_cal_ray(C, R[m], p, e0, e1, e2, flag);
-                    else
-                        eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2, flag);
-                    acc[m] += msac_min(e0, t0, w0) + msac_min(e1, t1, w1) + msac_min(e2, t2, w2);
-                }
-            }
-        }
-        work += __popc(live);
-        const int done = trip + 1;
-        if (done < ntrip && done >= sb.first && (done - sb.first) % sb.every == 0) {
-            const int par = checks & 1; // double-buffered: one barrier per check
-            if (threadIdx.x == 0) {
-                s_skip[par] = (unsigned)(recw >> 32) == sb.epoch_hi && (int)(unsigned)(recw & 0xffffffffu) < b;
-                if (sb.rec) recw = __hip_atomic_load(sb.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int m = 0; m < MAXM; ++m) {
-                if ((live >> m) & 1u) {
-                    const double v = wave_sum(acc[m]);
-                    if (lane == 0) part[par][wave][m] = v;
-                }
-            }
-            const bool wf = __any(flag);
-            if (lane == 0) s_flag[par][wave] = wf;
-            __syncthreads();
-#pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) uncertain = uncertain || s_flag[par][w] != 0;
-            unsigned keep = live;
-            if (!uncertain) {
-#pragma unroll
-                for (int m = 0; m < MAXM; ++m) {
+                for (int m = 0; m < NM; ++m) {
                     if ((live >> m) & 1u) {
-                        double v = 0.0;
-#pragma unroll
-                        for (int w = 0; w < kBlock / 64; ++w) v += part[par][w][m];
-                        if (v - R[m].tie >= sb.best) keep &= ~(1u << m);
+                        double e0, e1, e2;
+                        if (FAST && V == kCal)
+                            eval_corr_cal_ray(C, R[m], p, e0, e1, e2, flag);
+                        else
+                            eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2, flag);
+                        acc[m] += msac_min(e0, t0, w0) + msac_min(e1, t1, w1) + msac_min(e2, t2, w2);
                     }
                 }
             }
-            live = __builtin_amdgcn_readfirstlane(keep);
-            if (s_skip[par]) { // (uniform) a record earlier in the batch: this iteration is discarded
-                live = 0;
-                skipped = true;
+            work += __popc(live);
+            const int done = trip + 1;
+            if (done < ntrip && done >= sb.first && (done - sb.first) % sb.every == 0) {
+                const int par = checks & 1; // double-buffered: one barrier per check
+                if (threadIdx.x == 0) {
+                    s_skip[par] = (unsigned)(recw >> 32) == sb.epoch_hi && (int)(unsigned)(recw & 0xffffffffu) < b;
+                    if (sb.rec) recw = __hip_atomic_load(sb.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+#pragma unroll
+                for (int m = 0; m < NM; ++m) {
+                    if ((live >> m) & 1u) {
+                        const double v = wave_sum(acc[m]);
+                        if (lane == 0) part[par][wave][m] = v;
+                    }
+                }
+                const bool wf = __any(flag);
+                if (lane == 0) s_flag[par][wave] = wf;
+                __syncthreads();
+#pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) uncertain = uncertain || s_flag[par][w] != 0;
+                unsigned keep = live;
+                if (!uncertain) {
+#pragma unroll
+                    for (int m = 0; m < NM; ++m) {
+                        if ((live >> m) & 1u) {
+                            double v = 0.0;
+#pragma unroll
+                            for (int w = 0; w < kBlock / 64; ++w) v += part[par][w][m];
+                            if (v - R[m].tie >= sb.best) keep &= ~(1u << m);
+                        }
+                    }
+                }
+                live = __builtin_amdgcn_readfirstlane(keep);
+                if (s_skip[par]) { // (uniform) a record earlier in the batch: this iteration is discarded
+                    live = 0;
+                    skipped = true;
+                }
+                ++checks;
+                if (live == 0) break;
             }
-            ++checks;
-            if (live == 0) break;
         }
-    }
+    };
+    if (nm == 1)
+        trips(std::integral_constant<int, 1>());
+    else
+        trips(std::integral_constant<int, MAXM>());
     const int par = checks & 1;
 #pragma unroll
     for (int m = 0; m < MAXM; ++m) {
