@@ -586,22 +586,29 @@ def parse_cpulist(text):
     return out
 
 
-def gpu_local_cpus():
+def gpu_local_cpus(base="/sys/class/kfd/kfd/topology/nodes", pci="/sys/bus/pci/devices"):
     """The CPUs local to each HIP device, in HIP's order (the GPU nodes of the KFD
     topology, ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES applied), from sysfs only (no
     GPU call); None when the topology cannot be read."""
-    base = "/sys/class/kfd/kfd/topology/nodes"
     try:
         out = []
         for k in sorted(int(d) for d in os.listdir(base) if d.isdigit()):
-            with open(f"{base}/{k}/properties") as f:
-                props = dict(l.split()[:2] for l in f if len(l.split()) >= 2)
+            try:
+                with open(f"{base}/{k}/properties") as f:
+                    props = dict(l.split()[:2] for l in f if len(l.split()) >= 2)
+            except OSError:
+                # a node this process may not open is a GPU it cannot use either: the
+                # pool's boxes expose only their own GPU's node (profiles/r05/topo.log)
+                continue
             if int(props.get("simd_count", "0")) <= 0:
                 continue
             loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
             bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
-            with open(f"/sys/bus/pci/devices/{bdf}/local_cpulist") as f:
-                out.append(parse_cpulist(f.read()))
+            try:
+                with open(f"{pci}/{bdf}/local_cpulist") as f:
+                    out.append(parse_cpulist(f.read()))
+            except OSError:
+                out.append([])  # locality unknown: every allowed CPU is a candidate
         for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
             vis = os.environ.get(var)
             if vis:

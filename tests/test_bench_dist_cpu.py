@@ -251,3 +251,28 @@ def test_cpu_partition_one_l3_domain_per_rank():
         assert p and not set(p) & seen
         seen |= set(p)
 
+
+def test_gpu_local_cpus_skips_nodes_it_may_not_open(tmp_path, monkeypatch):
+    """The pool's boxes let a process open only its own GPU's KFD node (the others raise
+    EPERM, profiles/r05/topo.log): those are skipped, not a reason to give up on
+    locality; a CPU node (simd_count 0) is skipped; a GPU whose PCI locality is missing
+    gets an empty list (every allowed CPU)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    kfd, pci = tmp_path / "nodes", tmp_path / "pci"
+    for k, props in {0: "cpu_cores_count 128\nsimd_count 0\n", 1: None,
+                     2: "simd_count 1024\nlocation_id 56320\ndomain 0\n",
+                     3: "simd_count 1024\nlocation_id 4096\ndomain 0\n"}.items():
+        (kfd / str(k)).mkdir(parents=True)
+        if props is None:
+            (kfd / str(k) / "properties").mkdir()  # opening a directory raises an OSError
+        else:
+            (kfd / str(k) / "properties").write_text(props)
+    (pci / "0000:dc:00.0").mkdir(parents=True)
+    (pci / "0000:dc:00.0" / "local_cpulist").write_text("64-66,192\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert bench.gpu_local_cpus(str(kfd), str(pci)) == [[64, 65, 66, 192], []]
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert bench.gpu_local_cpus(str(kfd), str(pci)) == [[]]
