@@ -519,6 +519,7 @@ struct ScoreBound {
     double best;         // +inf: no early exit
     int first, every;    // first check after `first` trips, then every `every` trips
     int *work;           // per iteration: (model, trip) pairs evaluated (profiling)
+    int pair;            // two trips per loop step between checks (MADPOSE_SCORE_PAIR=0: one)
     unsigned long long *rec; // nullptr: no record skip
     unsigned epoch_hi;       // ~epoch of this batch
     // record models (nullable): an iteration whose lo is below best (it could hold a new
@@ -593,15 +594,24 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
     // the trip loop over the first NM model slots: a separate instance for iterations with
     // one model (most of them), whose model constants then stay in scalar registers
     // across the trips instead of being reloaded with every trip
+    // a check follows `done` trips
+    auto check_after = [&](int done) { return done < ntrip && done >= sb.first && (done - sb.first) % sb.every == 0; };
     auto trips = [&](auto nmc) {
         constexpr int NM = decltype(nmc)::value;
-        for (int trip = 0; EXIT && trip < ntrip; ++trip) {
-            const int i = trip * kBlock + threadIdx.x;
-            if (i < C.n) {
-                Corr p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
+        for (int trip = 0; EXIT && trip < ntrip;) {
+            // two trips at once where no check falls between them (sb.pair): both
+            // correspondences' loads are in flight together, and each model's constants
+            // serve two evaluations
+            const int step = (sb.pair && trip + 1 < ntrip && !check_after(trip + 1)) ? 2 : 1;
+            const int i = trip * kBlock + threadIdx.x, i2 = i + kBlock;
+            const bool has = i < C.n, has2 = step == 2 && i2 < C.n;
+            Corr p, p2;
+            if (has) p = (FAST && V == kCal) ? load_corr_ray(D, i) : load_corr(C, D, i, V == kCal);
+            if (has2) p2 = (FAST && V == kCal) ? load_corr_ray(D, i2) : load_corr(C, D, i2, V == kCal);
 #pragma unroll
-                for (int m = 0; m < NM; ++m) {
-                    if ((live >> m) & 1u) {
+            for (int m = 0; m < NM; ++m) {
+                if ((live >> m) & 1u) {
+                    if (has) {
                         double e0, e1, e2;
                         if (FAST && V == kCal)
                             eval_corr_cal_ray(C, R[m], p, e0, e1, e2, flag);
@@ -609,11 +619,20 @@ __global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairCon
                             eval_corr<V>(C, R[m], p, !FAST, e0, e1, e2, flag);
                         acc[m] += msac_min(e0, t0, w0) + msac_min(e1, t1, w1) + msac_min(e2, t2, w2);
                     }
+                    if (has2) {
+                        double e0, e1, e2;
+                        if (FAST && V == kCal)
+                            eval_corr_cal_ray(C, R[m], p2, e0, e1, e2, flag);
+                        else
+                            eval_corr<V>(C, R[m], p2, !FAST, e0, e1, e2, flag);
+                        acc[m] += msac_min(e0, t0, w0) + msac_min(e1, t1, w1) + msac_min(e2, t2, w2);
+                    }
                 }
             }
-            work += __popc(live);
-            const int done = trip + 1;
-            if (done < ntrip && done >= sb.first && (done - sb.first) % sb.every == 0) {
+            work += __popc(live) * step;
+            trip += step;
+            const int done = trip;
+            if (check_after(done)) {
                 const int par = checks & 1; // double-buffered: one barrier per check
                 if (threadIdx.x == 0) {
                     s_skip[par] = (unsigned)(recw >> 32) == sb.epoch_hi && (int)(unsigned)(recw & 0xffffffffu) < b;
@@ -1174,6 +1193,11 @@ static ScoreBound score_bound(const PairConst &C, double best, int *work, unsign
     sb.first = sched[0] > 0 ? sched[0] : q;
     sb.every = sched[0] > 0 ? sched[1] : q;
     sb.work = work;
+    static const int pair = [] {
+        const char *e = std::getenv("MADPOSE_SCORE_PAIR");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    sb.pair = pair;
     static const bool skip = [] {
         const char *e = std::getenv("MADPOSE_RECORD_SKIP");
         return !(e && e[0] == '0');
