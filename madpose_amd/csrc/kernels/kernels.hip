@@ -537,11 +537,15 @@ struct ScoreBound {
 
 // EXIT = false (no finite bound yet, or MADPOSE_SCORE_EXIT=0): the plain sweep,
 // without the trip-boundary checks and their barriers.
+//
+// Five waves per SIMD asked of the compiler (FAST instances): the calibrated one
+// otherwise takes 99 VGPRs (four waves); at 96 it keeps five without spilling, 50.9 ->
+// 47.9 us per launch (sf and tf already fit five / seven; profiles/r05/occ).  The
+// general path would spill under the same request and is left alone.
 template <int V, int MAXM, bool FAST, bool EXIT>
-__global__ void __launch_bounds__(kBlock) score_batch_kernel(PairData D, PairConst C,
-                                                             const ScoreRec *__restrict__ recs,
-                                                             const int *__restrict__ counts, double *scores,
-                                                             IterResult *res, ScoreBound sb) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FAST ? 5 : 1)))
+score_batch_kernel(PairData D, PairConst C, const ScoreRec *__restrict__ recs, const int *__restrict__ counts,
+                   double *scores, IterResult *res, ScoreBound sb) {
     if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     const int b = blockIdx.x;
     const int nm = counts[b];
