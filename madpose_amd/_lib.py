@@ -8,7 +8,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmadpose_mi355x.so")
+# (MADPOSE_LIB_VARIANT=name loads lib/libmadpose_mi355x_<name>.so instead: same-box A/B
+# of two builds)
+_VARIANT = os.environ.get("MADPOSE_LIB_VARIANT", "")
+LIB_PATH = os.path.join(_HERE, "lib", "libmadpose_mi355x" + (f"_{_VARIANT}" if _VARIANT.isidentifier() else "") + ".so")
 
 MP_OK, MP_EINVAL, MP_EDEVICE = 0, 1, 2
 CALIBRATED, SHARED_FOCAL, TWO_FOCAL, SCALE_ONLY = 0, 1, 2, 3

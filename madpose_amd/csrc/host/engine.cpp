@@ -895,6 +895,10 @@ class Run {
     double lo_t_[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     double lo_seg_[3] = {0, 0, 0}; // steps phase: before, during and after the parallel run
     bool lo_parallel_ = true;
+    const bool early_hook_ = [] {
+        const char *e = std::getenv("MADPOSE_LO_EARLY_HOOK");
+        return !(e && e[0] == '0');
+    }();
 
     // LO sweeps run on the issuing thread's core (host/lo_sweep.h): the reference's
     // residual operations and ScoreModel order, bit-identical to the oracle; a lane
@@ -1226,6 +1230,24 @@ class Run {
             upd[t] = (o_.threshold_multiplier - 1.0) * thr_[t] / (int)(o_.num_lsq_iterations - 1);
             thr[t] = thr_[t] * o_.threshold_multiplier;
         }
+        // Early hook (MADPOSE_LO_EARLY_HOOK=0 turns it off): the stream's end is predicted
+        // before the serial prefix, so the speculative batch is on the GPU while the prefix
+        // runs.  The prefix's shuffle draws k_nonmin values when the base inlier set is
+        // larger -- k_nonmin = max(non_min_sample_size, min(min_sample_size x multiplier,
+        // |base| / 2)) is that constant whenever |base| / 2 reaches the product (always for
+        // the default options: 35 >= 15) -- and every step draws per_step unless it is
+        // skipped.  Any other outcome ends the LO elsewhere and the speculation is
+        // discarded (the caller compares the draw counts), as for the late prediction.
+        bool hooked = false;
+        const int R_steps = o_.num_lo_steps;
+        if (predicted && early_hook_ && lo_parallel_ && R_steps > 1) {
+            const uint64_t per_step = (uint64_t)(1 + o_.num_lsq_iterations) * (uint64_t)lsq_fit_draws(st);
+            const int k_pred = std::max(non_min_sample_size_, min_sample_size_ * o_.non_min_sample_multiplier);
+            Mt19937 e = rs_.sel;
+            e.discard((uint64_t)k_pred + (uint64_t)R_steps * per_step);
+            predicted(e);
+            hooked = true;
+        }
         Model m_init = *best_min;
         lsq_fit(L0, thr, st, &m_init, true);
         double sc;
@@ -1266,8 +1288,8 @@ class Run {
                 // the hook takes a short step after it (the hook may wait for the
                 // sampler thread to finish launching a continuation it cancels)
                 Mt19937 end = base_sel;
-                const bool hook_job = predicted && X_.lo_workers->lanes() > 1;
-                if (predicted) {
+                const bool hook_job = predicted && !hooked && X_.lo_workers->lanes() > 1;
+                if (predicted && !hooked) {
                     end.discard(pos - base_sel.draws());
                     if (!hook_job) predicted(end);
                 }
