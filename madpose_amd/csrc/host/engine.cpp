@@ -98,9 +98,23 @@ class Sampler {
     // starts drawing B iterations from `from` into *g (the caller must not touch *g
     // or the slot memory until finish()/cancel() returned); `after` runs on the worker
     // once the batch is drawn (the post-LO speculation launches it on the GPU there)
+    // chain (nullable): a second batch for the same job -- once *g is drawn (and `after`
+    // ran), chain->B more iterations are drawn from where it ended into chain->g (the
+    // post-LO speculation's successor, drawn while the LO runs)
+    struct Chain {
+        Batch *g;
+        uint32_t B;
+        int slot;
+        int *smp;
+    };
     void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp,
-               std::function<void()> after = nullptr) {
+               std::function<void()> after = nullptr, const Chain *chain = nullptr) {
         std::lock_guard<std::mutex> lk(mu_);
+        g2_ = chain ? chain->g : nullptr;
+        B2_ = chain ? chain->B : 0;
+        slot2_ = chain ? chain->slot : 0;
+        smp2_ = chain ? chain->smp : nullptr;
+        ok2_ = false;
         after_ = std::move(after);
         err_ = nullptr;
         rs_ = from;
@@ -113,6 +127,12 @@ class Sampler {
         ok_ = false;
         ++gen_;
         cv_.notify_all();
+    }
+    // after finish(): whether the chained batch was drawn; *rs the stream state after it
+    bool chained(IterationStream *rs) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (ok2_) *rs = rs2_;
+        return ok2_;
     }
     // waits for the batch; on success *rs is the stream state after it
     bool finish(IterationStream *rs) {
@@ -146,7 +166,16 @@ class Sampler {
                     err = std::current_exception();
                 }
             }
+            Batch *const g2 = g2_; // (set with the job, under the lock)
+            bool ok2 = false;
+            IterationStream r2;
+            if (ok && !err && g2) {
+                r2 = rs_;
+                ok2 = draw_batch(r2, *g2, B2_, slot2_, smp2_, &abort_, sampler_mode());
+            }
             lk.lock();
+            rs2_ = r2;
+            ok2_ = ok2;
             err_ = err;
             ok_ = ok;
             busy_ = false;
@@ -161,6 +190,12 @@ class Sampler {
     int slot_ = 0;
     int *smp_ = nullptr;
     std::function<void()> after_;
+    Batch *g2_ = nullptr;
+    uint32_t B2_ = 0;
+    int slot2_ = 0;
+    int *smp2_ = nullptr;
+    IterationStream rs2_;
+    bool ok2_ = false;
     std::exception_ptr err_;
     std::atomic<bool> abort_{false};
     bool busy_ = false, ok_ = false, quit_ = false;
@@ -1661,6 +1696,28 @@ void Run::run(Model *best, Stats *S) {
         const char *e = std::getenv("MADPOSE_LO_SPECULATE");
         return !(e && e[0] == '0');
     }();
+    // Chained speculation (MADPOSE_LO_CHAIN=0 disables): the sampler job of the post-LO
+    // batch (at `at`, Bs iterations, in `slot`) also draws the batch after it into the
+    // other slot, whose batch -- the one that led to the LO -- is spent; if the
+    // speculative batch comes next and leads to no LO, that one is next and is already
+    // drawn when the host has read the speculative batch.
+    const bool chain_on = [] {
+        const char *e = std::getenv("MADPOSE_LO_CHAIN");
+        return !(e && e[0] == '0');
+    }();
+    bool chain_ready = false; // gen[cur ^ 1] holds the drawn batch from chain_at on
+    uint32_t chain_at = 0;
+    IterationStream chain_rs; // the streams after it
+    auto make_chain = [&](uint32_t at, uint32_t Bs, int slot, Sampler::Chain *ch, uint32_t *ch_at) {
+        const uint32_t at2 = at + Bs;
+        if (!chain_on || early_mode_ != 0 || at2 >= max_total || at2 == lo_start) return false;
+        const uint32_t B2 = batch_size(at2, grow(at2));
+        if (B2 == 0) return false;
+        slot_free(slot ^ 1);
+        *ch = Sampler::Chain{&gen[slot ^ 1], B2, slot ^ 1, slot_ptr(slot ^ 1)};
+        *ch_at = at2;
+        return true;
+    };
     while (it < max_total && !done) {
         if (it == lo_start && best_min_score < kMax) {
             ++S->number_lo_iterations;
@@ -1675,17 +1732,23 @@ void Run::run(Model *best, Stats *S) {
             const double bound = best_min_score;
             Batch *const gs = &gen[slot];
             const uint32_t at = it;
+            bool spec0_chain = false;
+            uint32_t spec0_chain_at = 0;
             auto predicted = [this, rs_at_lo, slot, bound, gs, at, max_total, speculate, lo_start, &grow, &batch_size,
-                              &spec0, &spec0_draws](const Mt19937 &sel_end) {
+                              &spec0, &spec0_draws, &make_chain, &spec0_chain, &spec0_chain_at](const Mt19937 &sel_end) {
                 if (!speculate || at >= max_total) return;
                 IterationStream from = rs_at_lo;
                 from.sel = sel_end;
                 slot_free(slot);
-                X_.sampler->start(from, gs, batch_size(at, sync_batch(grow(at))), slot, slot_ptr(slot),
+                const uint32_t Bs = batch_size(at, sync_batch(grow(at)));
+                Sampler::Chain ch;
+                spec0_chain = make_chain(at, Bs, slot, &ch, &spec0_chain_at);
+                X_.sampler->start(from, gs, Bs, slot, slot_ptr(slot),
                                   [this, gs, bound, at, lo_start] {
                                       MP_HIP(hipSetDevice(X_.device));
                                       launch_batch(*gs, bound, at >= lo_start);
-                                  });
+                                  },
+                                  spec0_chain ? &ch : nullptr);
                 spec0 = true;
                 spec0_draws = sel_end.draws();
             };
@@ -1700,6 +1763,8 @@ void Run::run(Model *best, Stats *S) {
                     if (have_next) {
                         cur ^= 1;
                         launched = true;
+                        chain_ready = spec0_chain && X_.sampler->chained(&chain_rs);
+                        chain_at = spec0_chain_at;
                     }
                 } else {
                     X_.sampler->cancel();
@@ -1744,11 +1809,15 @@ void Run::run(Model *best, Stats *S) {
         // batch's pre-batch best, which is its own unless this batch holds a new best,
         // and then (before lo_start) the bound is conservative and no record skip runs.
         const uint32_t it_next = it + B;
-        const uint32_t Bn = (it_next < max_total && it_next != lo_start)
-                                ? batch_size(it_next, grow(it_next))
-                                : 0;
-        const bool early = Bn > 0 && early_now(Bn);
-        if (Bn > 0) {
+        const uint32_t Bn0 = (it_next < max_total && it_next != lo_start)
+                                 ? batch_size(it_next, grow(it_next))
+                                 : 0;
+        // the chained batch, when it starts where the next one does
+        const bool use_chain = chain_ready && Bn0 > 0 && it_next == chain_at;
+        chain_ready = false;
+        const uint32_t Bn = use_chain ? gen[cur ^ 1].B : Bn0;
+        const bool early = !use_chain && Bn > 0 && early_now(Bn);
+        if (Bn > 0 && !use_chain) {
             slot_free(cur ^ 1);
             if (early) {
                 Batch *gn = &gen[cur ^ 1];
@@ -1806,6 +1875,8 @@ void Run::run(Model *best, Stats *S) {
         bool invalidated = false;
         bool spec = false; // the sampler holds the post-LO speculation, not the Bn batch
         uint64_t spec_draws = 0;
+        bool spec_chain = false; // ... and the batch after it (make_chain)
+        uint32_t spec_chain_at = 0;
         uint32_t j = 0;
         const bool dumping = model_dump_ || count_dump_;
         for (; j < B; ++j) {
@@ -1911,21 +1982,25 @@ void Run::run(Model *best, Stats *S) {
                             const double bound = best_min_score;
                             Batch *const gs = &gen[slot];
                             auto predicted = [this, rs_at_lo, slot, cont_pending, bound, gs, at, max_total, speculate,
-                                              lo_start, &grow, &batch_size, &spec,
-                                              &spec_draws](const Mt19937 &sel_end) {
+                                              lo_start, &grow, &batch_size, &spec, &spec_draws, &make_chain,
+                                              &spec_chain, &spec_chain_at](const Mt19937 &sel_end) {
                                 if (!speculate || at >= max_total) return;
                                 if (cont_pending) X_.sampler->cancel(); // the no-LO continuation
                                 IterationStream from = rs_at_lo;
                                 from.sel = sel_end;
                                 const uint32_t bc = grow(at);
                                 slot_free(slot); // (an early continuation's samples are on the device)
-                                X_.sampler->start(from, gs, batch_size(at, sync_batch(bc)), slot, slot_ptr(slot),
+                                const uint32_t Bs = batch_size(at, sync_batch(bc));
+                                Sampler::Chain ch;
+                                spec_chain = make_chain(at, Bs, slot, &ch, &spec_chain_at);
+                                X_.sampler->start(from, gs, Bs, slot, slot_ptr(slot),
                                                   [this, gs, bound, at, lo_start] {
                                                       // the sampler thread is not bound to the
                                                       // estimator's device by itself
                                                       MP_HIP(hipSetDevice(X_.device));
                                                       launch_batch(*gs, bound, at >= lo_start);
-                                                  });
+                                                  },
+                                                  spec_chain ? &ch : nullptr);
                                 spec = true;
                                 spec_draws = sel_end.draws();
                             };
@@ -1956,7 +2031,13 @@ void Run::run(Model *best, Stats *S) {
         if (!done && !invalidated) {
             it += B;
             have_next = false;
-            if (Bn > 0) { // rs_ moves to the end of the drawn batch
+            if (Bn > 0 && use_chain) { // drawn during the LO (chained speculation)
+                tl_.mark("chained", (long)Bn);
+                rs_ = chain_rs;
+                have_next = true;
+                cur ^= 1;
+                launched = false;
+            } else if (Bn > 0) { // rs_ moves to the end of the drawn batch
                 auto t0 = Clock::now();
                 tl_.mark("join_sampler");
                 have_next = X_.sampler->finish(&rs_);
@@ -1978,6 +2059,8 @@ void Run::run(Model *best, Stats *S) {
                 if (have_next) {
                     cur ^= 1;
                     launched = true;
+                    chain_ready = spec_chain && X_.sampler->chained(&chain_rs);
+                    chain_at = spec_chain_at;
                 }
             } else {
                 X_.sampler->cancel();

@@ -10,7 +10,8 @@ draw-by-draw sampler (MADPOSE_SAMPLER_TWO_PASS), and the calibrated MD and 5pt r
 stage on two streams instead of one fused launch (MADPOSE_SOLVE_FUSE), score_batch
 one trip per loop step instead of two between early-exit checks (MADPOSE_SCORE_PAIR), the
 post-LO speculation predicted after the LO prefix instead of before it
-(MADPOSE_LO_EARLY_HOOK) or not at all (MADPOSE_LO_SPECULATE)."""
+(MADPOSE_LO_EARLY_HOOK) or not at all (MADPOSE_LO_SPECULATE), and without the batch after
+it drawn in the same job (MADPOSE_LO_CHAIN)."""
 import json
 import os
 import subprocess
@@ -27,7 +28,7 @@ SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOS
             "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "mdx_two_lanes": {"MADPOSE_MDX_R": "2"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
             "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"},
             "solve_unfused": {"MADPOSE_SOLVE_FUSE": "0"}, "early_big": {"MADPOSE_EARLY_CONT": "3"}, "lo_late_hook": {"MADPOSE_LO_EARLY_HOOK": "0"},
-            "lo_no_speculation": {"MADPOSE_LO_SPECULATE": "0"},
+            "lo_no_speculation": {"MADPOSE_LO_SPECULATE": "0"}, "lo_no_chain": {"MADPOSE_LO_CHAIN": "0"},
             "score_single_trips": {"MADPOSE_SCORE_PAIR": "0"}}
 
 
