@@ -2148,7 +2148,14 @@ void validate(const PairInput &in, const RansacOptions &o) {
 
 } // namespace
 
-void profile_enable(bool on) { g_prof_on.store(on); }
+// (MADPOSE_PROF_OFF=1: profiling stays off whatever the caller asks -- A/B of its cost)
+void profile_enable(bool on) {
+    static const bool off = [] {
+        const char *e = std::getenv("MADPOSE_PROF_OFF");
+        return e && e[0] == '1';
+    }();
+    g_prof_on.store(on && !off);
+}
 void profile_reset() {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof = KernelProfile();
