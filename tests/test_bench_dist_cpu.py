@@ -30,7 +30,7 @@ def _worker(rank, world, port, out_path):
     # rank r: elapsed 1 + r seconds, 1000 * (r + 1) hypotheses, ...
     local = [1.0 + rank, 1000.0 * (rank + 1), 500.0, 2.0, 0.5, 10.0, 5.0, 1000.0 * (rank + 1),
              2000.0 * 1000.0 * (rank + 1), 4.0, 7.0, 3.0, 1.0, 2.0, 400.0, 0.3, 0.4, 900.0, 5000.0, 1.0, 0.5,
-             4000.0 * (rank + 1), 8000.0 * (rank + 1), 700.0 * (rank + 1), 900.0 * (rank + 1)]
+             4000.0 * (rank + 1), 8000.0 * (rank + 1), 700.0 * (rank + 1), 900.0 * (rank + 1), 3.0]
     allv = bench.gather_counters(local, world)
     if rank == 0:
         res = bench.summarize(allv, bench.WORKLOADS["cal"], 3, 1, world)
@@ -61,7 +61,7 @@ def test_single_rank_summary_fields():
     import bench
 
     allv = np.array([[2.0, 3e5, 3e5, 30, 1.0, 100.0, 50.0, 3e5, 3e5 * 2000, 30, 90, 10, 5.0, 6.0, 3e5, 1.0, 2.0, 2000.0,
-                      5e4, 3, 2.0, 1e6, 2.4e6, 2.5e5, 2.75e5]])
+                      5e4, 3, 2.0, 1e6, 2.4e6, 2.5e5, 2.75e5, 1.0]])
     assert allv.shape[1] == len(bench.COUNTERS)
     res = bench.summarize(allv, bench.WORKLOADS["cal"], 3, 1, 1)
     for k in ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -79,6 +79,8 @@ def test_single_rank_summary_fields():
     assert abs(rf["evaluated_bytes_per_launch"] - 3e5 * 2000 * 48 * (1e6 / 2.4e6) / 30) < 1e-3
     assert abs(res["speculation"]["solved_over_accepted"] - 3e5 / 2.5e5) < 1e-12
     assert abs(res["speculation"]["scored_over_accepted"] - 2.75e5 / 2.5e5) < 1e-12
+    # the per-pair breakdown averages the profiled pairs (one of the three here)
+    assert res["profiled_pairs"] == 1 and abs(res["ms_per_pair"]["run"] - 2000.0) < 1e-9
 
 
 def test_scannet_summary_and_gathered_errors():
