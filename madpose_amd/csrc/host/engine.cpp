@@ -930,10 +930,6 @@ class Run {
     double lo_t_[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     double lo_seg_[3] = {0, 0, 0}; // steps phase: before, during and after the parallel run
     bool lo_parallel_ = true;
-    const bool warm_ = [] {
-        const char *e = std::getenv("MADPOSE_WARM");
-        return !(e && e[0] == '0');
-    }();
     const bool early_hook_ = [] {
         const char *e = std::getenv("MADPOSE_LO_EARLY_HOOK");
         return !(e && e[0] == '0');
@@ -1683,7 +1679,6 @@ void Run::run(Model *best, Stats *S) {
         return (uint32_t)std::min<double>((double)max_batch_, std::max<double>((double)min_batch_, growth_ * at));
     };
     Batch gen[2];
-    bool warmed = false;
     // the worker may be drawing into gen[] when an exception unwinds this frame
     struct CancelOnExit {
         Sampler *s;
@@ -1796,15 +1791,6 @@ void Run::run(Model *best, Stats *S) {
             tl_.mark("launched");
             launch_s_ += secs(tl);
             ++launch_n_;
-            // while the first batch is on the GPU: wake the LO lanes and the LM pool, which
-            // have slept since the last pair's LO (they spin for a while after a job), so
-            // the first LO's fits do not pay the wake-ups (MADPOSE_WARM=0: off)
-            if (!warmed && warm_ && active_runs(X_.device) <= 1) {
-                if (lo_parallel_ && X_.lo_workers) X_.lo_workers->run(X_.lo_workers->lanes(), [](int, int) {});
-                lm_pool_warm();
-                tl_.mark("warmed");
-            }
-            warmed = true;
         } else {
             tl_.mark("prelaunched", (long)g.B);
         }

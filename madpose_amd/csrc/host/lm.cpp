@@ -603,10 +603,4 @@ bool lm_refine(const HostPair &P, const std::vector<int> *sample, const LMSettin
     return true;
 }
 
-// (64 empty jobs, wide: every worker wakes, takes part or finds none, and spins after)
-void lm_pool_warm() {
-    static const std::function<void(size_t)> noop = [](size_t) {};
-    lo_pool().run(64, noop, true);
-}
-
 } // namespace mp

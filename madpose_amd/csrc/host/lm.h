@@ -45,10 +45,6 @@ extern thread_local int lm_last_evals;
 // the LM pool's spin before blocking, in microseconds (MADPOSE_LO_SPIN, or the
 // affinity-based default of lm.cpp)
 int lo_spin_us();
-// wakes the LM pool's workers with an empty job, after which they spin (lo_spin_us)
-// instead of sleeping: the estimator calls it while its first batch is on the GPU, so
-// the first LO's all-inlier fit does not pay the workers' wake-ups
-void lm_pool_warm();
 
 // quaternion helpers (w, x, y, z) -- Eigen::Quaternion(Matrix3) / toRotationMatrix
 void rot_to_quat(const double *R, double *q);
