@@ -106,6 +106,7 @@ class Sampler {
         uint32_t B;
         int slot;
         int *smp;
+        std::function<void()> after; // runs once it is drawn (launches it; nullable)
     };
     void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp,
                std::function<void()> after = nullptr, const Chain *chain = nullptr) {
@@ -114,6 +115,7 @@ class Sampler {
         B2_ = chain ? chain->B : 0;
         slot2_ = chain ? chain->slot : 0;
         smp2_ = chain ? chain->smp : nullptr;
+        after2_ = chain ? chain->after : nullptr;
         ok2_ = false;
         after_ = std::move(after);
         err_ = nullptr;
@@ -172,6 +174,14 @@ class Sampler {
             if (ok && !err && g2) {
                 r2 = rs_;
                 ok2 = draw_batch(r2, *g2, B2_, slot2_, smp2_, &abort_, sampler_mode());
+                if (ok2 && after2_) {
+                    try {
+                        after2_();
+                    } catch (...) {
+                        err = std::current_exception();
+                        ok2 = false;
+                    }
+                }
             }
             lk.lock();
             rs2_ = r2;
@@ -191,6 +201,7 @@ class Sampler {
     int *smp_ = nullptr;
     std::function<void()> after_;
     Batch *g2_ = nullptr;
+    std::function<void()> after2_;
     uint32_t B2_ = 0;
     int slot2_ = 0;
     int *smp2_ = nullptr;
@@ -1708,16 +1719,38 @@ void Run::run(Model *best, Stats *S) {
     bool chain_ready = false; // gen[cur ^ 1] holds the drawn batch from chain_at on
     uint32_t chain_at = 0;
     IterationStream chain_rs; // the streams after it
-    auto make_chain = [&](uint32_t at, uint32_t Bs, int slot, Sampler::Chain *ch, uint32_t *ch_at) {
+    // MADPOSE_LO_CHAIN_LAUNCH=1: the job also launches the chained batch, behind the
+    // speculative batch (the GPU otherwise idles for the rest of the LO), bound by the
+    // pre-LO best and gated on the speculative batch's record word (kernels.h
+    // batch_cancelled) like an early continuation; when the host discards it, the next
+    // batch in its slot follows it on the slot's stream.  Off by default: cal 4.28 ->
+    // 4.24 ms, sf 9.72 -> 9.93 ms (its discarded batches overlap the next scoring,
+    // profiles/r05/chain_launch).
+    const bool chain_launch = [] {
+        const char *e = std::getenv("MADPOSE_LO_CHAIN_LAUNCH");
+        return e && e[0] == '1';
+    }();
+    auto make_chain = [&](uint32_t at, uint32_t Bs, int slot, double bound, Sampler::Chain *ch, uint32_t *ch_at) {
         const uint32_t at2 = at + Bs;
         if (!chain_on || early_mode_ != 0 || at2 >= max_total || at2 == lo_start) return false;
         const uint32_t B2 = batch_size(at2, grow(at2));
         if (B2 == 0) return false;
         slot_free(slot ^ 1);
-        *ch = Sampler::Chain{&gen[slot ^ 1], B2, slot ^ 1, slot_ptr(slot ^ 1)};
+        Batch *g2 = &gen[slot ^ 1];
+        std::function<void()> after;
+        if (chain_launch && active_runs(X_.device) <= 1) {
+            const BatchBufs *prev = &X_.bb[slot];
+            const bool cut = at2 >= lo_start;
+            after = [this, g2, bound, cut, prev] {
+                MP_HIP(hipSetDevice(X_.device));
+                launch_batch(*g2, bound, cut, prev);
+            };
+        }
+        *ch = Sampler::Chain{g2, B2, slot ^ 1, slot_ptr(slot ^ 1), std::move(after)};
         *ch_at = at2;
         return true;
     };
+    bool chain_launched = false; // (the chained batch is on the GPU already)
     while (it < max_total && !done) {
         if (it == lo_start && best_min_score < kMax) {
             ++S->number_lo_iterations;
@@ -1732,17 +1765,19 @@ void Run::run(Model *best, Stats *S) {
             const double bound = best_min_score;
             Batch *const gs = &gen[slot];
             const uint32_t at = it;
-            bool spec0_chain = false;
+            bool spec0_chain = false, spec0_chain_launched = false;
             uint32_t spec0_chain_at = 0;
             auto predicted = [this, rs_at_lo, slot, bound, gs, at, max_total, speculate, lo_start, &grow, &batch_size,
-                              &spec0, &spec0_draws, &make_chain, &spec0_chain, &spec0_chain_at](const Mt19937 &sel_end) {
+                              &spec0, &spec0_draws, &make_chain, &spec0_chain, &spec0_chain_at,
+                              &spec0_chain_launched](const Mt19937 &sel_end) {
                 if (!speculate || at >= max_total) return;
                 IterationStream from = rs_at_lo;
                 from.sel = sel_end;
                 slot_free(slot);
                 const uint32_t Bs = batch_size(at, sync_batch(grow(at)));
                 Sampler::Chain ch;
-                spec0_chain = make_chain(at, Bs, slot, &ch, &spec0_chain_at);
+                spec0_chain = make_chain(at, Bs, slot, bound, &ch, &spec0_chain_at);
+                spec0_chain_launched = spec0_chain && ch.after != nullptr;
                 X_.sampler->start(from, gs, Bs, slot, slot_ptr(slot),
                                   [this, gs, bound, at, lo_start] {
                                       MP_HIP(hipSetDevice(X_.device));
@@ -1765,6 +1800,7 @@ void Run::run(Model *best, Stats *S) {
                         launched = true;
                         chain_ready = spec0_chain && X_.sampler->chained(&chain_rs);
                         chain_at = spec0_chain_at;
+                        chain_launched = chain_ready && spec0_chain_launched;
                     }
                 } else {
                     X_.sampler->cancel();
@@ -1875,7 +1911,7 @@ void Run::run(Model *best, Stats *S) {
         bool invalidated = false;
         bool spec = false; // the sampler holds the post-LO speculation, not the Bn batch
         uint64_t spec_draws = 0;
-        bool spec_chain = false; // ... and the batch after it (make_chain)
+        bool spec_chain = false, spec_chain_launched = false; // ... and the batch after it (make_chain)
         uint32_t spec_chain_at = 0;
         uint32_t j = 0;
         const bool dumping = model_dump_ || count_dump_;
@@ -1983,7 +2019,7 @@ void Run::run(Model *best, Stats *S) {
                             Batch *const gs = &gen[slot];
                             auto predicted = [this, rs_at_lo, slot, cont_pending, bound, gs, at, max_total, speculate,
                                               lo_start, &grow, &batch_size, &spec, &spec_draws, &make_chain,
-                                              &spec_chain, &spec_chain_at](const Mt19937 &sel_end) {
+                                              &spec_chain, &spec_chain_at, &spec_chain_launched](const Mt19937 &sel_end) {
                                 if (!speculate || at >= max_total) return;
                                 if (cont_pending) X_.sampler->cancel(); // the no-LO continuation
                                 IterationStream from = rs_at_lo;
@@ -1992,7 +2028,8 @@ void Run::run(Model *best, Stats *S) {
                                 slot_free(slot); // (an early continuation's samples are on the device)
                                 const uint32_t Bs = batch_size(at, sync_batch(bc));
                                 Sampler::Chain ch;
-                                spec_chain = make_chain(at, Bs, slot, &ch, &spec_chain_at);
+                                spec_chain = make_chain(at, Bs, slot, bound, &ch, &spec_chain_at);
+                                spec_chain_launched = spec_chain && ch.after != nullptr;
                                 X_.sampler->start(from, gs, Bs, slot, slot_ptr(slot),
                                                   [this, gs, bound, at, lo_start] {
                                                       // the sampler thread is not bound to the
@@ -2036,7 +2073,7 @@ void Run::run(Model *best, Stats *S) {
                 rs_ = chain_rs;
                 have_next = true;
                 cur ^= 1;
-                launched = false;
+                launched = chain_launched;
             } else if (Bn > 0) { // rs_ moves to the end of the drawn batch
                 auto t0 = Clock::now();
                 tl_.mark("join_sampler");
@@ -2061,6 +2098,7 @@ void Run::run(Model *best, Stats *S) {
                     launched = true;
                     chain_ready = spec_chain && X_.sampler->chained(&chain_rs);
                     chain_at = spec_chain_at;
+                    chain_launched = chain_ready && spec_chain_launched;
                 }
             } else {
                 X_.sampler->cancel();

@@ -11,7 +11,7 @@ stage on two streams instead of one fused launch (MADPOSE_SOLVE_FUSE), score_bat
 one trip per loop step instead of two between early-exit checks (MADPOSE_SCORE_PAIR), the
 post-LO speculation predicted after the LO prefix instead of before it
 (MADPOSE_LO_EARLY_HOOK) or not at all (MADPOSE_LO_SPECULATE), and without the batch after
-it drawn in the same job (MADPOSE_LO_CHAIN)."""
+it drawn (MADPOSE_LO_CHAIN) or launched (MADPOSE_LO_CHAIN_LAUNCH) in the same job."""
 import json
 import os
 import subprocess
@@ -29,6 +29,7 @@ SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOS
             "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"},
             "solve_unfused": {"MADPOSE_SOLVE_FUSE": "0"}, "early_big": {"MADPOSE_EARLY_CONT": "3"}, "lo_late_hook": {"MADPOSE_LO_EARLY_HOOK": "0"},
             "lo_no_speculation": {"MADPOSE_LO_SPECULATE": "0"}, "lo_no_chain": {"MADPOSE_LO_CHAIN": "0"},
+            "lo_chain_launched": {"MADPOSE_LO_CHAIN_LAUNCH": "1"},
             "score_single_trips": {"MADPOSE_SCORE_PAIR": "0"}}
 
 
