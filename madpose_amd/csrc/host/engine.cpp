@@ -849,7 +849,11 @@ class Run {
         // (1024: the solver kernels cost about the same at 128 and at 1024 samples, so a
         // short run -- the ScanNet stand-in's 1000 iterations -- takes fewer round trips:
         // 903 / 982 / 998 pairs/s at 128 / 512 / 1000 on one box, profiles/r03/s6)
-        min_batch_ = env2 ? std::max(1, std::atoi(env2)) : 1024;
+        // calibrated: 4096 since the post-LO speculation runs beside the LO (§2 step 6): a
+        // bigger speculative batch costs no wait and covers more iterations per LO cycle,
+        // 4.31 -> 4.07 ms per pair (2048: 4.19; profiles/r05/min_batch); shared focal
+        // neutral at 2048 (9.94 -> 9.97 ms)
+        min_batch_ = env2 ? std::max(1, std::atoi(env2)) : (variant_ == kCal ? 4096 : 1024);
         min_batch_ = std::min(min_batch_, max_batch_);
         // growth 1 for every variant: round 4 ran the shared focal at 2 (fewer, larger
         // batches for its latency-bound chain: 11.48 -> 10.97-11.20 ms, profiles/r04/gab2)
