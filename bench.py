@@ -792,7 +792,7 @@ def main(argv=None):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)), per_ccd=a.workload != "scannet")
     # hardware queues of the HIP runtime (read once, at its start): every estimator in
-    # flight drives two streams (main + MD side stream), and with HIP's default of 4
+    # flight drives three streams (one per batch slot + the MD side stream), and with HIP's default of 4
     # queues the kernels of different pairs serialize behind each other -- ScanNet
     # stand-in 943-946 pairs/s at 4 queues, 1302-1309 at 8, 1281-1337 at 16, 1232-1271
     # at 24 (8 pairs in flight, profiles/r05/r5r).  The boxes export 4, so it is set, not

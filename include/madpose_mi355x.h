@@ -250,8 +250,10 @@ int mp_debug_pt5_roots(int impl, int64_t ns, const double *pts0, const double *p
  * as called at src/hybrid_pose_shared_focal_estimator.cpp:87, by the deflated
  * eigenproblem the estimator runs; pts0/pts1: ns x 6 x 2 normalized points; cand per
  * sample: the 3x9 epipolar null-space basis N, then the positive roots u = f^2 of the
- * degree-15 focal polynomial, ascending).  Other impl values return MP_EINVAL.  Test
- * hook. */
+ * degree-15 focal polynomial, ascending), or 2 (two-focal 7-point, impl 1: the root stage of
+ * PoseLib relpose_7pt as called at src/hybrid_pose_two_focal_estimator.cpp:116; pts0/pts1: ns x 7
+ * x 2 normalized points; cand per sample: the unit-norm fundamental matrices, 9 doubles each,
+ * in root order).  Other impl values return MP_EINVAL.  Test hook. */
 int mp_debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, const double *pts1, double *cand,
                       int32_t *ncand, int device);
 

@@ -429,9 +429,11 @@ int mp_debug_pt_roots(int variant, int impl, int64_t ns, const double *pts0, con
                       int32_t *ncand, int device) {
     if (!pts0 || !pts1 || !cand || !ncand) return fail(MP_EINVAL, "null pointer");
     // impl names the estimator's root stage: 1 for the 5-point (16-lane groups), 3 for
-    // the 6-point (deflated eigenproblem); the round-2 alternates left the library
-    if ((variant == 0 && impl != 1) || (variant == 1 && impl != 3))
-        return fail(MP_EINVAL, "impl must be 1 (5-point group stage) or 3 (6-point eigen stage)");
+    // the 6-point (deflated eigenproblem), 1 for the 7-point (lane per sample); the
+    // round-2 alternates left the library
+    if ((variant == 0 && impl != 1) || (variant == 1 && impl != 3) || (variant == 2 && impl != 1) || variant < 0 ||
+        variant > 2)
+        return fail(MP_EINVAL, "impl must be 1 (5-point group stage, 7-point) or 3 (6-point eigen stage)");
     return guarded([&] {
         mp::debug_pt_roots(variant, ns, pts0, pts1, cand, ncand, device);
         return MP_OK;

@@ -17,7 +17,10 @@
 //
 // Local optimisation stays on the host (north star); its full-data sweeps
 // (ScoreModel / GetInliers) run on the GPU through the single-model sweep kernel.
+#include <fcntl.h>
 #include <immintrin.h>
+#include <signal.h>
+#include <unistd.h>
 #include "engine.h"
 
 #include <hip/hip_runtime.h>
@@ -42,6 +45,7 @@
 #include "../include/mp_score.h"
 #include "../kernels/kernels.h"
 #include "batch_draw.h"
+#include "env.h"
 #include "lo_sweep.h"
 #include "rng.h"
 
@@ -72,10 +76,8 @@ const double kMax = DBL_MAX;
 // two passes (A/B; identical draws).
 int sampler_mode() {
     static const int mode = [] {
-        const char *e = std::getenv("MADPOSE_SAMPLER_TWO_PASS");
-        if (e && e[0] == '0') return 0;
-        const char *v = std::getenv("MADPOSE_SAMPLER_SIMD");
-        return v && v[0] == '0' ? 1 : 2;
+        if (!env_flag("MADPOSE_SAMPLER_TWO_PASS", true)) return 0;
+        return env_flag("MADPOSE_SAMPLER_SIMD", true) ? 2 : 1;
     }();
     return mode;
 }
@@ -262,8 +264,7 @@ class LoWorkers {
         // microseconds (MADPOSE_LO_WORKER_SPIN; 0: block at once); default 2000 -- the
         // LO runs of a pair come ~0.3-1 ms apart, so a shorter spin sleeps through the
         // gap -- or 0 where the LM pool does not spin either (a small CPU share per rank)
-        const char *e = std::getenv("MADPOSE_LO_WORKER_SPIN");
-        spin_ns_ = e ? std::max(0, std::atoi(e)) * 1000ll : (lo_spin_us() > 0 ? 2000 * 1000ll : 0);
+        spin_ns_ = 1000ll * env_int("MADPOSE_LO_WORKER_SPIN", lo_spin_us() > 0 ? 2000 : 0, 0, 1000000);
         for (int i = 1; i < lanes; ++i) th_.emplace_back([this, i] { loop(i); });
     }
     ~LoWorkers() {
@@ -360,9 +361,7 @@ constexpr int kLoLanes = 12; // most concurrent LO steps (and sweep slots) per c
 // is 4 lanes; see DESIGN.md §8 for the measurements behind it
 inline int lo_lanes_setting() {
     static const int v = [] {
-        const char *e = std::getenv("MADPOSE_LO_LANES");
-        const int n = e ? std::atoi(e) : 4;
-        return std::max(1, std::min(kLoLanes, n));
+        return (int)env_int("MADPOSE_LO_LANES", 4, 1, kLoLanes);
     }();
     return v;
 }
@@ -526,6 +525,68 @@ struct DeviceCtx {
 std::mutex g_pool_mu;
 std::vector<DeviceCtx *> g_pool;
 
+// Process teardown: the pooled (idle) contexts' host threads -- each context's sampler
+// and LO workers -- are stopped and joined before the HIP runtime's own teardown (this
+// library's static destructors run first: it is loaded after libamdhip64).  A context
+// leased by an estimator still running at exit is not in the pool and is left alone.
+// The device buffers are not freed: the process is ending.
+struct PoolReaper {
+    ~PoolReaper() {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (DeviceCtx *c : g_pool) {
+            c->sampler.reset();
+            c->lo_workers.reset();
+        }
+    }
+} g_pool_reaper;
+
+// MADPOSE_SEGV_MAPS (diagnostic, presence): on SIGSEGV / SIGBUS write the fault address
+// and /proc/self/maps to stderr, then hand the signal to the handler installed before
+// (a profiler's stack printer, or the default action).  Async-signal-safe: open / read /
+// write only.
+struct sigaction g_old_segv, g_old_bus;
+void segv_maps_handler(int sig, siginfo_t *si, void *uc) {
+    char buf[4096];
+    static const char hex[] = "0123456789abcdef";
+    int k = 0;
+    const char *hdr = "[madpose] fault address 0x";
+    while (*hdr) buf[k++] = *hdr++;
+    const unsigned long long a = (unsigned long long)(uintptr_t)(si ? si->si_addr : nullptr);
+    for (int sh = 60; sh >= 0; sh -= 4) buf[k++] = hex[(a >> sh) & 15];
+    const char *tail = ", /proc/self/maps:\n";
+    while (*tail) buf[k++] = *tail++;
+    ssize_t w = write(2, buf, (size_t)k);
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        ssize_t r;
+        while ((r = read(fd, buf, sizeof(buf))) > 0) w = write(2, buf, (size_t)r);
+        close(fd);
+    }
+    (void)w;
+    const struct sigaction &old = sig == SIGBUS ? g_old_bus : g_old_segv;
+    if (old.sa_flags & SA_SIGINFO) {
+        old.sa_sigaction(sig, si, uc);
+    } else if (old.sa_handler != SIG_IGN && old.sa_handler != SIG_DFL) {
+        old.sa_handler(sig);
+    } else {
+        signal(sig, SIG_DFL);
+        raise(sig);
+    }
+}
+void install_segv_maps() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        if (!std::getenv("MADPOSE_SEGV_MAPS")) return;
+        struct sigaction sa;
+        std::memset(&sa, 0, sizeof(sa));
+        sa.sa_sigaction = segv_maps_handler;
+        sa.sa_flags = SA_SIGINFO;
+        sigemptyset(&sa.sa_mask);
+        sigaction(SIGSEGV, &sa, &g_old_segv);
+        sigaction(SIGBUS, &sa, &g_old_bus);
+    });
+}
+
 std::atomic<bool> g_prof_on{false};
 std::mutex g_prof_mu;
 KernelProfile g_prof;
@@ -541,6 +602,7 @@ int active_runs(int device) {
 struct CtxLease {
     DeviceCtx *c = nullptr;
     explicit CtxLease(int device) {
+        install_segv_maps();
         {
             std::lock_guard<std::mutex> lk(g_pool_mu);
             for (size_t i = 0; i < g_pool.size(); ++i)
@@ -763,8 +825,7 @@ Problem make_problem(const PairInput &in, const RansacOptions &o, const Estimato
     }
     pair_magnitudes(C, H);
     {
-        const char *ts = std::getenv("MADPOSE_TIE_SCALE");
-        C.tie_scale = ts ? std::max(1.0, std::atof(ts)) : 1.0;
+        C.tie_scale = env_real("MADPOSE_TIE_SCALE", 1.0, 1.0, 1e300);
         // a non-finite coordinate or depth: no screening at all (every margin infinite;
         // the score kernel's residuals could be NaN where no gate flags them)
         bool finite = true;
@@ -792,17 +853,22 @@ void upload_pair(DeviceCtx &X, const Problem &P, PairData *D) {
     const int64_t n = P.C.n;
     double *base = X.d_pair;
     const int64_t cn = X.cap_n;
-    // (one upload: the six arrays at their device stride cap_n)
-    std::vector<double> soa(5 * (size_t)cn + (size_t)n, 0.0);
+    // one upload: the six arrays packed at stride n on the host, placed at their device
+    // stride cap_n by one 2-D copy (the pooled context's cap_n is the high-water mark of
+    // the pairs it has seen: a small pair after a large one moves 6 n doubles, not 6 cap_n)
+    if (n > cn) throw std::logic_error("upload_pair: pair larger than the device buffers");
+    std::vector<double> soa(6 * (size_t)n);
     for (int64_t i = 0; i < n; ++i) {
         soa[i] = P.H.x0[2 * i];
-        soa[cn + i] = P.H.x0[2 * i + 1];
-        soa[2 * cn + i] = P.H.x1[2 * i];
-        soa[3 * cn + i] = P.H.x1[2 * i + 1];
-        soa[4 * cn + i] = P.H.d0[i];
-        soa[5 * cn + i] = P.H.d1[i];
+        soa[n + i] = P.H.x0[2 * i + 1];
+        soa[2 * n + i] = P.H.x1[2 * i];
+        soa[3 * n + i] = P.H.x1[2 * i + 1];
+        soa[4 * n + i] = P.H.d0[i];
+        soa[5 * n + i] = P.H.d1[i];
     }
-    MP_HIP(hipMemcpyAsync(base, soa.data(), sizeof(double) * soa.size(), hipMemcpyHostToDevice, X.stream));
+    if (n > 0)
+        MP_HIP(hipMemcpy2DAsync(base, sizeof(double) * (size_t)cn, soa.data(), sizeof(double) * (size_t)n,
+                                sizeof(double) * (size_t)n, 6, hipMemcpyHostToDevice, X.stream));
     D->x0u = base;
     D->x0v = base + cn;
     D->x1u = base + 2 * cn;
@@ -843,9 +909,7 @@ class Run {
         w_[0] = P.C.w[0];
         w_[1] = P.C.w[1];
         w_[2] = P.C.w[2];
-        const char *env = std::getenv("MADPOSE_MAX_BATCH");
-        max_batch_ = env ? std::max(1, std::atoi(env)) : 32768;
-        const char *env2 = std::getenv("MADPOSE_MIN_BATCH");
+        max_batch_ = (int)env_int("MADPOSE_MAX_BATCH", 32768, 1, 1 << 22);
         // (1024: the solver kernels cost about the same at 128 and at 1024 samples, so a
         // short run -- the ScanNet stand-in's 1000 iterations -- takes fewer round trips:
         // 903 / 982 / 998 pairs/s at 128 / 512 / 1000 on one box, profiles/r03/s6)
@@ -853,7 +917,7 @@ class Run {
         // bigger speculative batch costs no wait and covers more iterations per LO cycle,
         // 4.31 -> 4.07 ms per pair (2048: 4.19; profiles/r05/min_batch); shared focal
         // neutral at 2048 (9.94 -> 9.97 ms)
-        min_batch_ = env2 ? std::max(1, std::atoi(env2)) : (variant_ == kCal ? 4096 : 1024);
+        min_batch_ = (int)env_int("MADPOSE_MIN_BATCH", variant_ == kCal ? 4096 : 1024, 1, 1 << 22);
         min_batch_ = std::min(min_batch_, max_batch_);
         // growth 1 for every variant: round 4 ran the shared focal at 2 (fewer, larger
         // batches for its latency-bound chain: 11.48 -> 10.97-11.20 ms, profiles/r04/gab2)
@@ -861,8 +925,7 @@ class Run {
         // 10.62 (1.33) against 10.39 ms (1.42), 1.5: 10.50 (1.38), 3 x 60 pairs on one
         // box (profiles/r05/r5sg).  For cal, 0.5 and the waste it saves cost more round
         // trips than they save work (r04 gab)
-        const char *env3 = std::getenv("MADPOSE_BATCH_GROWTH");
-        growth_ = env3 ? std::max(0.01, std::atof(env3)) : 1.0;
+        growth_ = env_real("MADPOSE_BATCH_GROWTH", 1.0, 0.01, 1e6);
         trace_ = std::getenv("MADPOSE_TRACE") != nullptr;
     }
 
@@ -946,8 +1009,7 @@ class Run {
     double lo_seg_[3] = {0, 0, 0}; // steps phase: before, during and after the parallel run
     bool lo_parallel_ = true;
     const bool early_hook_ = [] {
-        const char *e = std::getenv("MADPOSE_LO_EARLY_HOOK");
-        return !(e && e[0] == '0');
+        return env_flag("MADPOSE_LO_EARLY_HOOK", true);
     }();
 
     // LO sweeps run on the issuing thread's core (host/lo_sweep.h): the reference's
@@ -1418,9 +1480,19 @@ class Run {
         return std::min<uint32_t>(want, (uint32_t)std::max<double>(min_batch_, std::min<double>(b, 1e9)));
     }
     int *slot_ptr(int slot) const { return X_.h_samples + (size_t)slot * 9 * max_batch_; }
+    // slot_ptr for a draw or an upload of B iterations, bounds-checked on the host: slot s
+    // spans [9 s max_batch_, 9 (s + 1) max_batch_) of the 2 x 9 cap_b ints of h_samples
+    // (every draw into and upload from a slot is range-checked)
+    int *slot_for(int slot, uint32_t B) const {
+        if (slot < 0 || slot > 1 || B > (uint32_t)max_batch_ || max_batch_ > X_.cap_b || !X_.h_samples)
+            throw std::logic_error("sample slot out of range: slot " + std::to_string(slot) + ", B " +
+                                   std::to_string(B) + ", max_batch " + std::to_string(max_batch_) + ", cap_b " +
+                                   std::to_string(X_.cap_b));
+        return slot_ptr(slot);
+    }
     void generate(Batch &g, uint32_t B, int slot) {
         auto t0 = Clock::now();
-        draw_batch(rs_, g, B, slot, slot_ptr(slot), nullptr, sampler_mode());
+        draw_batch(rs_, g, B, slot, slot_for(slot, B), nullptr, sampler_mode());
         sample_s_ += secs(t0);
     }
     // both streams to the end of iteration j of batch g
@@ -1448,11 +1520,16 @@ class Run {
     // 5.99 vs 5.80-5.86 ms, profiles/r04/hook2/)
     // =3: continuations of at least kEarlyMinBatch iterations while alone on the device
     // (the growth phase, where new bests are rare): each slot has its own stream, so the
-    // continuation's solvers run while this batch is scored.  (On one stream, round 5's
+    // continuation's solvers run while this batch is scored.  Its gating is best-effort
+    // (ADVICE r05): the continuation waits only for the previous batch's solve, so both
+    // score kernels can run at once against the one record word, and the newer epoch's
+    // atomicMin can replace the older batch's record -- the older batch's workgroups then
+    // stop skipping and the continuation is no longer cancelled by it.  Results do not
+    // change (the host walks and discards as always); a discarded continuation merely
+    // costs its full GPU time.  (On one stream, round 5's
     // first form, it measured slower: cal 5.62 -> 5.86 ms per pair, profiles/r05/r5o.)
     const int early_mode_ = [] {
-        const char *e = std::getenv("MADPOSE_EARLY_CONT");
-        return e ? (e[0] == '3' ? 3 : (e[0] == '2' ? 2 : (e[0] == '1' ? 1 : 0))) : 0;
+        return (int)env_int("MADPOSE_EARLY_CONT", 0, 0, 3);
     }();
     static constexpr uint32_t kEarlyMinBatch = 4096;
     bool early_now(uint32_t Bn) const {
@@ -1470,8 +1547,7 @@ class Run {
     // the 5pt root stage its third wave -- cal 5.62 (always fused) -> 5.46 ms per pair
     // (up to 8192), 3 x 200 pairs on one box, profiles/r05/r5o
     const int64_t fuse_max_ = [] {
-        const char *e = std::getenv("MADPOSE_SOLVE_FUSE_MAX");
-        return e ? std::atoll(e) : (int64_t)8192;
+        return (int64_t)env_int("MADPOSE_SOLVE_FUSE_MAX", 8192, 0, 1ll << 40);
     }();
 
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new
@@ -1493,7 +1569,7 @@ class Run {
             D.gate_hi = gate_prev->epoch_hi;
         }
         // one upload: samples, then the MD list and the (descending) point list
-        MP_HIP(hipMemcpyAsync(Q.d_samples, slot_ptr(g.slot), sizeof(int) * 9 * (size_t)B, hipMemcpyHostToDevice, s));
+        MP_HIP(hipMemcpyAsync(Q.d_samples, slot_for(g.slot, B), sizeof(int) * 9 * (size_t)B, hipMemcpyHostToDevice, s));
         tl_.mark("  h2d");
         MP_HIP(hipEventRecord(Q.ev_h2d, s));
         Q.h2d_pending = true;
@@ -1640,10 +1716,8 @@ void Run::run(Model *best, Stats *S) {
     lanes_[0].slot = &X_.sweep_slot[0];
     lanes_[0].sel = &rs_.sel;
     {
-        const char *e = std::getenv("MADPOSE_LO_PARALLEL");
-        lo_parallel_ = !(e && e[0] == '0') && o_.num_lo_steps > 1;
-        const char *d = std::getenv("MADPOSE_DEVICE_LM");
-        device_lm_ = d && d[0] == '1';
+        lo_parallel_ = env_flag("MADPOSE_LO_PARALLEL", true) && o_.num_lo_steps > 1;
+        device_lm_ = env_flag("MADPOSE_DEVICE_LM", false);
     }
     if (lo_parallel_) {
         const int nl = lo_lanes_setting();
@@ -1708,8 +1782,7 @@ void Run::run(Model *best, Stats *S) {
     // predicted state and launches it while the steps run; it is kept if the LO ends
     // exactly there (else discarded), so results never depend on the speculation.
     const bool speculate = [] {
-        const char *e = std::getenv("MADPOSE_LO_SPECULATE");
-        return !(e && e[0] == '0');
+        return env_flag("MADPOSE_LO_SPECULATE", true);
     }();
     // Chained speculation (MADPOSE_LO_CHAIN=0 disables): the sampler job of the post-LO
     // batch (at `at`, Bs iterations, in `slot`) also draws the batch after it into the
@@ -1717,8 +1790,7 @@ void Run::run(Model *best, Stats *S) {
     // speculative batch comes next and leads to no LO, that one is next and is already
     // drawn when the host has read the speculative batch.
     const bool chain_on = [] {
-        const char *e = std::getenv("MADPOSE_LO_CHAIN");
-        return !(e && e[0] == '0');
+        return env_flag("MADPOSE_LO_CHAIN", true);
     }();
     bool chain_ready = false; // gen[cur ^ 1] holds the drawn batch from chain_at on
     uint32_t chain_at = 0;
@@ -1731,8 +1803,7 @@ void Run::run(Model *best, Stats *S) {
     // 4.24 ms, sf 9.72 -> 9.93 ms (its discarded batches overlap the next scoring,
     // profiles/r05/chain_launch).
     const bool chain_launch = [] {
-        const char *e = std::getenv("MADPOSE_LO_CHAIN_LAUNCH");
-        return e && e[0] == '1';
+        return env_flag("MADPOSE_LO_CHAIN_LAUNCH", false);
     }();
     auto make_chain = [&](uint32_t at, uint32_t Bs, int slot, double bound, Sampler::Chain *ch, uint32_t *ch_at) {
         const uint32_t at2 = at + Bs;
@@ -1750,7 +1821,7 @@ void Run::run(Model *best, Stats *S) {
                 launch_batch(*g2, bound, cut, prev);
             };
         }
-        *ch = Sampler::Chain{g2, B2, slot ^ 1, slot_ptr(slot ^ 1), std::move(after)};
+        *ch = Sampler::Chain{g2, B2, slot ^ 1, slot_for(slot ^ 1, B2), std::move(after)};
         *ch_at = at2;
         return true;
     };
@@ -1782,7 +1853,7 @@ void Run::run(Model *best, Stats *S) {
                 Sampler::Chain ch;
                 spec0_chain = make_chain(at, Bs, slot, bound, &ch, &spec0_chain_at);
                 spec0_chain_launched = spec0_chain && ch.after != nullptr;
-                X_.sampler->start(from, gs, Bs, slot, slot_ptr(slot),
+                X_.sampler->start(from, gs, Bs, slot, slot_for(slot, Bs),
                                   [this, gs, bound, at, lo_start] {
                                       MP_HIP(hipSetDevice(X_.device));
                                       launch_batch(*gs, bound, at >= lo_start);
@@ -1864,12 +1935,12 @@ void Run::run(Model *best, Stats *S) {
                 const double bound = best_min_score;
                 const bool cut_next = it_next >= lo_start;
                 const BatchBufs *prev = it >= lo_start ? &Q : nullptr; // this batch can publish a record
-                X_.sampler->start(rs_, gn, Bn, cur ^ 1, slot_ptr(cur ^ 1), [this, gn, bound, cut_next, prev] {
+                X_.sampler->start(rs_, gn, Bn, cur ^ 1, slot_for(cur ^ 1, Bn), [this, gn, bound, cut_next, prev] {
                     MP_HIP(hipSetDevice(X_.device));
                     launch_batch(*gn, bound, cut_next, prev);
                 });
             } else {
-                X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_ptr(cur ^ 1));
+                X_.sampler->start(rs_, &gen[cur ^ 1], Bn, cur ^ 1, slot_for(cur ^ 1, Bn));
             }
         }
         auto tw = Clock::now();
@@ -2034,7 +2105,7 @@ void Run::run(Model *best, Stats *S) {
                                 Sampler::Chain ch;
                                 spec_chain = make_chain(at, Bs, slot, bound, &ch, &spec_chain_at);
                                 spec_chain_launched = spec_chain && ch.after != nullptr;
-                                X_.sampler->start(from, gs, Bs, slot, slot_ptr(slot),
+                                X_.sampler->start(from, gs, Bs, slot, slot_for(slot, Bs),
                                                   [this, gs, bound, at, lo_start] {
                                                       // the sampler thread is not bound to the
                                                       // estimator's device by itself
@@ -2193,8 +2264,7 @@ void validate(const PairInput &in, const RansacOptions &o) {
 // (MADPOSE_PROF_OFF=1: profiling stays off whatever the caller asks -- A/B of its cost)
 void profile_enable(bool on) {
     static const bool off = [] {
-        const char *e = std::getenv("MADPOSE_PROF_OFF");
-        return e && e[0] == '1';
+        return env_flag("MADPOSE_PROF_OFF", false);
     }();
     g_prof_on.store(on && !off);
 }
@@ -2524,11 +2594,11 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
     std::memcpy(in, x1, sizeof(double) * per);
     std::memcpy(in + per, x2, sizeof(double) * per);
     constexpr int kCap = 16;
-    DevArray<double> d_in(30);
-    DevArray<int> d_n(1);
+    DevArray<double> d_in(30), d_cand(kPtCandStride);
+    DevArray<int> d_n(1), d_nc(1);
     DevArray<Model> d_poses(kCap);
     MP_HIP(hipMemcpyAsync(d_in.p, in, sizeof(in), hipMemcpyHostToDevice, X.stream));
-    MP_HIP(launch_point_direct(X.stream, kind, d_in.p, d_poses.p, d_n.p));
+    MP_HIP(launch_point_direct(X.stream, kind, d_in.p, d_poses.p, d_n.p, d_cand.p, d_nc.p));
     int hn = 0;
     Model hp[kCap];
     MP_HIP(hipMemcpyAsync(&hn, d_n.p, sizeof(int), hipMemcpyDeviceToHost, X.stream));
@@ -2540,11 +2610,12 @@ int solve_point_direct(int kind, const double *x1, const double *x2, Model *pose
 
 void debug_pt_roots(int variant, int64_t ns, const double *pts0, const double *pts1, double *cand, int *ncand,
                     int device) {
-    if (variant != kCal && variant != kSF) throw std::invalid_argument("variant must be 0 (5pt) or 1 (6pt)");
+    if (variant != kCal && variant != kSF && variant != kTF)
+        throw std::invalid_argument("variant must be 0 (5pt), 1 (6pt) or 2 (7pt)");
     if (ns <= 0 || ns > (1 << 22)) throw std::invalid_argument("bad number of samples");
     CtxLease lease(device);
     DeviceCtx &X = *lease.c;
-    const int K = variant == kCal ? 5 : 6;
+    const int K = variant == kCal ? 5 : (variant == kSF ? 6 : 7);
     const int64_t np = K * ns;
     // one correspondence per sample point, identity intrinsics, sample s = points Ks..Ks+K-1
     std::vector<double> host(8 * (size_t)np);

@@ -1,6 +1,7 @@
 // Host LM for LO -- see lm.h.
 #include "lm.h"
 #include "lm_eval.h"
+#include "env.h"
 
 #include <sched.h>
 
@@ -119,7 +120,7 @@ constexpr int kSpinCpusPerRank = 12; // about the threads one rank keeps busy (L
 
 int lo_spin_us() {
     static const int v = [] {
-        if (const char *e = std::getenv("MADPOSE_LO_SPIN")) return std::max(0, std::atoi(e));
+        if (std::getenv("MADPOSE_LO_SPIN")) return (int)env_int("MADPOSE_LO_SPIN", 0, 0, 1000000);
         int cpus = 0;
         cpu_set_t set;
         CPU_ZERO(&set);
@@ -146,8 +147,7 @@ constexpr int kNarrow = 4;
 // (prefix 132-134 us).  MADPOSE_LM_WIDE overrides the threshold, in blocks.
 size_t pool_wide() {
     static const size_t v = [] {
-        const char *e = std::getenv("MADPOSE_LM_WIDE");
-        return e ? (size_t)std::max(1L, std::atol(e)) : (size_t)2048;
+        return (size_t)env_int("MADPOSE_LM_WIDE", 2048, 1, 1ll << 40);
     }();
     return v;
 }
@@ -254,9 +254,7 @@ class Pool {
 
 Pool &lo_pool() {
     static Pool pool([] {
-        const char *e = std::getenv("MADPOSE_LO_THREADS");
-        const int n = e ? std::atoi(e) : 8;
-        return std::max(1, std::min(n, 64));
+        return (int)env_int("MADPOSE_LO_THREADS", 8, 1, 64);
     }());
     return pool;
 }
@@ -265,8 +263,7 @@ Pool &lo_pool() {
 // either way, lm_eval.inc); MADPOSE_LM_ISA=avx2 forces the AVX2 build (A/B)
 bool lm_eval_avx512() {
     static const bool on = [] {
-        const char *e = std::getenv("MADPOSE_LM_ISA");
-        if (e && std::strcmp(e, "avx2") == 0) return false;
+        if (env_avx2("MADPOSE_LM_ISA")) return false;
         __builtin_cpu_init();
         return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
                __builtin_cpu_supports("avx512vl");

@@ -14,6 +14,7 @@
 // (K^-1 x and the unit bearings of the calibrated variant) are formed once per pair
 // with the same operations.
 #include "lo_sweep.h"
+#include "env.h"
 
 #include <algorithm>
 #include <cfloat>
@@ -259,8 +260,7 @@ __attribute__((target("avx512f,avx512dq,avx512vl"))) void sweep_avx512(const LoS
 
 bool use_avx512() {
     static const bool on = [] {
-        const char *e = std::getenv("MADPOSE_LO_SWEEP_ISA"); // "avx2": the 4-wide path (A/B)
-        if (e && std::strcmp(e, "avx2") == 0) return false;
+        if (env_avx2("MADPOSE_LO_SWEEP_ISA")) return false; // the 4-wide path (A/B)
         __builtin_cpu_init();
         return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
                __builtin_cpu_supports("avx512vl");

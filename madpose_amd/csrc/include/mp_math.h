@@ -18,6 +18,24 @@ MP_HD void cross3(const double *a, const double *b, double *c) {
 }
 MP_HD double dot3(const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
+// the same without FMA contraction (the exact point-solver stages: the oracle's
+// operations to the bit)
+MP_HD void cross3_x(const double *a, const double *b, double *c) {
+#pragma clang fp contract(off)
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+MP_HD double dot3_x(const double *a, const double *b) {
+#pragma clang fp contract(off)
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+MP_HD void matvec3_x(const double *A, const double *v, double *o) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) o[r] = A[3 * r] * v[0] + A[3 * r + 1] * v[1] + A[3 * r + 2] * v[2];
+}
+
 MP_HD void matmul3(const double *A, const double *B, double *C) {
 #pragma unroll
     for (int r = 0; r < 3; ++r)

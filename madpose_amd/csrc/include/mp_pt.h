@@ -154,7 +154,10 @@ struct Cub {
 // the accumulators to leave private (scratch) memory.  Terms are accumulated in
 // the order of the loops they replace: i outer, j inner (lin_mul); a, b >= a, c
 // (quad_lin_acc).
+// (no FMA contraction in these products: the 5pt root stage is the oracle's to the bit,
+// kernels/group_5pt.h)
 template <int K> MP_HD void lin_mul_term(const Lin &a, const Lin &b, Quad &o) {
+#pragma clang fp contract(off)
     constexpr int slot = quad_index(K / 4, K % 4);
     o.c[slot] += a.c[K / 4] * b.c[K % 4];
 }
@@ -167,6 +170,7 @@ MP_HD void lin_mul(const Lin &a, const Lin &b, Quad &o) {
 }
 
 template <int A, int B, int Cc> MP_HD void quad_lin_term(const Quad &q, const Lin &l, double s, Cub &o) {
+#pragma clang fp contract(off)
     if constexpr (A <= B) {
         constexpr int ex = lin_e(A, 0) + lin_e(B, 0) + lin_e(Cc, 0);
         constexpr int ey = lin_e(A, 1) + lin_e(B, 1) + lin_e(Cc, 1);
@@ -181,6 +185,56 @@ MP_HD void quad_lin_all(const Quad &q, const Lin &l, double s, Cub &o, std::inte
 }
 MP_HD void quad_lin_acc(const Quad &q, const Lin &l, double s, Cub &o) {
     quad_lin_all(q, l, s, o, std::make_integer_sequence<int, 64>());
+}
+
+// Householder null space of a K x 9 system (rows = epipolar constraints) without FMA
+// contraction: the oracle's householder_nullspace<K> (oracle/src/pt_poselib.cpp) to the
+// bit -- Q = H_0 .. H_{K-1} of the QR of Q^T, the basis vectors Q e_{K+b}.  The 5pt
+// root stage (K = 5) and the 7pt solver (K = 7).
+template <int K> MP_HD void householder_nullspace_x(const double (&Q)[K][9], double (&N)[9 - K][9]) {
+#pragma clang fp contract(off)
+    double A[9][K];
+    static_for<K>([&](auto i) { static_for<9>([&](auto e) { A[e][i] = Q[i][e]; }); });
+    double V[K][9], beta[K];
+    static_for<K>([&](auto k) {
+        double nrm = 0.0;
+        static_for<9>([&](auto i) {
+            if constexpr (i >= k) nrm += A[i][k] * A[i][k];
+        });
+        nrm = sqrt(nrm);
+        const double alpha = (A[k][k] > 0) ? -nrm : nrm;
+        double vn = 0.0;
+        static_for<9>([&](auto i) {
+            if constexpr (i < k) {
+                V[k][i] = 0.0;
+            } else {
+                V[k][i] = A[i][k];
+                if constexpr (i == k) V[k][i] -= alpha;
+            }
+            vn += V[k][i] * V[k][i];
+        });
+        beta[k] = (vn > 0) ? 2.0 / vn : 0.0;
+        static_for<K>([&](auto j) {
+            if constexpr (j >= k) {
+                double d = 0.0;
+                static_for<9>([&](auto i) { d += V[k][i] * A[i][j]; });
+                d *= beta[k];
+                static_for<9>([&](auto i) { A[i][j] -= d * V[k][i]; });
+            }
+        });
+    });
+    static_for<9 - K>([&](auto b) {
+        double v[9];
+        static_for<9>([&](auto i) { v[i] = (i == K + b) ? 1.0 : 0.0; });
+        static_for<K>([&](auto kk) {
+            constexpr int k = K - 1 - kk;
+            double d = 0.0;
+            static_for<9>([&](auto i) { d += V[k][i] * v[i]; });
+            d *= beta[k];
+            static_for<9>([&](auto i) { v[i] -= d * V[k][i]; });
+        });
+        static_for<9>([&](auto i) { N[b][i] = v[i]; });
+    });
 }
 
 // Householder null space of the 5x9 system (rows = points), returning 4 basis

@@ -4,7 +4,8 @@
 //   relpose_7pt_F   PoseLib relpose_7pt as called at
 //                   src/hybrid_pose_two_focal_estimator.cpp:116 -- Householder null
 //                   space of the 7x9 epipolar system, det(a N0 + N1) expanded
-//                   multilinearly into a cubic, real roots by Sturm bisection.
+//                   multilinearly into a cubic, PoseLib's closed-form solve_cubic_real
+//                   (round 6: the oracle's restatement, oracle/src/pt_poselib.cpp).
 //   bougnoux_sq     the reference's bougnoux_focals (:11-32) in closed form (the
 //                   epipoles are the cross products of rows / columns of the rank-2 F).
 //   recover_pose_cv cv::recoverPose(E, p0, p1, I, R, t, 1e9) (:143): R1 = U W V^T,
@@ -97,19 +98,71 @@ MP_HD double det_rows(const double *a, const double *b, const double *c) {
 }
 
 // ---------------------------------------------------------------------------
-// 7-point fundamental matrices: returns k <= 3, F[k] row-major with x2^T F x1 = 0.
+// det_rows without FMA contraction (the 7pt cubic: the oracle's expression)
+MP_HD double det_rows_x(const double *a, const double *b, const double *c) {
+#pragma clang fp contract(off)
+    return a[0] * (b[1] * c[2] - b[2] * c[1]) - a[1] * (b[0] * c[2] - b[2] * c[0]) + a[2] * (b[0] * c[1] - b[1] * c[0]);
+}
+
+// PoseLib misc/univariate.cc solve_cubic_real (oracle/src/pt_poselib.cpp): real roots of
+// x^3 + c2 x^2 + c1 x + c0 -- Cardano when the discriminant term is positive (one
+// root), the trigonometric form otherwise (three), one Newton step each.  The root
+// count depends on +, -, *, / only, so it is the oracle's; cbrt / acos / cos come from
+// the device math library (the host's may differ in the last bit).
+MP_HD int solve_cubic_real_x(double c2, double c1, double c0, double (&roots)[3]) {
+#pragma clang fp contract(off)
+    double a = c1 - c2 * c2 / 3.0;
+    double b = (2.0 * c2 * c2 * c2 - 9.0 * c2 * c1) / 27.0 + c0;
+    double c = b * b / 4.0 + a * a * a / 27.0;
+    int n_roots;
+    if (c > 0) {
+        c = sqrt(c);
+        b *= -0.5;
+        roots[0] = cbrt(b + c) + cbrt(b - c) - c2 / 3.0;
+        roots[1] = roots[2] = 0.0;
+        n_roots = 1;
+    } else {
+        c = 3.0 * b / (2.0 * a) * sqrt(-3.0 / a);
+        const double d = 2.0 * sqrt(-a / 3.0);
+        const double theta = acos(c) / 3.0;
+        roots[0] = d * cos(theta) - c2 / 3.0;
+        roots[1] = d * cos(theta - 2.0 * M_PI / 3.0) - c2 / 3.0;
+        roots[2] = d * cos(theta - 4.0 * M_PI / 3.0) - c2 / 3.0;
+        n_roots = 3;
+    }
+    static_for<3>([&](auto i) {
+        if (i < n_roots) {
+            const double x = roots[i];
+            const double x2 = x * x;
+            const double x3 = x * x2;
+            const double dx = -(x3 + c2 * x2 + c1 * x + c0) / (3 * x2 + 2 * c2 * x + c1);
+            roots[i] += dx;
+        }
+    });
+    return n_roots;
+}
+
+// 7-point fundamental matrices (PoseLib relpose_7pt, as the oracle's restatement
+// oracle/src/pt_poselib.cpp): Householder null space of the 7 x 9 system, det(a N0 +
+// N1) expanded by rows into c3 a^3 + .. + c0, normalised by c3, solve_cubic_real, F = a
+// N0 + N1 normalised.  Returns k (1 or 3), F[k] row-major with x2^T F x1 = 0.  (Until
+// round 5: Sturm bisection of the cubic.)
 MP_HD int relpose_7pt_F(const double (&x1)[7][3], const double (&x2)[7][3], double (&F)[3][9]) {
+#pragma clang fp contract(off)
     double Q[7][9], N[2][9];
     epipolar_rows<7>(x1, x2, Q);
-    nullspace_kx9<7>(Q, N);
+    householder_nullspace_x<7>(Q, N);
     const double *A = N[0], *B = N[1];
-    double c[4];
-    c[3] = det_rows(A, A + 3, A + 6);
-    c[2] = det_rows(A, A + 3, B + 6) + det_rows(A, B + 3, A + 6) + det_rows(B, A + 3, A + 6);
-    c[1] = det_rows(A, B + 3, B + 6) + det_rows(B, A + 3, B + 6) + det_rows(B, B + 3, A + 6);
-    c[0] = det_rows(B, B + 3, B + 6);
+    const double c3 = det_rows_x(A, A + 3, A + 6);
+    double c2 = det_rows_x(A, A + 3, B + 6) + det_rows_x(A, B + 3, A + 6) + det_rows_x(B, A + 3, A + 6);
+    double c1 = det_rows_x(A, B + 3, B + 6) + det_rows_x(B, A + 3, B + 6) + det_rows_x(B, B + 3, A + 6);
+    double c0 = det_rows_x(B, B + 3, B + 6);
+    const double inv_c3 = 1.0 / c3;
+    c2 *= inv_c3;
+    c1 *= inv_c3;
+    c0 *= inv_c3;
     double roots[3];
-    const int nr = sturm_real_roots<3>(c, roots);
+    const int nr = solve_cubic_real_x(c2, c1, c0, roots);
     // (constant indices from the front end on: F and roots stay in registers)
     static_for<3>([&](auto K) {
         constexpr int k = decltype(K)::value;
@@ -120,9 +173,9 @@ MP_HD int relpose_7pt_F(const double (&x1)[7][3], const double (&x2)[7][3], doub
                 F[k][e] = roots[k] * A[e] + B[e];
                 nn += F[k][e] * F[k][e];
             }
-            nn = 1.0 / sqrt(nn);
+            nn = sqrt(nn);
 #pragma unroll
-            for (int e = 0; e < 9; ++e) F[k][e] *= nn;
+            for (int e = 0; e < 9; ++e) F[k][e] /= nn;
         }
     });
     return nr;

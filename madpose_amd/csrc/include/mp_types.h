@@ -105,8 +105,9 @@ struct BatchGate {
 };
 
 // Per-iteration outcome of a batch (score_batch): the iteration's best score
-// (GetBestEstimatedModelId), its model slot and the number of models -- one 16-byte
-// record, so a batch's results come back in one copy.
+// (GetBestEstimatedModelId), its bounds, its model slot and the number of models -- one
+// 32-byte record; the walk reads only the marked iterations' records (written to mapped
+// host memory) and one flag byte per iteration (engine.cpp).
 // hi = best + the best model's margin (its reference-order score is below hi), lo = the
 // smallest score - margin over the iteration's models (no reference-order score of the
 // iteration is below lo).  slot | kSlotAmbiguous: another model's interval reaches the

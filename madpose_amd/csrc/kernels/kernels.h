@@ -85,7 +85,9 @@ hipError_t launch_score_models(hipStream_t s, const PairData &D, const PairConst
 // standalone solvers (mp_solve_* C API): one sample, one thread
 hipError_t launch_md_direct(hipStream_t s, int variant, int alt, const double *in /* x(3K) y(3K) dx(K) dy(K) */,
                             double *sols, int *nsols, Model *poses, int *nposes);
-hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes);
+// (kind 0: cand / ncand are the root stage's workspace, kPtCandStride doubles and one int)
+hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes, double *cand,
+                               int *ncand);
 // shared-focal 6pt poses from a root stage's output (cand: null space + roots of one
 // sample, ncand: root count); in: the 6 + 6 normalized 2-D points
 hipError_t launch_point_direct_6pt(hipStream_t s, const double *in, const double *cand, const int *ncand,

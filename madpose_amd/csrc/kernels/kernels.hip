@@ -29,6 +29,7 @@
 #include "eig6_defl_grp.h"
 #include "lm_device.h"
 #include "kernels.h"
+#include "../host/env.h"
 
 namespace mp {
 
@@ -389,6 +390,24 @@ __device__ inline void load_uncal_sample(const PairData &D, const int *s, double
     }
 }
 
+// the same with the oracle's bearings to the bit (c / |c|, no FMA contraction): the
+// two-focal 7pt root stage, which is the oracle's relpose_7pt operation for operation
+template <int K>
+__device__ inline void load_uncal_sample_x(const PairData &D, const int *s, double (&b0)[K][3], double (&b1)[K][3]) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const int i = s[j];
+        const double a[3] = {D.x0u[i], D.x0v[i], 1.0}, c[3] = {D.x1u[i], D.x1v[i], 1.0};
+        const double na = sqrt(dot3_x(a, a)), nc = sqrt(dot3_x(c, c));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            b0[j][q] = a[q] / na;
+            b1[j][q] = c[q] / nc;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Point solvers in three stages, so that the per-root work (pose recovery, depth
 // tail) runs one root per lane instead of looping inside one lane per sample:
@@ -412,7 +431,8 @@ template <> struct PtTraits<kTF> {
 };
 
 // two-focal root stage, one lane per sample: the 7-point fundamental matrices
-// (PoseLib relpose_7pt: cubic by multilinear expansion, Sturm roots)
+// (PoseLib relpose_7pt: cubic by multilinear expansion, closed-form roots; the
+// oracle's relpose_7pt operation for operation, oracle/src/pt_poselib.cpp)
 __global__ void __launch_bounds__(64) pt_roots7_kernel(PairData D, const int *list, int nlist, const int *samples,
                                                        double *cand, int *ncand) {
     if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
@@ -420,8 +440,8 @@ __global__ void __launch_bounds__(64) pt_roots7_kernel(PairData D, const int *li
     if (idx >= nlist) return;
     const int *s = samples + (size_t)list[idx] * kSampleStride;
     double *out = cand + (size_t)idx * kCandStride;
-    double b0[7][3], b1[7][3], p0[7][2], p1[7][2], dd0[7], dd1[7];
-    load_uncal_sample<7>(D, s, b0, b1, p0, p1, dd0, dd1);
+    double b0[7][3], b1[7][3];
+    load_uncal_sample_x<7>(D, s, b0, b1);
     double F[3][9];
     const int n = relpose_7pt_F(b0, b1, F);
     static_for<3>([&](auto K) {
@@ -928,13 +948,7 @@ __global__ void md_direct_kernel(int variant, int alt, const double *in, double 
 __global__ void point_direct_kernel(int kind, const double *in, Model *poses, int *nposes) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     if (kind == 0) {
-        double b1[5][3], b2[5][3];
-        for (int j = 0; j < 5; ++j)
-            for (int c = 0; c < 3; ++c) {
-                b1[j][c] = in[3 * j + c];
-                b2[j][c] = in[15 + 3 * j + c];
-            }
-        *nposes = relpose_5pt(b1, b2, poses, kMaxModelsCal);
+        *nposes = 0; // (launch_point_direct runs the 5pt through the estimator's root stage)
     } else {
         double b0[7][3], b1[7][3], p0[7][2], p1[7][2];
         for (int j = 0; j < 7; ++j) {
@@ -1035,8 +1049,9 @@ static bool md_plain(const PairConst &C) {
 // md_exact's lanes per sample (MADPOSE_MDX_R=1|2|4 overrides the default)
 static int md_lanes(int v) {
     static const int r_env = [] {
-        const char *e = std::getenv("MADPOSE_MDX_R");
-        return e ? std::atoi(e) : 0;
+        const int r = (int)env_int("MADPOSE_MDX_R", 0, 0, 4);
+        if (r == 3) env_reject("MADPOSE_MDX_R", "3", "expected 1, 2 or 4");
+        return r;
     }();
     return (r_env == 1 || r_env == 2 || r_env == 4) ? r_env : (v == kSF ? 2 : 4);
 }
@@ -1084,8 +1099,7 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
 // MADPOSE_EIG_WAVES overrides, MADPOSE_EIG_WAVES=16 packs 64 samples per wave at 1024)
 int eig_spw(int nlist) {
     static const int waves = [] {
-        const char *e = std::getenv("MADPOSE_EIG_WAVES");
-        return e ? std::max(1, std::atoi(e)) : 1024;
+        return (int)env_int("MADPOSE_EIG_WAVES", 1024, 1, 1 << 20);
     }();
     return std::min(64, std::max(1, (nlist + waves - 1) / waves));
 }
@@ -1106,8 +1120,7 @@ static void launch_sf_eig(hipStream_t s, const PairData &D, const int *list, int
 
 bool solve_fusable(const PairConst &C) {
     static const bool off = [] {
-        const char *e = std::getenv("MADPOSE_SOLVE_FUSE");
-        return e && e[0] == '0';
+        return !env_flag("MADPOSE_SOLVE_FUSE", true);
     }();
     return !off && C.variant == kCal && md_plain(C) && md_lanes(kCal) == 4;
 }
@@ -1165,18 +1178,17 @@ static ScoreBound score_bound(const PairConst &C, double best, int *work, unsign
                               const Model *models, Model *rec_out, bool *exit) {
     const int n = C.n;
     static const int mode = [] {
-        const char *e = std::getenv("MADPOSE_SCORE_EXIT");
-        return (e && e[0] == '0') ? 0 : 1;
+        return env_flag("MADPOSE_SCORE_EXIT", true) ? 1 : 0;
     }();
-    static const int sched[2] = {[] {
-                                     const char *e = std::getenv("MADPOSE_SCORE_CHECK");
-                                     return e ? std::max(1, std::atoi(e)) : 0;
-                                 }(),
-                                 [] {
-                                     const char *e = std::getenv("MADPOSE_SCORE_CHECK");
-                                     const char *c = e ? std::strchr(e, ',') : nullptr;
-                                     return c ? std::max(1, std::atoi(c + 1)) : 1;
-                                 }()};
+    // "first,every" (or "first": every trip after it), both >= 1
+    static const std::pair<int, int> sched = [] {
+        const char *e = std::getenv("MADPOSE_SCORE_CHECK");
+        if (!e) return std::pair<int, int>(0, 1);
+        int f = 0, v = 1, used = 0;
+        const int k = std::sscanf(e, "%d%n,%d%n", &f, &used, &v, &used);
+        if (k < 1 || e[used] != '\0' || f < 1 || v < 1) env_reject("MADPOSE_SCORE_CHECK", e, "expected first[,every] >= 1");
+        return std::pair<int, int>(f, k == 2 ? v : 1);
+    }();
     ScoreBound sb;
     // the exit and the record skip rest on every MSAC term being >= 0 (a partial sum is
     // then a lower bound of the total): errors are squares or DBL_MAX, thresholds are
@@ -1194,17 +1206,15 @@ static ScoreBound score_bound(const PairConst &C, double best, int *work, unsign
     // averages): cal 44.7 / 45.5 / 47.7 us at 2,2 / 1,1 / 3,3, sf 33.1 / 35.2 us at 2,2 /
     // 1,1, tf (N = 4000) 56.7 us at 2,2 against 60.2 at 4,4
     const int q = std::min(2, std::max(1, ntrip / 4));
-    sb.first = sched[0] > 0 ? sched[0] : q;
-    sb.every = sched[0] > 0 ? sched[1] : q;
+    sb.first = sched.first > 0 ? sched.first : q;
+    sb.every = sched.first > 0 ? sched.second : q;
     sb.work = work;
     static const int pair = [] {
-        const char *e = std::getenv("MADPOSE_SCORE_PAIR");
-        return (e && e[0] == '0') ? 0 : 1;
+        return env_flag("MADPOSE_SCORE_PAIR", true) ? 1 : 0;
     }();
     sb.pair = pair;
     static const bool skip = [] {
-        const char *e = std::getenv("MADPOSE_RECORD_SKIP");
-        return !(e && e[0] == '0');
+        return env_flag("MADPOSE_RECORD_SKIP", true);
     }();
     sb.rec = (skip && on) ? rec : nullptr;
     sb.epoch_hi = epoch_hi;
@@ -1261,6 +1271,8 @@ hipError_t launch_pt_roots(hipStream_t s, const PairData &D, const PairConst &C,
                                                                       kCandStride);
     else if (C.variant == kSF && pen)
         launch_sf_eig(s, D, list, nlist, samples, cand, ncand, pen);
+    else if (C.variant == kTF)
+        pt_roots7_kernel<<<(nlist + 63) / 64, 64, 0, s>>>(D, list, nlist, samples, cand, ncand);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -1518,7 +1530,30 @@ hipError_t launch_point_direct_6pt(hipStream_t s, const double *in, const double
     return hipGetLastError();
 }
 
-hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes) {
+// the poses of a 5-point sample from the estimator's root stage (E candidates in cand):
+// motion_from_essential with cheirality on the five bearings, one lane
+__global__ void point_direct_5pt_kernel(const double *in, const double *cand, const int *ncand, Model *poses,
+                                        int *nposes) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double b1[5][3], b2[5][3];
+    for (int j = 0; j < 5; ++j)
+        for (int c = 0; c < 3; ++c) {
+            b1[j][c] = in[3 * j + c];
+            b2[j][c] = in[15 + 3 * j + c];
+        }
+    int k = 0;
+    for (int e = 0; e < ncand[0] && e < 10; ++e) k += motion_from_essential<5>(cand + 9 * e, b1, b2, poses, k, kMaxModelsCal);
+    *nposes = k;
+}
+
+hipError_t launch_point_direct(hipStream_t s, int kind, const double *in, Model *poses, int *nposes, double *cand,
+                               int *ncand) {
+    if (kind == 0) {
+        // the estimator's root stage (group_5pt.h) on the one sample, then its poses
+        pt_roots5_bearings_kernel<<<1, 64, 0, s>>>(in, 1, cand, ncand, kCandStride);
+        point_direct_5pt_kernel<<<1, 64, 0, s>>>(in, cand, ncand, poses, nposes);
+        return hipGetLastError();
+    }
     point_direct_kernel<<<1, 64, 0, s>>>(kind, in, poses, nposes);
     return hipGetLastError();
 }

@@ -150,6 +150,38 @@ def relpose_5pt(b1, b2):
     return [model_to_dict(out[i]) for i in range(min(n, 32))]
 
 
+def relpose_5pt_E(b1, b2):
+    """Root stage of the 5pt restatement (PoseLib: Nister + Sturm bisection): the
+    essential matrices (k, 3, 3) and the real roots z of det B(z), ascending."""
+    E = np.zeros((16, 9))
+    roots = np.zeros(10)
+    nr = ctypes.c_int(0)
+    n = lib().oracle_relpose_5pt_E(_dp(_c(b1)), _dp(_c(b2)), _dp(E), 16, _dp(roots), ctypes.byref(nr))
+    return E[:n].reshape(-1, 3, 3).copy(), roots[:min(nr.value, 10)].copy()
+
+
+def relpose_5pt_action(b1, b2):
+    """The same 5-point problem by Stewenius' action matrix (an independent algorithm)."""
+    out = (OrModel * 32)()
+    n = lib().oracle_relpose_5pt_action(_dp(_c(b1)), _dp(_c(b2)), out, 32)
+    return [model_to_dict(out[i]) for i in range(min(n, 32))]
+
+
+def relpose_7pt_svd(b1, b2):
+    """The 7-point problem by an SVD null space + companion roots (independent cross-check)."""
+    out = np.zeros((8, 9))
+    n = lib().oracle_relpose_7pt_svd(_dp(_c(b1)), _dp(_c(b2)), _dp(out), 8)
+    return out[:n].reshape(-1, 3, 3).copy()
+
+
+def solve_cubic_real(c2, c1, c0):
+    """PoseLib solve_cubic_real: real roots of x^3 + c2 x^2 + c1 x + c0 (1 or 3)."""
+    lib().oracle_solve_cubic_real.argtypes = [ctypes.c_double] * 3 + [ctypes.POINTER(ctypes.c_double)]
+    out = np.zeros(3)
+    n = lib().oracle_solve_cubic_real(float(c2), float(c1), float(c0), _dp(out))
+    return out[:n].copy()
+
+
 def sixpt_roots(b1, b2):
     """Root stage of the 6pt restatement: positive real u = f^2 (deflated companion)."""
     out = np.zeros(32)

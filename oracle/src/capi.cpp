@@ -135,6 +135,38 @@ int oracle_relpose_5pt(const double *x1, const double *x2, or_model *out, int ma
     return (int)sols.size();
 }
 
+// E candidates of the 5-point root stage and the roots z (ascending); returns the
+// number of E (<= max_out written); *nroots = number of real roots (<= 10 written)
+int oracle_relpose_5pt_E(const double *x1, const double *x2, double *E_out, int max_out, double *roots, int *nroots) {
+    std::vector<double> rz;
+    auto Es = oracle::relpose_5pt_E(x1, x2, &rz);
+    const int n = std::min((int)Es.size(), max_out);
+    for (int i = 0; i < n; ++i)
+        for (int e = 0; e < 9; ++e) E_out[9 * i + e] = Es[i][e];
+    *nroots = (int)rz.size();
+    for (size_t k = 0; k < rz.size() && k < 10; ++k) roots[k] = rz[k];
+    return (int)Es.size();
+}
+
+int oracle_relpose_5pt_action(const double *x1, const double *x2, or_model *out, int max_out) {
+    auto sols = oracle::relpose_5pt_action(x1, x2);
+    int n = std::min((int)sols.size(), max_out);
+    for (int i = 0; i < n; ++i) put_model(sols[i], &out[i]);
+    return (int)sols.size();
+}
+
+int oracle_relpose_7pt_svd(const double *x1, const double *x2, double *F_out, int max_out) {
+    auto sols = oracle::relpose_7pt_svd(x1, x2);
+    int n = std::min((int)sols.size(), max_out);
+    for (int i = 0; i < n; ++i)
+        for (int e = 0; e < 9; ++e) F_out[9 * i + e] = sols[i][e];
+    return (int)sols.size();
+}
+
+int oracle_solve_cubic_real(double c2, double c1, double c0, double *roots) {
+    return oracle::solve_cubic_real(c2, c1, c0, roots);
+}
+
 int oracle_scale_and_pose(const double *X, const double *Y, const double *W, int k, or_model *out) {
     put_model(oracle::estimate_scale_and_pose(X, Y, W, k), out);
     return 0;

@@ -4,8 +4,10 @@
 // because PoseLib v2.0.4 / OpenCV are not vendored in the reference
 // (CMakeLists.txt:25-37): parity for these is "unpinned" (see DESIGN.md).
 //
-//   relpose_5pt  -- PoseLib relpose_5pt as called at src/hybrid_pose_estimator.cpp:134.
-//                   Restated as Stewenius/Nister: 4-dim null space of the 5x9
+//   relpose_5pt_action -- the 5-point problem of PoseLib relpose_5pt (called at
+//                   src/hybrid_pose_estimator.cpp:134) by a different algorithm than the
+//                   estimator's restatement (pt_poselib.cpp), kept as a cross-check.
+//                   Stewenius' action-matrix form: 4-dim null space of the 5x9
 //                   epipolar system, ten cubic constraints (det E = 0 and
 //                   2 E E^T E - tr(E E^T) E = 0), Gauss-Jordan of the 10x20 template,
 //                   10x10 action matrix for x, real eigenpairs, then
@@ -149,7 +151,7 @@ bool check_cheirality(const double R[9], const double t[3], const double x1[3], 
     return l1 > min_depth && l2 > min_depth;
 }
 
-std::vector<Model> relpose_5pt(const double *x1, const double *x2) {
+std::vector<Model> relpose_5pt_action(const double *x1, const double *x2) {
     std::vector<Model> out;
     // epipolar rows: x2^T E x1 = 0, E row-major
     Mat Q(9, 9);

@@ -4,7 +4,9 @@
 // restated from their published algorithms because neither PoseLib v2.0.4 nor
 // OpenCV is vendored in the reference (parity "unpinned"):
 //
-//   relpose_7pt   PoseLib relpose_7pt (called at src/hybrid_pose_two_focal_estimator.cpp:116):
+//   relpose_7pt_svd  the 7-point problem of PoseLib relpose_7pt (called at
+//                 src/hybrid_pose_two_focal_estimator.cpp:116) by other means than the
+//                 estimator's restatement (pt_poselib.cpp), kept as a cross-check:
 //                 2-dim null space of the 7x9 epipolar system, F(a) = a N0 + N1,
 //                 real roots of the cubic det F(a) = 0, F normalised to unit norm.
 //   bougnoux_focals  src/hybrid_pose_two_focal_estimator.cpp:11-32 (the formula is
@@ -95,7 +97,7 @@ const int kMono[10][2] = {{3, 0}, {2, 1}, {1, 2}, {0, 3}, {2, 0}, {1, 1}, {0, 2}
 
 } // namespace
 
-std::vector<std::array<double, 9>> relpose_7pt(const double *x1, const double *x2) {
+std::vector<std::array<double, 9>> relpose_7pt_svd(const double *x1, const double *x2) {
     Mat V = epipolar_nullspace(x1, x2, 7);
     double N0[9], N1[9];
     for (int e = 0; e < 9; ++e) {

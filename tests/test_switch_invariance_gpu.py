@@ -11,7 +11,11 @@ stage on two streams instead of one fused launch (MADPOSE_SOLVE_FUSE), score_bat
 one trip per loop step instead of two between early-exit checks (MADPOSE_SCORE_PAIR), the
 post-LO speculation predicted after the LO prefix instead of before it
 (MADPOSE_LO_EARLY_HOOK) or not at all (MADPOSE_LO_SPECULATE), and without the batch after
-it drawn (MADPOSE_LO_CHAIN) or launched (MADPOSE_LO_CHAIN_LAUNCH) in the same job."""
+it drawn (MADPOSE_LO_CHAIN) or launched (MADPOSE_LO_CHAIN_LAUNCH) in the same job; the
+scoring without its exact early exit (MADPOSE_SCORE_EXIT) or record skip
+(MADPOSE_RECORD_SKIP), with an exit check after every trip (MADPOSE_SCORE_CHECK), and the
+fused MD + 5pt launch for no batch or for every batch (MADPOSE_SOLVE_FUSE_MAX).  A value
+that does not parse is refused loudly (host/env.h)."""
 import json
 import os
 import subprocess
@@ -30,7 +34,10 @@ SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOS
             "solve_unfused": {"MADPOSE_SOLVE_FUSE": "0"}, "early_big": {"MADPOSE_EARLY_CONT": "3"}, "lo_late_hook": {"MADPOSE_LO_EARLY_HOOK": "0"},
             "lo_no_speculation": {"MADPOSE_LO_SPECULATE": "0"}, "lo_no_chain": {"MADPOSE_LO_CHAIN": "0"},
             "lo_chain_launched": {"MADPOSE_LO_CHAIN_LAUNCH": "1"},
-            "score_single_trips": {"MADPOSE_SCORE_PAIR": "0"}}
+            "score_single_trips": {"MADPOSE_SCORE_PAIR": "0"},
+            "score_no_exit": {"MADPOSE_SCORE_EXIT": "0"}, "no_record_skip": {"MADPOSE_RECORD_SKIP": "0"},
+            "score_check_every_trip": {"MADPOSE_SCORE_CHECK": "1,1"},
+            "fuse_never": {"MADPOSE_SOLVE_FUSE_MAX": "0"}, "fuse_always": {"MADPOSE_SOLVE_FUSE_MAX": "65536"}}
 
 
 def _run(extra):
@@ -57,3 +64,20 @@ def test_switch_changes_no_result(default_run, name):
     assert len(other) == len(default_run)
     for k, (a, b) in enumerate(zip(default_run, other)):
         assert a == b, (name, k, a, b)
+
+
+@pytest.mark.parametrize("var,val", [("MADPOSE_TIE_SCALE", "np.float64(4.0)"), ("MADPOSE_MIN_BATCH", "4k"),
+                                     ("MADPOSE_SCORE_EXIT", "off"), ("MADPOSE_SCORE_CHECK", "2;2")])
+def test_unparsable_switch_is_refused(var, val):
+    """An unparsable MADPOSE_* value raises instead of being read as 0 / 1.0 (VERDICT r05
+    weak #8: MADPOSE_TIE_SCALE="np.float64(...)" once became 1.0 silently)."""
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MADPOSE_")}
+    env[var] = val
+    code = ("import madpose\nfrom madpose_amd import synthetic\np = synthetic.config_pair(2, seed=0)\n"
+            "o, c = synthetic.throughput_options('calibrated', iterations=2000)\n"
+            "try:\n    madpose.HybridEstimatePoseScaleOffset(p['x0'], p['x1'], p['depth0'], p['depth1'], "
+            "p['min_depth'], p['K0'], p['K1'], o, c)\nexcept ValueError as e:\n    print('REFUSED', e)\n")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "REFUSED" in r.stdout and var in r.stdout, r.stdout
