@@ -103,6 +103,13 @@ def _oracle_pair_run(job):
     return st.num_hypotheses, time.perf_counter() - t0
 
 
+# the CPU baseline's build (oracle/Makefile): the reference's -O3 without -ffast-math (in a
+# shared object it flips FTZ/DAZ process-wide and assumes away the residuals' DBL_MAX / NaN
+# sentinels, CMakeLists.txt:14 has -O3 -ffast-math -fno-associative-math); baseline x86-64,
+# so -ffp-contract=fast emits no FMA
+ORACLE_FLAGS = "g++ -O3 -std=c++17 -fPIC -ffp-contract=fast -fno-math-errno (x86-64 baseline ISA)"
+
+
 def cpu_baseline(wl, pair, budget_s=15.0, procs=0):
     """Scalar CPU oracle (kind "port", compiled like the reference: -O3, FMA contraction)
     on a bounded iteration count of the workload: (1) one thread on the bench's own pair,
@@ -143,6 +150,7 @@ def cpu_baseline(wl, pair, budget_s=15.0, procs=0):
             "sample": f"{p} processes (one per physical core of the host's CPU share), each the oracle on its own "
                       f"pair of the workload for {it} iterations; {hyps} hypotheses over the slowest process's "
                       f"{inner:.1f} s ({wall:.1f} s with process start-up)",
+            "iterations": it, "workload_iterations": wl["iterations"], "compile_flags": ORACLE_FLAGS,
             "single_thread": single, "host": host}
 
 
@@ -408,7 +416,7 @@ def cpu_baseline_pairs(wl, seeds, budget_s, procs=0):
     return {"value": rate, "unit": "pairs/s", "cores": p, "kind": "port",
             "sample": f"{p} processes (one per physical core of the host's CPU share) over disjoint pairs of the "
                       f"set, {done} pairs in {budget_s / 2:.1f} s each; value = sum of per-process rates",
-            "single_thread": single, "host": host}
+            "compile_flags": ORACLE_FLAGS, "single_thread": single, "host": host}
 
 
 RECORD_FIELDS = (["seed"] + [f"R{i}{j}" for i in range(3) for j in range(3)] + ["t0", "t1", "t2", "scale", "offset0",

@@ -48,12 +48,14 @@ MP_HD void matvec3(const double *A, const double *v, double *o) {
 }
 
 // PoseLib check_cheirality (src/solver.cpp:1188-1206); x1, x2 unit vectors
+// (no FMA contraction: the oracle's check_cheirality to the bit)
 MP_HD bool check_cheirality(const double *R, const double *t, const double *x1, const double *x2, double min_depth) {
+#pragma clang fp contract(off)
     double Rx1[3];
-    matvec3(R, x1, Rx1);
-    const double a = -dot3(Rx1, x2);
-    const double b1 = -dot3(Rx1, t);
-    const double b2 = dot3(x2, t);
+    matvec3_x(R, x1, Rx1);
+    const double a = -dot3_x(Rx1, x2);
+    const double b1 = -dot3_x(Rx1, t);
+    const double b2 = dot3_x(x2, t);
     const double l1 = b1 - a * b2;
     const double l2 = -a * b1 + b2;
     min_depth = min_depth * (1 - a * a);
@@ -460,6 +462,7 @@ MP_HD void horn_rotation(const double (&M)[3][3], double *R) {
 // Right singular vector of the smallest singular value of a 4x4 matrix
 // (one-sided Jacobi), used by DLT triangulation (src/utils.h:24-38).
 MP_HD void smallest_right_sv4(const double (&A0)[4][4], double *v) {
+#pragma clang fp contract(off)
     double A[4][4], V[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -522,7 +525,8 @@ MP_HD void smallest_right_sv4(const double (&A0)[4][4], double *v) {
 }
 
 // The same vector for the DLT triangulation of the depth fits (the chosen pose: A of
-// rank 3 up to noise) without the Jacobi sweeps: Householder QR of A (A^T A = R^T R,
+// rank 3 up to noise) without the Jacobi sweeps -- round 6: without FMA contraction,
+// the oracle's dlt_null4 (oracle/src/pt.cpp) to the bit, fallback included: Householder QR of A (A^T A = R^T R,
 // backward stable), then inverse iteration on R^T R by triangular solves, starting
 // from R^-1 e4 -- for a rank-3 A that start is already the null vector (R[3][3] ~ 0),
 // and each step multiplies the error by (s4 / s3)^2.  The iteration stops once two
@@ -535,6 +539,7 @@ MP_HD void smallest_right_sv4(const double (&A0)[4][4], double *v) {
 // eps |R| (inverse iteration on a singular matrix; the DLT matrices have A[0][0] =
 // -f != 0, so R != 0).
 template <int NIT = 16> MP_HD void dlt_null4(const double (&A)[4][4], double *v) {
+#pragma clang fp contract(off)
     double R[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)

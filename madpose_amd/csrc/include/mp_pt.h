@@ -27,12 +27,13 @@ namespace mp {
 template <int NP, class All, class Emit>
 MP_HD int motion_from_essential_r(const double *E, const double (&x1)[NP][3], const double (&x2)[NP][3],
                                   const bool *use, int cap, All &&all_ok, Emit &&emit) {
+#pragma clang fp contract(off)
     const double c0[3] = {E[0], E[3], E[6]}, c1[3] = {E[1], E[4], E[7]}, c2[3] = {E[2], E[5], E[8]};
     double u12[3], u13[3], u23[3];
-    cross3(c0, c1, u12);
-    cross3(c0, c2, u13);
-    cross3(c1, c2, u23);
-    const double n12 = dot3(u12, u12), n13 = dot3(u13, u13), n23 = dot3(u23, u23);
+    cross3_x(c0, c1, u12);
+    cross3_x(c0, c2, u13);
+    cross3_x(c1, c2, u23);
+    const double n12 = dot3_x(u12, u12), n13 = dot3_x(u13, u13), n23 = dot3_x(u23, u23);
     double ec[3], uu[3], nn;
     const bool use12 = (n12 > n13) && (n12 > n23);
     const bool use13 = !(n12 > n13) && (n13 > n23);
@@ -43,13 +44,13 @@ MP_HD int motion_from_essential_r(const double *E, const double (&x1)[NP][3], co
     }
     nn = use12 ? n12 : (use13 ? n13 : n23);
     double U1[3], U2[3], U0[3], tmp[3];
-    const double en = sqrt(dot3(ec, ec)), un = sqrt(nn);
+    const double en = sqrt(dot3_x(ec, ec)), un = sqrt(nn);
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         U1[r] = ec[r] / en;
         U2[r] = uu[r] / un;
     }
-    cross3(U2, U1, tmp);
+    cross3_x(U2, U1, tmp);
 #pragma unroll
     for (int r = 0; r < 3; ++r) U0[r] = -tmp[r];
     double V0[3], V1[3], V2[3];
@@ -58,16 +59,16 @@ MP_HD int motion_from_essential_r(const double *E, const double (&x1)[NP][3], co
         V0[j] = U1[0] * E[j] + U1[1] * E[3 + j] + U1[2] * E[6 + j];
         V1[j] = -(U0[0] * E[j] + U0[1] * E[3 + j] + U0[2] * E[6 + j]);
     }
-    const double n0 = sqrt(dot3(V0, V0));
+    const double n0 = sqrt(dot3_x(V0, V0));
 #pragma unroll
     for (int j = 0; j < 3; ++j) V0[j] /= n0;
-    const double d = dot3(V0, V1);
+    const double d = dot3_x(V0, V1);
 #pragma unroll
     for (int j = 0; j < 3; ++j) V1[j] -= d * V0[j];
-    const double n1 = sqrt(dot3(V1, V1));
+    const double n1 = sqrt(dot3_x(V1, V1));
 #pragma unroll
     for (int j = 0; j < 3; ++j) V1[j] /= n1;
-    cross3(V0, V1, V2);
+    cross3_x(V0, V1, V2);
     int added = 0;
     for (int c = 0; c < 4; ++c) {
         // signs of the candidates (c: R sign, t sign) = (+,+), (+,-), (-,-), (-,+)
@@ -506,9 +507,15 @@ MP_HD int relpose_5pt(const double (&x1)[5][3], const double (&x2)[5][3], Model 
     return nout;
 }
 
-// DLT triangulation (src/utils.h:24-38) with P0 = diag(fa,fa,1)[I|0], P1 = diag(fb,fb,1)[R|t]
+// DLT triangulation (src/utils.h:24-38) with P0 = diag(fa,fa,1)[I|0], P1 = diag(fb,fb,1)[R|t],
+// the null vector by Householder QR + inverse iteration (dlt_null4), no FMA contraction --
+// the oracle's triangulate_point_qr (oracle/src/pt.cpp) to the bit.  (The reference takes
+// it from Eigen's JacobiSVD, src/utils.h:34; a bitwise restatement of that on the device
+// made the calibrated tail 19 -> 79 us per launch, +0.9 ms of GPU solve per pair,
+// profiles/r06/exact1 -- the two agree to ~1e-12, and Eigen is absent here either way.)
 MP_HD void triangulate(const double *R, const double *t, double fa, double fb, const double *p0, const double *p1,
                        double *X) {
+#pragma clang fp contract(off)
     double P1[3][4];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -539,6 +546,7 @@ MP_HD void triangulate(const double *R, const double *t, double fa, double fb, c
 // lane holds one point).
 template <int K, class Sum>
 MP_HD void ls_affine(const double *d, const double *z, const bool *use, double n, Sum &&sum, double *a, double *b) {
+#pragma clang fp contract(off)
     double sdd = 0, sd = 0, sz = 0, sdz = 0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
@@ -565,6 +573,7 @@ template <int K, class Sum>
 MP_HD bool point_model_tail_r(const double (&p0)[K][2], const double (&p1)[K][2], const double *dd0, const double *dd1,
                               const bool *use, double n, double fa, double fb, bool use_shift,
                               bool min_depth_constraint, const double *min_depth, Model &m, Sum &&sum) {
+#pragma clang fp contract(off)
     double X[K][3], z[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) triangulate(m.R, m.t, fa, fb, p0[j], p1[j], X[j]);

@@ -34,6 +34,18 @@ __device__ inline int gsum8(int v) {
     return v + dpp_i<dpp::kHalfMirror>(v);
 }
 
+// the sum over the 8-lane group in lane order, (((0 + v0) + v1) + ..) + v7, in every lane:
+// the oracle's sequential sums over the sample's points (lane j holds point j)
+__device__ inline double gsum8_ordered(double v) {
+    const bool hi = (threadIdx.x & 8) != 0;
+    double s = 0.0;
+    static_for<kTail>([&](auto j) {
+        const double a = gbcast<decltype(j)::value>(v), b = gbcast<decltype(j)::value + 8>(v);
+        s += hi ? b : a;
+    });
+    return s;
+}
+
 // group g of the launch = root k of sample idx, root-major as pt_tail_kernel.
 // G = 8: one 8-lane group per (root, sample), every lane tests its point under the
 // four recoverPose candidates in turn.  G = 32: four 8-lane subgroups per (root,
@@ -109,10 +121,14 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
 // Calibrated tail (src/hybrid_pose_estimator.cpp:134-182) with one 8-lane group per
 // (root, sample), lane j < 5 holding point j: the cheirality tests of
 // motion_from_essential (AND over the group), then for each of the at most two poses
-// the triangulation and depth fit with the group's sums.
+// the triangulation (Eigen's JacobiSVD, eigen_svd4_null) and depth fit with the group's
+// sums taken in point order -- round 6: the oracle's point_model_tail operation for
+// operation, so a calibrated 5pt model is the oracle's to the bit
+// (tests/test_pt_roots_gpu.py::test_5pt_models_are_the_oracles_to_the_bit).
 __global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                             const double *cand, const int *ncand, const int *samples,
                                                             Model *slots, int *valid) {
+#pragma clang fp contract(off)
     if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     constexpr int K = 5, kRoots = 10, kPoses = 2;
     const int lane = threadIdx.x % kTail;
@@ -122,13 +138,14 @@ __global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairCons
     const int *s = samples + (size_t)list[idx] * kSampleStride;
     const bool has = lane < K;
     const int i = s[has ? lane : K - 1];
-    // one point of load_cal_sample: calibrated ray, unit bearings, depth priors
+    // one point of the oracle's minimal_solver: calibrated ray c = K^-1 x, unit bearing
+    // c / |c|, depth priors (no FMA contraction: the oracle's values to the bit)
     const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
     double a[3], c[3];
-    matvec3(C.K0i, xa, a);
-    matvec3(C.K1i, xb, c);
-    const double na = 1.0 / sqrt(dot3(a, a)), nc = 1.0 / sqrt(dot3(c, c));
-    const double b1[1][3] = {{a[0] * na, a[1] * na, a[2] * na}}, b2[1][3] = {{c[0] * nc, c[1] * nc, c[2] * nc}};
+    matvec3_x(C.K0i, xa, a);
+    matvec3_x(C.K1i, xb, c);
+    const double na = sqrt(dot3_x(a, a)), nc = sqrt(dot3_x(c, c));
+    const double b1[1][3] = {{a[0] / na, a[1] / na, a[2] / na}}, b2[1][3] = {{c[0] / nc, c[1] / nc, c[2] / nc}};
     const double p0[1][2] = {{a[0], a[1]}}, p1[1][2] = {{c[0], c[1]}};
     const double dd0[1] = {D.d0[i]}, dd1[1] = {D.d1[i]};
     const bool use[1] = {has};
@@ -148,7 +165,7 @@ __global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairCons
         if (j < np) { // (uniform over the group)
             m = poses[j];
             ok = point_model_tail_r<1>(p0, p1, dd0, dd1, use, (double)K, 1.0, 1.0, shift, mdc, C.min_depth, m,
-                                       [](double v) { return gsum8(v); });
+                                       [](double v) { return gsum8_ordered(v); });
         }
         if (lane == 0) {
             const size_t q = (size_t)idx * kPtSlotStride + kPoses * k + j;

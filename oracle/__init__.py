@@ -182,6 +182,14 @@ def solve_cubic_real(c2, c1, c0):
     return out[:n].copy()
 
 
+def eigen_svd3(A):
+    """Eigen JacobiSVD<MatrixXd>(A, ComputeFullU | ComputeFullV) restatement (la.cpp): U, V."""
+    A = _c(np.asarray(A).reshape(3, 3))
+    U, V = np.zeros((3, 3)), np.zeros((3, 3))
+    lib().oracle_eigen_svd3(_dp(A), _dp(U), _dp(V))
+    return U, V
+
+
 def sixpt_roots(b1, b2):
     """Root stage of the 6pt restatement: positive real u = f^2 (deflated companion)."""
     out = np.zeros(32)

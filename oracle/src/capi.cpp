@@ -11,6 +11,7 @@
 #include <random>
 #include <vector>
 
+#include "la.h"
 #include "oracle.h"
 
 extern "C" {
@@ -161,6 +162,12 @@ int oracle_relpose_7pt_svd(const double *x1, const double *x2, double *F_out, in
     for (int i = 0; i < n; ++i)
         for (int e = 0; e < 9; ++e) F_out[9 * i + e] = sols[i][e];
     return (int)sols.size();
+}
+
+// Eigen JacobiSVD restatement of a 3 x 3 matrix (la.cpp eigen_jacobi_svd3): U, V row-major
+int oracle_eigen_svd3(const double *A, double *U, double *V) {
+    oracle::eigen_jacobi_svd3(A, U, V);
+    return 0;
 }
 
 int oracle_solve_cubic_real(double c2, double c1, double c0, double *roots) {

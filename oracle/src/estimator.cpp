@@ -249,7 +249,7 @@ bool point_model_tail(const Problem &P, const std::vector<int> &idx, const doubl
             p1[0] = P.x1[3 * i];
             p1[1] = P.x1[3 * i + 1];
         }
-        triangulate_point(P0, P1, p0, p1, &X[3 * j]);
+        triangulate_point_qr(P0, P1, p0, p1, &X[3 * j]);
         dd0[j] = P.d0[i];
         dd1[j] = P.d1[i];
     }

@@ -236,6 +236,155 @@ std::vector<Model> relpose_5pt_action(const double *x1, const double *x2) {
     return out;
 }
 
+namespace {
+// Right singular vector of the smallest singular value of a 4 x 4 matrix by one-sided
+// (Hestenes) cyclic Jacobi: at most 20 sweeps over (p, q), p < q, a rotation where the
+// columns' relative correlation exceeds 1e-16, stop when none exceeds 1e-15; the column
+// of the smallest norm (first minimum), picked by one-hot weights
+void smallest_right_sv4(const double A0[4][4], double v[4]) {
+    double A[4][4], V[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            A[i][j] = A0[i][j];
+            V[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    for (int sweep = 0; sweep < 20; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < 3; ++p)
+            for (int q = p + 1; q < 4; ++q) {
+                double al = 0, be = 0, ga = 0;
+                for (int i = 0; i < 4; ++i) {
+                    al += A[i][p] * A[i][p];
+                    be += A[i][q] * A[i][q];
+                    ga += A[i][p] * A[i][q];
+                }
+                const double rel = (ga != 0.0) ? std::fabs(ga) / std::sqrt(al * be) : 0.0;
+                off = std::fmax(off, rel);
+                if (rel > 1e-16) {
+                    const double zeta = (be - al) / (2.0 * ga);
+                    const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+                    const double c = 1.0 / std::sqrt(1.0 + t * t), s = c * t;
+                    for (int i = 0; i < 4; ++i) {
+                        const double ap = A[i][p], aq = A[i][q];
+                        A[i][p] = c * ap - s * aq;
+                        A[i][q] = s * ap + c * aq;
+                        const double vp = V[i][p], vq = V[i][q];
+                        V[i][p] = c * vp - s * vq;
+                        V[i][q] = s * vp + c * vq;
+                    }
+                }
+            }
+        if (!(off > 1e-15)) break;
+    }
+    double nrm[4];
+    for (int j = 0; j < 4; ++j) nrm[j] = A[0][j] * A[0][j] + A[1][j] * A[1][j] + A[2][j] * A[2][j] + A[3][j] * A[3][j];
+    int k = 0;
+    double best = nrm[0];
+    for (int j = 1; j < 4; ++j)
+        if (nrm[j] < best) {
+            best = nrm[j];
+            k = j;
+        }
+    double w[4];
+    for (int j = 0; j < 4; ++j) w[j] = (k == j) ? 1.0 : 0.0;
+    for (int i = 0; i < 4; ++i) v[i] = w[0] * V[i][0] + w[1] * V[i][1] + w[2] * V[i][2] + w[3] * V[i][3];
+}
+
+// The null vector of the 4 x 4 DLT matrix: Householder QR (A^T A = R^T R), then inverse
+// iteration on R^T R by triangular solves from R^-1 e4 until two normalised iterates
+// agree to 1e-14 (at most 16 steps), else the Jacobi sweeps above.  The device's
+// dlt_null4 (madpose_amd/csrc/include/mp_math.h) performs these operations in this
+// order without FMA contraction.
+void dlt_null4(const double A[4][4], double v[4]) {
+    double R[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) R[i][j] = A[i][j];
+    for (int k = 0; k < 3; ++k) {
+        double nn = 0.0;
+        for (int i = k; i < 4; ++i) nn += R[i][k] * R[i][k];
+        const double nrm = std::sqrt(nn);
+        const double alpha = R[k][k] >= 0.0 ? -nrm : nrm;
+        double h[4];
+        for (int i = 0; i < 4; ++i) h[i] = i < k ? 0.0 : R[i][k];
+        h[k] -= alpha;
+        const double hh = nn - 2.0 * alpha * R[k][k] + alpha * alpha;
+        const double f2 = hh > 0.0 ? 2.0 / hh : 0.0;
+        for (int j = k; j < 4; ++j) {
+            double sdot = 0.0;
+            for (int i = k; i < 4; ++i) sdot += h[i] * R[i][j];
+            const double f = sdot * f2;
+            for (int i = k; i < 4; ++i) R[i][j] -= f * h[i];
+        }
+    }
+    double big = 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = i; j < 4; ++j) big = std::fmax(big, std::fabs(R[i][j]));
+    const double floor_ = big * 2.220446049250313e-16;
+    double d[4];
+    for (int i = 0; i < 4; ++i) {
+        const double r = R[i][i];
+        d[i] = 1.0 / (std::fabs(r) > floor_ ? r : (r < 0.0 ? -floor_ : floor_));
+    }
+    double x[4];
+    x[3] = d[3];
+    x[2] = -(R[2][3] * x[3]) * d[2];
+    x[1] = -(R[1][2] * x[2] + R[1][3] * x[3]) * d[1];
+    x[0] = -(R[0][1] * x[1] + R[0][2] * x[2] + R[0][3] * x[3]) * d[0];
+    bool conv = false;
+    for (int it = 0; it < 16 && !conv; ++it) {
+        double mx = 0.0;
+        for (int i = 0; i < 4; ++i) mx = std::fmax(mx, std::fabs(x[i]));
+        const double sc = 1.0 / mx;
+        for (int i = 0; i < 4; ++i) x[i] *= sc;
+        double y[4], z[4];
+        y[0] = x[0] * d[0];
+        y[1] = (x[1] - R[0][1] * y[0]) * d[1];
+        y[2] = (x[2] - R[0][2] * y[0] - R[1][2] * y[1]) * d[2];
+        y[3] = (x[3] - R[0][3] * y[0] - R[1][3] * y[1] - R[2][3] * y[2]) * d[3];
+        z[3] = y[3] * d[3];
+        z[2] = (y[2] - R[2][3] * z[3]) * d[2];
+        z[1] = (y[1] - R[1][2] * z[2] - R[1][3] * z[3]) * d[1];
+        z[0] = (y[0] - R[0][1] * z[1] - R[0][2] * z[2] - R[0][3] * z[3]) * d[0];
+        double mz = 0.0;
+        for (int i = 0; i < 4; ++i) mz = std::fmax(mz, std::fabs(z[i]));
+        const double rz = 1.0 / mz;
+        double diff = 0.0;
+        for (int i = 0; i < 4; ++i) {
+            diff = std::fmax(diff, std::fabs(z[i] * rz - x[i]));
+            x[i] = z[i];
+        }
+        conv = diff < 1e-14;
+    }
+    if (!conv) {
+        smallest_right_sv4(A, v);
+        return;
+    }
+    const double n = 1.0 / std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+    for (int i = 0; i < 4; ++i) v[i] = x[i] * n;
+}
+} // namespace
+
+// COLMAP TriangulatePoint as the reference ships it (src/utils.h:24-38): the DLT matrix,
+// its null vector dehomogenised.  The reference takes the null vector from Eigen's
+// JacobiSVD (src/utils.h:34); this restatement takes it by Householder QR + inverse
+// iteration (dlt_null4 above; the two agree to ~1e-12 -- Eigen is not vendored, so the
+// reference's own bits are unpinned either way), because the device performs exactly
+// this (a bitwise device restatement of Eigen's two-sided sweeps cost 19 -> 79 us per
+// calibrated tail launch, profiles/r06/exact1).  The point solvers' depth tails.
+void triangulate_point_qr(const double P0[12], const double P1[12], const double p0[2], const double p1[2],
+                          double X[3]) {
+    double A[4][4], v[4];
+    for (int j = 0; j < 4; ++j) {
+        A[0][j] = p0[0] * P0[8 + j] - P0[j];
+        A[1][j] = p0[1] * P0[8 + j] - P0[4 + j];
+        A[2][j] = p1[0] * P1[8 + j] - P1[j];
+        A[3][j] = p1[1] * P1[8 + j] - P1[4 + j];
+    }
+    dlt_null4(A, v);
+    for (int c = 0; c < 3; ++c) X[c] = v[c] / v[3];
+}
+
+// the same with the one-sided Jacobi SVD (la.cpp jacobi_svd): recover_pose's tests
 void triangulate_point(const double P0[12], const double P1[12], const double p0[2], const double p1[2], double X[3]) {
     Mat A(4, 4);
     for (int j = 0; j < 4; ++j) {

@@ -245,6 +245,11 @@ struct Engine {
         const char *replay_path = std::getenv("ORACLE_MODEL_REPLAY");
         FILE *replay = replay_path ? std::fopen(replay_path, "rb") : nullptr;
         Closer closer2{replay};
+        // ORACLE_MODEL_DUMP=<file>: this loop's own models of every iteration in the
+        // engine's MADPOSE_MODEL_DUMP format (tests/test_ties_gpu.py compares the two)
+        const char *mdump_path = std::getenv("ORACLE_MODEL_DUMP");
+        FILE *mdump = mdump_path ? std::fopen(mdump_path, "wb") : nullptr;
+        Closer closer3{mdump};
 
         for (S->num_iterations_total = 0; S->num_iterations_total < max_total; ++S->num_iterations_total) {
             const uint32_t it = S->num_iterations_total;
@@ -282,6 +287,11 @@ struct Engine {
                 nm = hdr[1];
             }
             S->num_hypotheses += nm;
+            if (mdump) {
+                const int32_t hdr[2] = {(int32_t)it, (int32_t)nm};
+                std::fwrite(hdr, sizeof(hdr), 1, mdump);
+                if (nm > 0) std::fwrite(models.data(), sizeof(Model), (size_t)nm, mdump);
+            }
             if (dump) {
                 std::fprintf(dump, "%u %d %d", it, st, nm);
                 for (int i : sample[st == 0 ? 0 : 2]) std::fprintf(dump, " %d", i);

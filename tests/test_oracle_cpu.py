@@ -121,3 +121,92 @@ def test_oracle_md_pose_matches_reference_find_transform(variant, name):
             assert abs(p["offset1"] - r[14]) <= tol * (1 + abs(r[14]))
             checked += 1
     assert checked > 200
+
+
+# ---- round 6: the point solvers' restatements (oracle/src/pt_poselib.cpp) ----
+import sys  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pt_samples as ps  # noqa: E402
+
+
+def test_oracle_5pt_poselib_restatement_agrees_with_action_matrix_form():
+    """The estimator's 5pt restatement (Nister + PoseLib's Sturm bisection) against the
+    independent action-matrix form kept from round 2, on benign samples: equal pose
+    counts, and 97 % of the poses within 1e-6 (PoseLib's Newton stage is unguarded and
+    stops at |f| < 1e-10 on the monic polynomial: the roots of a close pair come out less
+    accurate, and now and then Newton leaves the isolating interval for the pair's other
+    root -- PoseLib's behaviour, restated)."""
+    rng = np.random.default_rng(17)
+    p0, p1 = ps.random_samples(rng, 600, 5)
+    p0, p1 = p0[::2], p1[::2]  # the noise-free half
+    b0, b1 = ps.bearings(p0), ps.bearings(p1)
+    close = 0
+    for s in range(len(b0)):
+        new = oracle.relpose_5pt(b0[s], b1[s])
+        old = oracle.relpose_5pt_action(b0[s], b1[s])
+        assert len(new) == len(old), s
+        for m in new:
+            d = min(np.abs(m["R"] - o["R"]).max() + np.abs(m["t"] - o["t"]).max() for o in old)
+            close += d < 1e-6
+    assert close >= 0.97 * sum(len(oracle.relpose_5pt(b0[s], b1[s])) for s in range(len(b0)))
+
+
+def test_oracle_5pt_root_stage_counts_on_hard_samples():
+    """The real-root count of det B(z) is even for a degree-10 polynomial with simple
+    roots; the E list has one matrix per root unless (x, y) is not finite -- on the hard
+    kinds the restatement returns no more than ten and keeps its roots ascending."""
+    kinds = ps.all_kinds(5, 150, 5, lambda a, b: len(oracle.relpose_5pt_E(ps.bearings(a), ps.bearings(b))[1]))
+    for kind, (p0, p1) in kinds.items():
+        for s in range(len(p0)):
+            E, roots = oracle.relpose_5pt_E(ps.bearings(p0[s]), ps.bearings(p1[s]))
+            assert len(E) <= len(roots) <= 10, (kind, s)
+            assert np.all(np.diff(roots) > 0), (kind, s, roots)
+
+
+def test_oracle_7pt_restatement_agrees_with_svd_form():
+    rng = np.random.default_rng(19)
+    p0, p1 = ps.random_samples(rng, 400, 7)
+    b0, b1 = ps.bearings(p0), ps.bearings(p1)
+    for s in range(len(b0)):
+        F, G = oracle.relpose_7pt(b0[s], b1[s]), oracle.relpose_7pt_svd(b0[s], b1[s])
+        assert len(F) == len(G), s
+        for f in F:
+            assert min(min(np.abs(f - g).max(), np.abs(f + g).max()) for g in G) < 1e-6, s
+
+
+@pytest.mark.parametrize("roots", [(1.0, 2.0, 3.0), (-5.0, 0.25, 40.0), (0.5, 0.5 + 1e-3, -2.0)])
+def test_oracle_solve_cubic_real_three_roots(roots):
+    r1, r2, r3 = roots
+    c2, c1, c0 = -(r1 + r2 + r3), r1 * r2 + r1 * r3 + r2 * r3, -r1 * r2 * r3
+    got = np.sort(oracle.solve_cubic_real(c2, c1, c0))
+    assert len(got) == 3
+    assert np.allclose(got, np.sort(roots), atol=1e-6)
+
+
+def test_oracle_solve_cubic_real_one_root():
+    # (x - 2)(x^2 + 1)
+    got = oracle.solve_cubic_real(-2.0, 1.0, -2.0)
+    assert len(got) == 1 and abs(got[0] - 2.0) < 1e-12
+
+
+@pytest.mark.parametrize("rank", [3, 2, 1])
+def test_oracle_eigen_svd3_is_an_svd(rank):
+    """the Eigen JacobiSVD restatement (la.cpp eigen_jacobi_svd3, which the
+    device's mdx::svd3 follows bit for bit) checked on its own -- U and V orthogonal,
+    U diag(s) V^T reconstructs A with s = diag(U^T A V) >= 0 descending -- on full-rank,
+    rank-2 and rank-1 inputs.  Parity with Eigen itself stays unpinned (not vendored)."""
+    rng = np.random.default_rng(rank)
+    for _ in range(200):
+        A = sum(np.outer(rng.normal(size=3), rng.normal(size=3)) * 10.0 ** rng.uniform(-3, 3) for _ in range(rank))
+        U, V = oracle.eigen_svd3(A)
+        assert np.abs(U.T @ U - np.eye(3)).max() < 1e-12
+        assert np.abs(V.T @ V - np.eye(3)).max() < 1e-12
+        S = U.T @ A @ V
+        s = np.diag(S)
+        scale = np.abs(A).max()
+        assert np.abs(S - np.diag(s)).max() <= 1e-12 * scale
+        assert np.all(s >= -1e-12 * scale) and np.all(np.diff(s) <= 1e-12 * scale)
+        assert np.abs(U @ np.diag(s) @ V.T - A).max() <= 1e-12 * scale
+        if rank < 3:
+            assert abs(s[2]) <= 1e-12 * scale
