@@ -78,49 +78,56 @@ __device__ inline void fivept_template_row(const double (*N)[9], int r, double (
              std::integral_constant<int, 4>(), std::integral_constant<int, 6>(), 1.0);
     } else if (r < 10) {
         // (2 E E^T E - tr(E E^T) E)_ab = sum_k 2 (E E^T)_ak E_kb - tr E_ab; only row a
-        // of E E^T is formed (the same products, in the same order, as the full one)
+        // of E E^T is formed (the same products, in the same order, as the full one).
+        // Operands come from LDS when used (a is the lane's row: a runtime index) and the
+        // trace is summed as soon as its diagonal terms exist -- the same operations in
+        // the same order as the oracle's template_row, with fewer registers live.
         const int a = (r - 1) / 3, b = (r - 1) - 3 * ((r - 1) / 3);
-        Lin Ea[3], Ek[3], Eab;
-        static_for<4>([&](auto i) {
+        auto lin_rt = [&](int e) {
+            Lin l;
+            static_for<4>([&](auto q) { l.c[q] = N[q][e]; });
+            return l;
+        };
+        auto diag = [&](auto d, Quad &D) {
+            static_for<10>([&](auto i) { D.c[i] = 0.0; });
             static_for<3>([&](auto m) {
-                Ea[m].c[i] = N[i][3 * a + m];
-                Ek[m].c[i] = N[i][3 * m + b];
+                Quad t;
+                const Lin l = lin(std::integral_constant<int, 3 * decltype(d)::value + m>());
+                lin_mul(l, l, t);
+                static_for<10>([&](auto i) { D.c[i] += t.c[i]; });
             });
-            Eab.c[i] = N[i][3 * a + b];
-        });
+        };
         Quad tr;
         {
-            Quad Dg[3];
-            static_for<3>([&](auto d) {
-                static_for<10>([&](auto i) { Dg[d].c[i] = 0.0; });
-                static_for<3>([&](auto m) {
-                    Quad t;
-                    const Lin l = lin(std::integral_constant<int, 3 * d + m>());
-                    lin_mul(l, l, t);
-                    static_for<10>([&](auto i) { Dg[d].c[i] += t.c[i]; });
-                });
-            });
-            static_for<10>([&](auto i) { tr.c[i] = Dg[0].c[i] + Dg[1].c[i] + Dg[2].c[i]; });
+            Quad D0, D1;
+            diag(std::integral_constant<int, 0>(), D0);
+            diag(std::integral_constant<int, 1>(), D1);
+            static_for<10>([&](auto i) { tr.c[i] = D0.c[i] + D1.c[i]; });
+        }
+        {
+            Quad D2;
+            diag(std::integral_constant<int, 2>(), D2);
+            static_for<10>([&](auto i) { tr.c[i] += D2.c[i]; });
         }
         static_for<3>([&](auto k) {
             Quad Q;
             static_for<10>([&](auto i) { Q.c[i] = 0.0; });
             static_for<3>([&](auto m) {
-                // operands in the order of (E E^T)_{min(a,k) max(a,k)}: with FMA
-                // contraction lin_mul is not symmetric in its arguments
+                // operands in the order of (E E^T)_{min(a,k) max(a,k)}
                 const Lin Lk = lin(std::integral_constant<int, 3 * k + m>());
+                const Lin La = lin_rt(3 * a + m);
                 Lin u, v;
                 static_for<4>([&](auto i) {
-                    u.c[i] = k < a ? Lk.c[i] : Ea[m].c[i];
-                    v.c[i] = k < a ? Ea[m].c[i] : Lk.c[i];
+                    u.c[i] = k < a ? Lk.c[i] : La.c[i];
+                    v.c[i] = k < a ? La.c[i] : Lk.c[i];
                 });
                 Quad t;
                 lin_mul(u, v, t);
                 static_for<10>([&](auto i) { Q.c[i] += t.c[i]; });
             });
-            quad_lin_acc(Q, Ek[k], 2.0, acc);
+            quad_lin_acc(Q, lin_rt(3 * k + b), 2.0, acc);
         });
-        quad_lin_acc(tr, Eab, -1.0, acc);
+        quad_lin_acc(tr, lin_rt(3 * a + b), -1.0, acc);
     }
     static_for<20>([&](auto c) { row[c] = acc.c[c]; });
 }
@@ -221,21 +228,24 @@ __device__ __forceinline__ void pt_roots5_group_core(int bid, int nlist, Load &&
         gargmax(used ? -1.0 : fabs(row[k]), r, &bv, &bi);
         ok = ok && (bv > 0.0);
         const bool piv_lane = r == bi;
+        // Columns c <= k are never read again (the later pivot searches read columns > k,
+        // the reduced rows columns 10..19), so their updates -- which the oracle performs
+        // -- are skipped: every value that is read is the oracle's
         if (piv_lane) {
 #pragma unroll
-            for (int c = 0; c < 20; ++c) sh.piv[g][c] = row[c];
+            for (int c = k; c < 20; ++c) sh.piv[g][c] = row[c];
         }
         __syncthreads();
         const double inv = 1.0 / sh.piv[g][k];
         if (piv_lane) {
 #pragma unroll
-            for (int c = 0; c < 20; ++c) row[c] *= inv;
+            for (int c = k + 1; c < 20; ++c) row[c] *= inv;
             used = true;
             logical = k;
         } else {
             const double f = row[k];
 #pragma unroll
-            for (int c = 0; c < 20; ++c) row[c] -= f * (sh.piv[g][c] * inv);
+            for (int c = k + 1; c < 20; ++c) row[c] -= f * (sh.piv[g][c] * inv);
         }
         __syncthreads();
     }
@@ -352,7 +362,9 @@ __device__ __forceinline__ void pt_roots5_group_body(int bid, const PairData &D,
     pt_roots5_group_core(bid, nlist, load, cand, ncand, cand_stride);
 }
 
-__global__ void __launch_bounds__(64) pt_roots5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+// (three waves per SIMD asked of the compiler: at 186 VGPRs it kept two)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+pt_roots5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                              const int *samples, double *cand, int *ncand,
                                                              int cand_stride) {
     pt_roots5_group_body(blockIdx.x, D, C, list, nlist, samples, cand, ncand, cand_stride);

@@ -30,6 +30,8 @@ namespace {
 constexpr int kBisectMaxDepth = 300;
 
 template <int N> struct GroupBisect {
+    double fvec[2 * N + 1];        // monic polynomial and monic derivative / N
+    double svec[3 * N];            // the Sturm chain's quotients (build_sturm_seq)
     double a[2][kGrp], b[2][kGrp]; // pending intervals of the level (double-buffered)
     int sa[2][kGrp], sb[2][kGrp];
     int npend[2];
@@ -42,7 +44,8 @@ template <int N> struct GroupBisect {
 // quotients and normalisers of the chain (svec: 3 N doubles).  Compile-time indices
 // only; the three rotating buffers of PoseLib's pointer juggling are selected
 // statically.
-template <int N> __device__ inline void bisect_build_chain(const double (&fvec)[2 * N + 1], double (&svec)[3 * N]) {
+template <int N>
+__device__ inline void bisect_build_chain(const double (&fvec)[2 * N + 1], double (&svec)[3 * N], bool writer) {
 #pragma clang fp contract(off)
     double f[3][N + 1];
     static_for<N + 1>([&](auto j) {
@@ -63,14 +66,18 @@ template <int N> __device__ inline void bisect_build_chain(const double (&fvec)[
         const double c = -fabs(f[i3][N - 2 - i]);
         const double ci = 1.0 / c;
         static_for<N - 1 - i>([&](auto j) { f[i3][j] = f[i3][j] * ci; });
-        svec[3 * i] = q0;
-        svec[3 * i + 1] = q1;
-        svec[3 * i + 2] = c;
+        if (writer) {
+            svec[3 * i] = q0;
+            svec[3 * i + 1] = q1;
+            svec[3 * i + 2] = c;
+        }
     });
     constexpr int e1 = (N - 1) % 3, e2 = N % 3; // f1, f2 after N - 1 rotations
-    svec[3 * N - 3] = f[e1][0];
-    svec[3 * N - 2] = f[e1][1];
-    svec[3 * N - 1] = f[e2][0];
+    if (writer) {
+        svec[3 * N - 3] = f[e1][0];
+        svec[3 * N - 2] = f[e1][1];
+        svec[3 * N - 1] = f[e2][0];
+    }
 }
 
 template <int N> __device__ inline double bisect_polyval(const double *f, double x) {
@@ -149,8 +156,10 @@ __device__ bool group_bisect_sturm(const double (&p)[N + 1], int r, GroupBisect<
 #pragma clang fp contract(off)
     static_assert(N <= kGrp, "one leaf per lane");
     ok = ok && p[N] != 0.0;
+    // the polynomial and the chain are the same in every lane of the group: computed
+    // redundantly, kept in LDS (written by lane 0) -- in registers they held the kernel
+    // at 186 VGPRs, two waves per SIMD
     double fvec[2 * N + 1];
-    double svec[3 * N];
     {
         static_for<N + 1>([&](auto i) { fvec[i] = p[i]; });
         const double c_inv = 1.0 / fvec[N];
@@ -161,13 +170,17 @@ __device__ bool group_bisect_sturm(const double (&p)[N + 1], int r, GroupBisect<
         // (the restatement's guard: a non-finite coefficient gives no roots)
         static_for<2 * N + 1>([&](auto i) { ok = ok && isfinite(fvec[i]); });
     }
-    bisect_build_chain<N>(fvec, svec);
     double r_max = 0.0;
     static_for<N>([&](auto i) { r_max = fmax(r_max, fabs(fvec[i])); });
     r_max = 1.0 + r_max;
     // (std::max(mx, |f_i|) keeps mx on a NaN |f_i|, fmax too: the same bound)
+    if (r == 0) static_for<2 * N + 1>([&](auto i) { S.fvec[i] = fvec[i]; });
+    bisect_build_chain<N>(fvec, S.svec, r == 0);
+    __syncthreads();
+    const double(&svec)[3 * N] = S.svec;
     const double a0 = -r_max, b0 = r_max;
     const int sa0 = bisect_signchanges<N>(svec, a0), sb0 = bisect_signchanges<N>(svec, b0);
+    __syncthreads(); // (S.npend / S.nleaf below: written by lane 0)
     if (r == 0) {
         S.npend[0] = (ok && sa0 - sb0 > 1) ? 1 : 0;
         S.nleaf = (ok && sa0 - sb0 == 1) ? 1 : 0;
@@ -259,7 +272,7 @@ __device__ bool group_bisect_sturm(const double (&p)[N + 1], int r, GroupBisect<
             S.lb[rank] = lb;
         }
         __syncthreads();
-        if (r < nleaf) found = bisect_ridders_newton<N>(fvec, S.la[r], S.lb[r], &x);
+        if (r < nleaf) found = bisect_ridders_newton<N>(S.fvec, S.la[r], S.lb[r], &x);
     }
     int nf;
     const int before = gscan(found ? 1 : 0, &nf);
