@@ -208,3 +208,43 @@ def deviation(m, ref):
     """(rotation deg, t-direction max abs) of m from a reference dict, for messages."""
     tn = lambda v: np.asarray(v) / np.linalg.norm(v)
     return float(rot_angle_deg(m.R(), ref["R"])), float(np.abs(tn(m.t()) - tn(ref["t"])).max())
+
+
+def is_local_minimum(variant, args, o, c, model, lists, norm_scale=1.0, h=1e-5, rtol=1e-6):
+    """No single-parameter perturbation lowers the LM cost by more than rtol of it: the
+    rotation about each axis by h rad, each t component, the scale, the offsets and the
+    focals by h relative (h absolute below 1).  The oracle's solutions of the kept
+    problems pass (largest decrease < 5e-7 over all configurations); its ends from far
+    starts often do not (up to 5e-3: Ceres stops there on its iteration cap or
+    tolerances).  Returns (ok, worst relative decrease)."""
+    d = oracle_model(model, variant)
+    c0 = lm_cost(variant, args, o, c, model, lists, norm_scale)
+    worst = 0.0
+
+    def trial(dd):
+        nonlocal worst
+        cm = lm_cost(variant, args, o, c, model_of(dd, variant), lists, norm_scale)
+        worst = max(worst, (c0 - cm) / max(c0, 1e-300))
+
+    for k in range(3):
+        for sgn in (1.0, -1.0):
+            a = np.zeros(3)
+            a[k] = sgn * h
+            K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+            dd = dict(d)
+            dd["R"] = np.asarray(d["R"]) @ (np.eye(3) + K + 0.5 * K @ K)
+            trial(dd)
+            dd = dict(d)
+            t = np.array(d["t"], float)
+            t[k] += sgn * h * max(1.0, abs(t[k]))
+            dd["t"] = t
+            trial(dd)
+    keys = ["scale", "offset0", "offset1"] + ([] if variant == 0 else ["focal0"] if variant == 1 else ["focal0", "focal1"])
+    for key in keys:
+        for sgn in (1.0, -1.0):
+            dd = dict(d)
+            dd[key] = d[key] + sgn * h * max(1.0, abs(d[key]))
+            if variant == 1 and key == "focal0":
+                dd["focal1"] = dd["focal0"]
+            trial(dd)
+    return worst <= rtol, worst

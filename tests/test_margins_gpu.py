@@ -55,14 +55,19 @@ def _models(p, rng, variant, k):
 
 
 @pytest.mark.parametrize("score_type", [0, 1, 2])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_sums_within_margins(variant, score_type):
+    """Variant 3 (scale-only): the calibrated geometry without offsets,
+    scored by the non-FAST matrix path with its own z < 1e-2 rule and 1/scale models."""
     rng = np.random.default_rng(300 + 3 * variant + score_type)
     p = synthetic.make_pair(300 + variant, n=1700)
-    o, c = synthetic.example_options(["calibrated", "shared_focal", "two_focal"][variant])
+    o, c = synthetic.example_options(["calibrated", "shared_focal", "two_focal", "calibrated"][variant])
     c.score_type = score_type
-    cam0, cam1 = _cams(p, variant)
-    ms = _models(p, rng, variant, 48)
+    cam0, cam1 = _cams(p, 0 if variant == 3 else variant)
+    if variant == 3:
+        ms = [api.PoseAndScale(m.R(), m.t(), m.scale) for m in _models(p, rng, 0, 48)]
+    else:
+        ms = _models(p, rng, variant, 48)
     args = (variant, p["x0"], p["x1"], p["depth0"], p["depth1"], cam0, cam1, o, c)
     dev, slots, _, bounds = api.debug_score_batch(*args, [[m] for m in ms], best=BIG, exit=False, record_skip=False)
     ref = api.score_models(*args, ms, host_lo=True)
@@ -161,6 +166,15 @@ def test_gate_correspondences_are_flagged():
         assert flags[k, i] == 1, (k, i)
     _, slots, _, _ = api.debug_score_batch(*args, [[mm] for mm in models], best=BIG, exit=False, record_skip=False)
     assert np.all(slots & UNC)
+    # scale-only (variant 3): the same z-gate correspondence of the first model
+    # -- offsets are 0 there, so t_z is rebuilt for o0 = 0 -- flags its iteration too
+    m = base[0]
+    R, t = m.R(), m.t().copy()
+    t[2] = 0.01 - _ref_z(K0i, R, t, x0[5], d0[5], 0.0)
+    so = [api.PoseAndScale(R, t, m.scale)]
+    args3 = (3, x0, x1, d0, d1, K0, K1, o, c)
+    _, slots3, _, _ = api.debug_score_batch(*args3, [so], best=BIG, exit=False, record_skip=False)
+    assert slots3[0] & UNC
 
 
 @pytest.mark.parametrize("seed", [0, 1])
