@@ -419,6 +419,9 @@ struct DeviceCtx {
     double *d_pt_cand = nullptr, *d_pt_pen = nullptr;
     int *d_pt_ncand = nullptr, *d_pt_valid = nullptr;
     Model *d_pt_slots = nullptr;
+    // the two-stage exact MD solver's per-sample state (kernels.h kMdWsStride, SoA, ld cap_b)
+    double *d_md_ws = nullptr;
+    int *d_md_nr = nullptr;
     // device resources of the LO lanes (lane 0: the estimator thread)
     SweepSlot sweep_slot[kLoLanes];
     std::unique_ptr<LoWorkers> lo_workers; // created on first parallel LO
@@ -437,7 +440,7 @@ struct DeviceCtx {
         hipSetDevice(device);
         for (void *p : {(void *)d_pair, (void *)bb[0].d_samples, (void *)bb[1].d_samples, (void *)d_recword, (void *)d_rec1, (void *)d_err,
                         (void *)d_score1, (void *)d_pt_cand, (void *)d_pt_pen, (void *)d_pt_ncand, (void *)d_pt_valid,
-                        (void *)d_pt_slots})
+                        (void *)d_pt_slots, (void *)d_md_ws, (void *)d_md_nr})
             if (p) hipFree(p);
         for (void *p : {(void *)h_samples, (void *)h_err, (void *)h_score1, (void *)h_rec1, (void *)h_model1})
             if (p) hipHostFree(p);
@@ -462,6 +465,8 @@ struct DeviceCtx {
         d_pt_cand = d_pt_pen = nullptr;
         d_pt_ncand = d_pt_valid = nullptr;
         d_pt_slots = nullptr;
+        d_md_ws = nullptr;
+        d_md_nr = nullptr;
         h_samples = nullptr;
         h_err = h_score1 = nullptr;
         h_rec1 = nullptr;
@@ -509,6 +514,8 @@ struct DeviceCtx {
         MP_HIP(hipMalloc(&d_pt_ncand, sizeof(int) * (size_t)bb_));
         MP_HIP(hipMalloc(&d_pt_valid, sizeof(int) * (size_t)bb_ * kPtSlotStride));
         MP_HIP(hipMalloc(&d_pt_slots, sizeof(Model) * (size_t)bb_ * kPtSlotStride));
+        MP_HIP(hipMalloc(&d_md_ws, sizeof(double) * (size_t)bb_ * kMdWsStride));
+        MP_HIP(hipMalloc(&d_md_nr, sizeof(int) * (size_t)bb_));
         MP_HIP(hipMalloc(&d_score1, sizeof(double) * 64));
         // two slots each: the next batch is generated while the current one is in flight
         MP_HIP(hipHostMalloc(&h_samples, sizeof(int) * 2 * 9 * bb_, hipHostMallocDefault));
@@ -1580,7 +1587,8 @@ class Run {
         // MD iterations on the side stream, point iterations on the main one (they
         // write disjoint model slots); scoring waits for both -- or, calibrated, both in
         // one launch on the main stream (launch_solve_fused)
-        const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen};
+        const PtWorkspace W{X_.d_pt_cand, X_.d_pt_ncand, X_.d_pt_slots, X_.d_pt_valid, X_.d_pt_pen,
+                            X_.d_md_ws,   X_.d_md_nr,   X_.cap_b};
         const bool fused = solve_fusable(P_.C) && (int64_t)B <= fuse_max_;
         if (fused) {
             MP_HIP(launch_solve_fused(s, D, P_.C, d_md_list, nmd, d_pt_list, npt, Q.d_samples, W, Q.d_models,
@@ -1590,8 +1598,8 @@ class Run {
             if (nmd > 0) {
                 MP_HIP(hipEventRecord(Q.ev_fork, s));
                 MP_HIP(hipStreamWaitEvent(X_.md_stream, Q.ev_fork, 0));
-                MP_HIP(launch_md_solve(X_.md_stream, D, P_.C, d_md_list, nmd, Q.d_samples, Q.d_models, Q.d_recs,
-                                       Q.d_counts, maxm_));
+                MP_HIP(launch_md_solve_staged(X_.md_stream, D, P_.C, d_md_list, nmd, Q.d_samples, W, Q.d_models,
+                                              Q.d_recs, Q.d_counts, maxm_));
                 MP_HIP(hipEventRecord(Q.ev_join, X_.md_stream));
             }
             MP_HIP(launch_pt_solve(s, D, P_.C, d_pt_list, npt, Q.d_samples, W, Q.d_models, Q.d_recs, Q.d_counts,

@@ -125,14 +125,16 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
 // sums taken in point order -- round 6: the oracle's point_model_tail operation for
 // operation, so a calibrated 5pt model is the oracle's to the bit
 // (tests/test_pt_roots_gpu.py::test_5pt_models_are_the_oracles_to_the_bit).
-__global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
-                                                            const double *cand, const int *ncand, const int *samples,
-                                                            Model *slots, int *valid) {
+// (the body of workgroup `bid`: pt_tail5_group_kernel, and the fused MD-root + tail
+// launch of kernels.hip, which gives it the workgroups past the MD roots')
+__device__ __forceinline__ void pt_tail5_group_body(int bid, const PairData &D, const PairConst &C, const int *list,
+                                                    int nlist, const double *cand, const int *ncand,
+                                                    const int *samples, Model *slots, int *valid) {
 #pragma clang fp contract(off)
     if (batch_cancelled(D.gate, D.gate_hi)) return; // (uniform: the record word is read by every lane)
     constexpr int K = 5, kRoots = 10, kPoses = 2;
     const int lane = threadIdx.x % kTail;
-    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kTail);
+    const int gid = (int)((bid * (size_t)blockDim.x + threadIdx.x) / kTail);
     const int k = gid / nlist, idx = gid - k * nlist;
     if (k >= kRoots || k >= ncand[idx]) return; // the whole group leaves together
     const int *s = samples + (size_t)list[idx] * kSampleStride;
@@ -173,6 +175,12 @@ __global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairCons
             valid[q] = ok ? 1 : 0;
         }
     }
+}
+
+__global__ void __launch_bounds__(64) pt_tail5_group_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                            const double *cand, const int *ncand, const int *samples,
+                                                            Model *slots, int *valid) {
+    pt_tail5_group_body(blockIdx.x, D, C, list, nlist, cand, ncand, samples, slots, valid);
 }
 
 // Shared-focal tail (src/hybrid_pose_shared_focal_estimator.cpp:87-126, the per-root

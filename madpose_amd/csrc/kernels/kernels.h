@@ -34,7 +34,20 @@ struct PtWorkspace {
     Model *slots;
     int *valid;
     double *pen; // kPtPenStride doubles per point sample (shared focal)
+    // the two-stage exact MD solver's per-sample state (kMdWsStride doubles per MD sample,
+    // structure of arrays with leading dimension md_ld >= the batch's MD samples) and root
+    // counts; null: the one-stage kernel
+    double *md_ws = nullptr;
+    int *md_nr = nullptr;
+    int md_ld = 0;
 };
+constexpr int kMdWsStride = 72; // doubles: the system (<= 62) + its roots (<= 8)
+// The exact MD solver in two launches when W.md_ws is set and MADPOSE_MD_TWO_STAGE=2 (the
+// setup with one lane per sample, then one lane per root); else launch_md_solve.  (The
+// fused calibrated launch, launch_solve_fused, takes the two stages by default.)
+hipError_t launch_md_solve_staged(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                                  const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs,
+                                  int *counts, int maxm);
 // point minimal solver over the listed iterations (three launches, see kernels.hip;
 // roots_done: the root stage ran in launch_solve_fused).
 hipError_t launch_pt_solve(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,

@@ -251,6 +251,30 @@ template <> struct MdxSys<kTF> {
     static constexpr int K = 4;
 };
 
+// an MD sample's inputs as the oracle forms them: calibrated rays K^-1 x (estimator.cpp
+// mv3) or the normalized homogeneous points, and the depth priors
+template <int V, int K>
+__device__ __forceinline__ void md_sample_inputs(const PairData &D, const PairConst &C, const int *s, double (&x)[K][3],
+                                                 double (&y)[K][3], double (&dx)[K], double (&dy)[K]) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const int i = s[j];
+        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
+        if (V == kCal) {
+            mdx::mv3_exact(C.K0i, xa, x[j]);
+            mdx::mv3_exact(C.K1i, xb, y[j]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                x[j][q] = xa[q];
+                y[j][q] = xb[q];
+            }
+        }
+        dx[j] = D.d0[i];
+        dy[j] = D.d1[i];
+    }
+}
+
 // the body of workgroup `bid` (md_exact_kernel, and the fused MD + 5pt launch below)
 template <int V, int R>
 __device__ __forceinline__ void md_exact_body(int bid, const PairData &D, const PairConst &C, const int *list,
@@ -269,23 +293,7 @@ __device__ __forceinline__ void md_exact_body(int bid, const PairData &D, const 
     const int b = list[active ? idx : nlist - 1];
     const int *s = samples + (size_t)b * kSampleStride;
     double x[K][3], y[K][3], dx[K], dy[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const int i = s[j];
-        const double xa[3] = {D.x0u[i], D.x0v[i], 1.0}, xb[3] = {D.x1u[i], D.x1v[i], 1.0};
-        if (V == kCal) { // calibrated rays K^-1 x as the oracle forms them (estimator.cpp mv3)
-            mdx::mv3_exact(C.K0i, xa, x[j]);
-            mdx::mv3_exact(C.K1i, xb, y[j]);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                x[j][q] = xa[q];
-                y[j][q] = xb[q];
-            }
-        }
-        dx[j] = D.d0[i];
-        dy[j] = D.d1[i];
-    }
+    md_sample_inputs<V, K>(D, C, s, x, y, dx, dy);
     auto accept = [&](const double (&sol)[6], Model &m) {
         m.focal0 = sol[4];
         m.focal1 = sol[5];
@@ -346,6 +354,110 @@ __device__ __forceinline__ void md_exact_body(int bid, const PairData &D, const 
     }
 }
 
+// ---- The exact MD solvers in two stages (round 6) ----
+// md_exact_body runs a sample's setup -- the system, the resultant, its real roots by
+// balance + Hessenberg QR, the longest part -- in each of its R lanes (the same doubles
+// in each) before the lanes take the roots: at R = 4 the calibrated kernel issues the
+// setup four times, and with big batches (16k-32k MD samples) the waves contend for the
+// SIMDs (md_exact<0,4> 155 us per launch against 77 us at 8192 samples, profiles/r06).
+// Stage 1 runs the setup once per sample (one lane each) and leaves the system and its
+// roots in a workspace (structure of arrays: value k of sample i at ws[k * ld + i],
+// coalesced); stage 2 takes one root per lane (NR lanes per sample: 4 calibrated and two
+// focal, 8 shared focal), with the same per-root operations, acceptance, Procrustes and
+// root-order compaction as md_exact_body -- the models are the same doubles in the same
+// slots (the MD bit-exactness tests and the switch-invariance test with
+// MADPOSE_MD_TWO_STAGE=0 check it).
+template <int V> struct MdxWs {
+    using S = typename MdxSys<V>::S;
+    static constexpr int W = (int)(sizeof(S) / sizeof(double));
+    static_assert(sizeof(S) % sizeof(double) == 0 && W + S::NR <= kMdWsStride, "MD workspace layout");
+};
+
+template <int V>
+__device__ __forceinline__ void md_setup_body(int bid, const PairData &D, const PairConst &C, const int *list,
+                                              int nlist, const int *samples, double *ws, int *ws_nr, int ld) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return;
+    using Sys = typename MdxSys<V>::S;
+    constexpr int K = MdxSys<V>::K, NR = Sys::NR, W = MdxWs<V>::W;
+    const int idx = bid * 64 + (int)threadIdx.x;
+    if (idx >= nlist) return;
+    const int *s = samples + (size_t)list[idx] * kSampleStride;
+    double x[K][3], y[K][3], dx[K], dy[K];
+    md_sample_inputs<V, K>(D, C, s, x, y, dx, dy);
+    Sys sys;
+    double roots[NR];
+    const int nr = sys.setup(x, y, dx, dy, roots);
+    double buf[W];
+    __builtin_memcpy(buf, &sys, sizeof(Sys));
+    static_for<W>([&](auto k) { ws[(size_t)k * ld + idx] = buf[k]; });
+    static_for<NR>([&](auto k) { ws[(size_t)(W + k) * ld + idx] = roots[k]; });
+    ws_nr[idx] = nr;
+}
+
+template <int V>
+__device__ __forceinline__ void md_root_body(int bid, const PairData &D, const PairConst &C, const int *list, int nlist,
+                                             const int *samples, const double *ws, const int *ws_nr, int ld,
+                                             Model *models, ScoreRec *recs, int *counts, int maxm) {
+    if (batch_cancelled(D.gate, D.gate_hi)) return;
+    using Sys = typename MdxSys<V>::S;
+    constexpr int K = MdxSys<V>::K, NR = Sys::NR, W = MdxWs<V>::W, R = NR;
+    const int g = threadIdx.x / R, r = threadIdx.x % R;
+    const int idx = bid * (64 / R) + g;
+    const bool active = idx < nlist;
+    const int ia = active ? idx : nlist - 1;
+    const int b = list[ia];
+    const int *s = samples + (size_t)b * kSampleStride;
+    double x[K][3], y[K][3], dx[K], dy[K];
+    md_sample_inputs<V, K>(D, C, s, x, y, dx, dy);
+    Sys sys;
+    {
+        double buf[W];
+        static_for<W>([&](auto k) { buf[k] = ws[(size_t)k * ld + ia]; });
+        __builtin_memcpy(&sys, buf, sizeof(Sys));
+    }
+    const int nr = ws_nr[ia];
+    const double root = ws[(size_t)(W + r) * ld + ia];
+    const int g0 = (threadIdx.x & 63) & ~(R - 1);
+    Model m;
+    double X[K][3], Y[K][3];
+    bool keep = false;
+    if (active && r < nr) {
+        double sol[6];
+        if (sys.root(root, sol)) {
+            m.focal0 = sol[4];
+            m.focal1 = sol[5];
+            if (md_pose_points<K>(x, y, dx, dy, sol, sol[4], sol[5], X, Y)) {
+                m.scale = sol[2];
+                m.offset0 = sol[1];
+                m.offset1 = sol[3];
+                keep = md_accept(C, m);
+            }
+        }
+    }
+    const unsigned long long ball = __ballot(keep);
+    const unsigned long long mine = (ball >> g0) & ((1ull << R) - 1);
+    const int pos = __popcll(mine & ((1ull << r) - 1));
+    if (keep && pos < maxm) {
+        mdx::procrustes<K>(X, Y, m);
+        put_model(C, m, b, pos, maxm, models, recs);
+    }
+    const int n = __popcll(mine);
+    if (active && r == 0) counts[b] = n < maxm ? n : maxm;
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) md_setup_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                      const int *samples, double *ws, int *ws_nr, int ld) {
+    md_setup_body<V>(blockIdx.x, D, C, list, nlist, samples, ws, ws_nr, ld);
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) md_root_kernel(PairData D, PairConst C, const int *list, int nlist,
+                                                     const int *samples, const double *ws, const int *ws_nr, int ld,
+                                                     Model *models, ScoreRec *recs, int *counts, int maxm) {
+    md_root_body<V>(blockIdx.x, D, C, list, nlist, samples, ws, ws_nr, ld, models, recs, counts, maxm);
+}
+
 template <int V, int R>
 __global__ void __launch_bounds__(64) md_exact_kernel(PairData D, PairConst C, const int *list, int nlist,
                                                       const int *samples, Model *models, ScoreRec *recs, int *counts,
@@ -366,6 +478,31 @@ __global__ void __launch_bounds__(64) md_pt5_kernel(PairData D, PairConst C, con
         md_exact_body<kCal, 4>(blockIdx.x, D, C, md_list, nmd, samples, models, recs, counts, maxm);
     else
         pt_roots5_group_body(blockIdx.x - md_blocks, D, C, pt_list, npt, samples, cand, ncand, cand_stride);
+}
+
+// The calibrated solvers with the two-stage MD: launch 1 = the MD setups (one lane per
+// sample, md_blocks workgroups) + the 5pt root stage, launch 2 = the MD roots (4 lanes per
+// sample) + the 5pt tails -- the same number of launches as md_pt5 + tails.
+__global__ void __launch_bounds__(64) md_setup_pt5_kernel(PairData D, PairConst C, const int *md_list, int nmd,
+                                                          int md_blocks, const int *pt_list, int npt,
+                                                          const int *samples, double *cand, int *ncand,
+                                                          int cand_stride, double *ws, int *ws_nr, int ld) {
+    if ((int)blockIdx.x < md_blocks)
+        md_setup_body<kCal>(blockIdx.x, D, C, md_list, nmd, samples, ws, ws_nr, ld);
+    else
+        pt_roots5_group_body(blockIdx.x - md_blocks, D, C, pt_list, npt, samples, cand, ncand, cand_stride);
+}
+
+__global__ void __launch_bounds__(64) md_root_tail5_kernel(PairData D, PairConst C, const int *md_list, int nmd,
+                                                           int md_blocks, const int *pt_list, int npt,
+                                                           const int *samples, const double *ws, const int *ws_nr,
+                                                           int ld, Model *models, ScoreRec *recs, int *counts, int maxm,
+                                                           const double *cand, const int *ncand, Model *slots,
+                                                           int *valid) {
+    if ((int)blockIdx.x < md_blocks)
+        md_root_body<kCal>(blockIdx.x, D, C, md_list, nmd, samples, ws, ws_nr, ld, models, recs, counts, maxm);
+    else
+        pt_tail5_group_body(blockIdx.x - md_blocks, D, C, pt_list, npt, cand, ncand, samples, slots, valid);
 }
 
 template <int K>
@@ -1046,6 +1183,20 @@ hipError_t launch_prep_pair(hipStream_t s, const PairConst &C, const PairData &D
 static bool md_plain(const PairConst &C) {
     return C.md_alt == 0 && (C.variant != kCal || (!C.scale_only && C.use_shift));
 }
+// Where the two-stage exact MD (md_setup + md_root) runs: MADPOSE_MD_TWO_STAGE = 1 (the
+// default) in the fused calibrated launch only, 2 in every MD launch, 0 nowhere;
+// MADPOSE_MDX_R (the one-stage kernel at R lanes per sample, A/B) turns it off.  Measured
+// (profiles/r06/md2): fused calibrated batches md_pt5 86 + tail 23 -> md_setup_pt5 74 +
+// md_root_tail5 22 us; the unfused ones gain nothing -- the setup with one lane per sample
+// takes 123 us at 16k-32k samples against md_exact<0,4>'s 155 us with the 36 us root stage
+// after it: a wave's setup lasts as long as the slowest of its 64 samples' QR trips, where
+// four lanes per sample wait for the slowest of 16 -- and the shared-focal setup spills
+// (310 VGPRs, 144 B scratch; 252 + 82 against 311 us)
+static int md_two_stage_mode() {
+    static const int mode = env_int("MADPOSE_MDX_R", 0, 0, 4) != 0 ? 0 : (int)env_int("MADPOSE_MD_TWO_STAGE", 1, 0, 2);
+    return mode;
+}
+static bool md_two_stage() { return md_two_stage_mode() >= 1; }
 // md_exact's lanes per sample (MADPOSE_MDX_R=1|2|4 overrides the default)
 static int md_lanes(int v) {
     static const int r_env = [] {
@@ -1092,6 +1243,23 @@ hipError_t launch_md_solve(hipStream_t s, const PairData &D, const PairConst &C,
     });
 }
 
+hipError_t launch_md_solve_staged(hipStream_t s, const PairData &D, const PairConst &C, const int *list, int nlist,
+                                  const int *samples, const PtWorkspace &W, Model *models, ScoreRec *recs,
+                                  int *counts, int maxm) {
+    if (nlist <= 0) return hipSuccess;
+    if (!W.md_ws || md_two_stage_mode() < 2 || !md_plain(C))
+        return launch_md_solve(s, D, C, list, nlist, samples, models, recs, counts, maxm);
+    if (nlist > W.md_ld) return hipErrorInvalidValue;
+    return by_variant(C.variant, [&](auto V) {
+        constexpr int v = decltype(V)::value;
+        constexpr int spw = 64 / MdxSys<v>::S::NR; // samples per workgroup of the root stage
+        md_setup_kernel<v><<<(nlist + 63) / 64, 64, 0, s>>>(D, C, list, nlist, samples, W.md_ws, W.md_nr, W.md_ld);
+        md_root_kernel<v><<<(nlist + spw - 1) / spw, 64, 0, s>>>(D, C, list, nlist, samples, W.md_ws, W.md_nr,
+                                                                W.md_ld, models, recs, counts, maxm);
+        return hipGetLastError();
+    });
+}
+
 // the shared-focal root stage by the deflated eigenproblem: the pencil (16-lane groups,
 // eig6.h), its deflation + balance + Hessenberg form (16-lane groups, eig6_defl_grp.h),
 // then the lockstep Francis QR (one sample per lane, eig6.h / eig15_gen.h)
@@ -1129,6 +1297,27 @@ hipError_t launch_solve_fused(hipStream_t s, const PairData &D, const PairConst 
                               const int *pt_list, int npt, const int *samples, const PtWorkspace &W, Model *models,
                               ScoreRec *recs, int *counts, int maxm) {
     if (!solve_fusable(C)) return hipErrorInvalidValue;
+    if (W.md_ws && md_two_stage()) {
+        if (nmd > W.md_ld) return hipErrorInvalidValue;
+        // launch 1: MD setups (one lane per sample) + 5pt roots; launch 2: MD roots (four
+        // lanes per sample) + 5pt tails; then the 5pt compaction
+        const int md1 = (nmd + 63) / 64, md2 = (nmd + 15) / 16, pt_blocks = (npt + kS5 - 1) / kS5;
+        const long lanes = (long)npt * PtTraits<kCal>::kRoots;
+        const int tgrid = (int)((lanes * kTail + 63) / 64);
+        if (md1 + pt_blocks > 0)
+            md_setup_pt5_kernel<<<md1 + pt_blocks, 64, 0, s>>>(D, C, md_list, nmd, md1, pt_list, npt, samples, W.cand,
+                                                               W.ncand, kCandStride, W.md_ws, W.md_nr, W.md_ld);
+        if (md2 + tgrid > 0)
+            md_root_tail5_kernel<<<md2 + tgrid, 64, 0, s>>>(D, C, md_list, nmd, md2, pt_list, npt, samples, W.md_ws,
+                                                            W.md_nr, W.md_ld, models, recs, counts, maxm, W.cand,
+                                                            W.ncand, W.slots, W.valid);
+        if (npt > 0) {
+            constexpr int kCompactG = 32; // (PtTraits<kCal>: 2 poses x 10 roots > 4)
+            pt_compact_kernel<kCal><<<(int)(((size_t)npt * kCompactG + 63) / 64), 64, 0, s>>>(
+                C, pt_list, npt, W.ncand, W.slots, W.valid, models, recs, counts, maxm, BatchGate{D.gate, D.gate_hi});
+        }
+        return hipGetLastError();
+    }
     const int md_blocks = (nmd + 15) / 16, pt_blocks = (npt + kS5 - 1) / kS5;
     if (md_blocks + pt_blocks > 0)
         md_pt5_kernel<<<md_blocks + pt_blocks, 64, 0, s>>>(D, C, md_list, nmd, md_blocks, pt_list, npt, samples, W.cand,
