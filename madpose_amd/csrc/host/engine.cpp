@@ -1696,7 +1696,12 @@ void Run::run(Model *best, Stats *S) {
         const long r = runs.fetch_add(1);
         const char *e = std::getenv("MADPOSE_TIMELINE");
         long lo = -1, hi = -1; // "k" or "k-m"
-        if (e && std::sscanf(e, "%ld-%ld", &lo, &hi) < 2) hi = lo;
+        if (e) {
+            int used = 0;
+            const int k = std::sscanf(e, "%ld%n-%ld%n", &lo, &used, &hi, &used);
+            if (k < 1 || e[used] != '\0' || lo < 0 || (k == 2 && hi < lo)) env_reject("MADPOSE_TIMELINE", e, "expected k or k-m");
+            if (k < 2) hi = lo;
+        }
         tl_.on = e && r >= lo && r <= hi;
         tl_.run = r;
         tl_.t0 = t_start;

@@ -121,3 +121,28 @@ def test_standalone_5pt_runs_the_estimators_root_stage():
         assert len(dev) == len(ref), s
         for m in ref:
             assert min(np.abs(d.R() - m["R"]).max() + np.abs(d.t() - m["t"]).max() for d in dev) <= 1e-9, s
+
+
+def test_6pt_root_stage_is_independent_of_the_packing():
+    """The shared-focal QR runs one sample per wave at <= 1024 samples (the window state
+    scalar: columns and rows outside the active window skipped by scalar branches) and
+    several samples per wave above (the whole band updated, windows by selects).  Both
+    perform the same operations on every entry inside the window, and entries outside
+    it are never read again, so a sample's candidates must not depend on the launch:
+    the same 600 samples alone (one per wave), inside 3000 (three per wave) and inside
+    6000 (six per wave) give the same bits."""
+    rng = np.random.default_rng(71)
+    r0, r1 = ps.random_samples(rng, 3000, 6)
+    o0, o1 = ps.outlier_samples(rng, 1500, 6)
+    w0, w1 = ps.wide_samples(rng, 1500, 6)
+    p0, p1 = np.concatenate([r0[:300], o0[:150], w0[:150], r0[300:], o0[150:], w0[150:]]), \
+        np.concatenate([r1[:300], o1[:150], w1[:150], r1[300:], o1[150:], w1[150:]])
+    c6k, n6k = _device_roots(1, 3, p0, p1)
+    c3k, n3k = _device_roots(1, 3, p0[:3000], p1[:3000])
+    c600, n600 = _device_roots(1, 3, p0[:600], p1[:600])
+    assert n600.sum() > 600, n600.sum()
+    for c, n, m in ((c3k, n3k, 600), (c6k, n6k, 600), (c6k, n6k, 3000)):
+        ref_c, ref_n = (c600, n600) if m == 600 else (c3k, n3k)
+        assert np.array_equal(n[:m], ref_n[:m]), m
+        diff = np.nonzero(~np.all((c[:m] == ref_c[:m]) | (np.isnan(c[:m]) & np.isnan(ref_c[:m])), axis=1))[0]
+        assert diff.size == 0, (m, diff[:10])
