@@ -225,13 +225,18 @@ template <int n, int m> MP_HD bool qr_solve(double (&A)[n][n], double (&B)[n][m]
             for (int k = i + 1; k < n; ++k) s -= A[i][k] * B[k][j];
             B[i][j] = s / A[i][i];
         }
+    // (a gather by selects: the scatter X[perm[i]] = B[i] stored through a selected
+    // pointer, which kept X in scratch)
 #pragma unroll
-    for (int i = 0; i < n; ++i)
+    for (int r = 0; r < n; ++r)
 #pragma unroll
-        for (int r = 0; r < n; ++r)
-            if (perm[i] == r)
+        for (int j = 0; j < m; ++j) {
+            double v = 0.0;
 #pragma unroll
-                for (int j = 0; j < m; ++j) X[r][j] = B[i][j];
+            for (int i = 0; i < n; ++i)
+                if (perm[i] == r) v = opaque(B[i][j]);
+            X[r][j] = v;
+        }
     return true;
 }
 

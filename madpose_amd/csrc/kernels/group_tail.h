@@ -121,10 +121,10 @@ __global__ void __launch_bounds__(64) pt_tail7_group_kernel(PairData D, PairCons
 // Calibrated tail (src/hybrid_pose_estimator.cpp:134-182) with one 8-lane group per
 // (root, sample), lane j < 5 holding point j: the cheirality tests of
 // motion_from_essential (AND over the group), then for each of the at most two poses
-// the triangulation (Eigen's JacobiSVD, eigen_svd4_null) and depth fit with the group's
-// sums taken in point order -- round 6: the oracle's point_model_tail operation for
-// operation, so a calibrated 5pt model is the oracle's to the bit
-// (tests/test_pt_roots_gpu.py::test_5pt_models_are_the_oracles_to_the_bit).
+// the triangulation (dlt_null4: Householder QR + inverse iteration, restated in the
+// oracle) and depth fit with the group's sums taken in point order -- round 6: the
+// oracle's point_model_tail operation for operation, so a calibrated 5pt model is the
+// oracle's to the bit (tests/test_ties_gpu.py::test_calibrated_models_are_the_oracles_to_the_bit).
 // (the body of workgroup `bid`: pt_tail5_group_kernel, and the fused MD-root + tail
 // launch of kernels.hip, which gives it the workgroups past the MD roots')
 __device__ __forceinline__ void pt_tail5_group_body(int bid, const PairData &D, const PairConst &C, const int *list,
