@@ -112,7 +112,11 @@ class Sampler {
     };
     void start(const IterationStream &from, Batch *g, uint32_t B, int slot, int *smp,
                std::function<void()> after = nullptr, const Chain *chain = nullptr) {
-        std::lock_guard<std::mutex> lk(mu_);
+        std::unique_lock<std::mutex> lk(mu_);
+        if (busy_) { // a chained batch nobody asked for (chained()) is still being drawn
+            abort_ = true;
+            done_cv_.wait(lk, [this] { return !busy_; });
+        }
         g2_ = chain ? chain->g : nullptr;
         B2_ = chain ? chain->B : 0;
         slot2_ = chain ? chain->slot : 0;
@@ -127,23 +131,28 @@ class Sampler {
         slot_ = slot;
         smp_ = smp;
         abort_ = false;
-        busy_ = true;
+        busy_ = busy1_ = true;
         ok_ = false;
         ++gen_;
         cv_.notify_all();
     }
-    // after finish(): whether the chained batch was drawn; *rs the stream state after it
+    // after finish(): waits for the chained batch (the rest of the job); whether it was
+    // drawn, *rs the stream state after it
     bool chained(IterationStream *rs) {
-        std::lock_guard<std::mutex> lk(mu_);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return !busy_; });
+        if (err2_) std::rethrow_exception(err2_);
         if (ok2_) *rs = rs2_;
         return ok2_;
     }
-    // waits for the batch; on success *rs is the stream state after it
+    // waits for the batch (not for a chained one: that is drawn on while the caller reads
+    // this one, until chained(), cancel() or the next start()); on success *rs is the
+    // stream state after it
     bool finish(IterationStream *rs) {
         std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return !busy_; });
+        done_cv_.wait(lk, [this] { return !busy1_; });
         if (err_) std::rethrow_exception(err_);
-        if (ok_) *rs = rs_;
+        if (ok_) *rs = rs1_;
         return ok_;
     }
     void cancel() {
@@ -171,25 +180,33 @@ class Sampler {
                 }
             }
             Batch *const g2 = g2_; // (set with the job, under the lock)
-            bool ok2 = false;
-            IterationStream r2;
-            if (ok && !err && g2) {
-                r2 = rs_;
-                ok2 = draw_batch(r2, *g2, B2_, slot2_, smp2_, &abort_, sampler_mode());
-                if (ok2 && after2_) {
-                    try {
-                        after2_();
-                    } catch (...) {
-                        err = std::current_exception();
-                        ok2 = false;
-                    }
+            lk.lock();
+            rs1_ = rs_;
+            err_ = err;
+            ok_ = ok;
+            busy1_ = false; // finish() returns here: the chained batch is drawn after it
+            ok2_ = false;
+            err2_ = nullptr;
+            const bool go2 = ok && !err && g2;
+            if (!go2) busy_ = false;
+            done_cv_.notify_all();
+            if (!go2) continue;
+            lk.unlock();
+            std::exception_ptr err2;
+            IterationStream r2 = rs_;
+            bool ok2 = draw_batch(r2, *g2, B2_, slot2_, smp2_, &abort_, sampler_mode());
+            if (ok2 && after2_) {
+                try {
+                    after2_();
+                } catch (...) {
+                    err2 = std::current_exception();
+                    ok2 = false;
                 }
             }
             lk.lock();
             rs2_ = r2;
             ok2_ = ok2;
-            err_ = err;
-            ok_ = ok;
+            err2_ = err2;
             busy_ = false;
             done_cv_.notify_all();
         }
@@ -207,11 +224,11 @@ class Sampler {
     uint32_t B2_ = 0;
     int slot2_ = 0;
     int *smp2_ = nullptr;
-    IterationStream rs2_;
+    IterationStream rs1_, rs2_; // the streams after the batch / after the chained one
     bool ok2_ = false;
-    std::exception_ptr err_;
+    std::exception_ptr err_, err2_;
     std::atomic<bool> abort_{false};
-    bool busy_ = false, ok_ = false, quit_ = false;
+    bool busy_ = false, busy1_ = false, ok_ = false, quit_ = false; // busy1_: the first batch is drawing
     uint64_t gen_ = 0;
     std::thread th_;
 };
@@ -1805,9 +1822,10 @@ void Run::run(Model *best, Stats *S) {
     const bool chain_on = [] {
         return env_flag("MADPOSE_LO_CHAIN", true);
     }();
-    bool chain_ready = false; // gen[cur ^ 1] holds the drawn batch from chain_at on
-    uint32_t chain_at = 0;
-    IterationStream chain_rs; // the streams after it
+    // gen[cur ^ 1] holds (or the sampler is still drawing, until chained()) the batch
+    // of chain_B iterations from chain_at on
+    bool chain_ready = false;
+    uint32_t chain_at = 0, chain_B = 0;
     // MADPOSE_LO_CHAIN_LAUNCH=1: the job also launches the chained batch, behind the
     // speculative batch (the GPU otherwise idles for the rest of the LO), bound by the
     // pre-LO best and gated on the speculative batch's record word (kernels.h
@@ -1818,7 +1836,8 @@ void Run::run(Model *best, Stats *S) {
     const bool chain_launch = [] {
         return env_flag("MADPOSE_LO_CHAIN_LAUNCH", false);
     }();
-    auto make_chain = [&](uint32_t at, uint32_t Bs, int slot, double bound, Sampler::Chain *ch, uint32_t *ch_at) {
+    auto make_chain = [&](uint32_t at, uint32_t Bs, int slot, double bound, Sampler::Chain *ch, uint32_t *ch_at,
+                          uint32_t *ch_B) {
         const uint32_t at2 = at + Bs;
         if (!chain_on || early_mode_ != 0 || at2 >= max_total || at2 == lo_start) return false;
         const uint32_t B2 = batch_size(at2, grow(at2));
@@ -1836,6 +1855,7 @@ void Run::run(Model *best, Stats *S) {
         }
         *ch = Sampler::Chain{g2, B2, slot ^ 1, slot_for(slot ^ 1, B2), std::move(after)};
         *ch_at = at2;
+        *ch_B = B2;
         return true;
     };
     bool chain_launched = false; // (the chained batch is on the GPU already)
@@ -1854,9 +1874,9 @@ void Run::run(Model *best, Stats *S) {
             Batch *const gs = &gen[slot];
             const uint32_t at = it;
             bool spec0_chain = false, spec0_chain_launched = false;
-            uint32_t spec0_chain_at = 0;
+            uint32_t spec0_chain_at = 0, spec0_chain_B = 0;
             auto predicted = [this, rs_at_lo, slot, bound, gs, at, max_total, speculate, lo_start, &grow, &batch_size,
-                              &spec0, &spec0_draws, &make_chain, &spec0_chain, &spec0_chain_at,
+                              &spec0, &spec0_draws, &make_chain, &spec0_chain, &spec0_chain_at, &spec0_chain_B,
                               &spec0_chain_launched](const Mt19937 &sel_end) {
                 if (!speculate || at >= max_total) return;
                 IterationStream from = rs_at_lo;
@@ -1864,7 +1884,7 @@ void Run::run(Model *best, Stats *S) {
                 slot_free(slot);
                 const uint32_t Bs = batch_size(at, sync_batch(grow(at)));
                 Sampler::Chain ch;
-                spec0_chain = make_chain(at, Bs, slot, bound, &ch, &spec0_chain_at);
+                spec0_chain = make_chain(at, Bs, slot, bound, &ch, &spec0_chain_at, &spec0_chain_B);
                 spec0_chain_launched = spec0_chain && ch.after != nullptr;
                 X_.sampler->start(from, gs, Bs, slot, slot_for(slot, Bs),
                                   [this, gs, bound, at, lo_start] {
@@ -1886,9 +1906,11 @@ void Run::run(Model *best, Stats *S) {
                     if (have_next) {
                         cur ^= 1;
                         launched = true;
-                        chain_ready = spec0_chain && X_.sampler->chained(&chain_rs);
+                        // (the chained batch may still be drawing: chained() below)
+                        chain_ready = spec0_chain;
                         chain_at = spec0_chain_at;
-                        chain_launched = chain_ready && spec0_chain_launched;
+                        chain_B = spec0_chain_B;
+                        chain_launched = spec0_chain && spec0_chain_launched;
                     }
                 } else {
                     X_.sampler->cancel();
@@ -1938,8 +1960,9 @@ void Run::run(Model *best, Stats *S) {
                                  : 0;
         // the chained batch, when it starts where the next one does
         const bool use_chain = chain_ready && Bn0 > 0 && it_next == chain_at;
+        if (chain_ready && !use_chain) X_.sampler->cancel(); // (not the next batch)
         chain_ready = false;
-        const uint32_t Bn = use_chain ? gen[cur ^ 1].B : Bn0;
+        const uint32_t Bn = use_chain ? chain_B : Bn0;
         const bool early = !use_chain && Bn > 0 && early_now(Bn);
         if (Bn > 0 && !use_chain) {
             slot_free(cur ^ 1);
@@ -2000,7 +2023,7 @@ void Run::run(Model *best, Stats *S) {
         bool spec = false; // the sampler holds the post-LO speculation, not the Bn batch
         uint64_t spec_draws = 0;
         bool spec_chain = false, spec_chain_launched = false; // ... and the batch after it (make_chain)
-        uint32_t spec_chain_at = 0;
+        uint32_t spec_chain_at = 0, spec_chain_B = 0;
         uint32_t j = 0;
         const bool dumping = model_dump_ || count_dump_;
         for (; j < B; ++j) {
@@ -2107,7 +2130,8 @@ void Run::run(Model *best, Stats *S) {
                             Batch *const gs = &gen[slot];
                             auto predicted = [this, rs_at_lo, slot, cont_pending, bound, gs, at, max_total, speculate,
                                               lo_start, &grow, &batch_size, &spec, &spec_draws, &make_chain,
-                                              &spec_chain, &spec_chain_at, &spec_chain_launched](const Mt19937 &sel_end) {
+                                              &spec_chain, &spec_chain_at, &spec_chain_B,
+                                              &spec_chain_launched](const Mt19937 &sel_end) {
                                 if (!speculate || at >= max_total) return;
                                 if (cont_pending) X_.sampler->cancel(); // the no-LO continuation
                                 IterationStream from = rs_at_lo;
@@ -2116,7 +2140,7 @@ void Run::run(Model *best, Stats *S) {
                                 slot_free(slot); // (an early continuation's samples are on the device)
                                 const uint32_t Bs = batch_size(at, sync_batch(bc));
                                 Sampler::Chain ch;
-                                spec_chain = make_chain(at, Bs, slot, bound, &ch, &spec_chain_at);
+                                spec_chain = make_chain(at, Bs, slot, bound, &ch, &spec_chain_at, &spec_chain_B);
                                 spec_chain_launched = spec_chain && ch.after != nullptr;
                                 X_.sampler->start(from, gs, Bs, slot, slot_for(slot, Bs),
                                                   [this, gs, bound, at, lo_start] {
@@ -2156,12 +2180,16 @@ void Run::run(Model *best, Stats *S) {
         if (!done && !invalidated) {
             it += B;
             have_next = false;
-            if (Bn > 0 && use_chain) { // drawn during the LO (chained speculation)
+            if (Bn > 0 && use_chain) { // drawn during the LO and the walk (chained speculation)
                 tl_.mark("chained", (long)Bn);
-                rs_ = chain_rs;
-                have_next = true;
-                cur ^= 1;
-                launched = chain_launched;
+                IterationStream crs;
+                if (X_.sampler->chained(&crs)) {
+                    tl_.mark("chain_joined");
+                    rs_ = crs;
+                    have_next = true;
+                    cur ^= 1;
+                    launched = chain_launched;
+                } // (else rs_ stands at the end of this batch)
             } else if (Bn > 0) { // rs_ moves to the end of the drawn batch
                 auto t0 = Clock::now();
                 tl_.mark("join_sampler");
@@ -2184,9 +2212,10 @@ void Run::run(Model *best, Stats *S) {
                 if (have_next) {
                     cur ^= 1;
                     launched = true;
-                    chain_ready = spec_chain && X_.sampler->chained(&chain_rs);
+                    chain_ready = spec_chain; // (still drawing, maybe: chained() above)
                     chain_at = spec_chain_at;
-                    chain_launched = chain_ready && spec_chain_launched;
+                    chain_B = spec_chain_B;
+                    chain_launched = spec_chain && spec_chain_launched;
                 }
             } else {
                 X_.sampler->cancel();
