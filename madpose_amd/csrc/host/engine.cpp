@@ -1136,7 +1136,16 @@ class Run {
 
     // UpdateRANSACTerminationCriteria (src/hybrid_ransac.h:351-378)
     void termination(const Model &m, uint32_t *max_per) {
-        S_->best_num_inliers = inliers(lanes_[0], m, thr_, S_->inlier_indices);
+        // after an LO the new best was usually swept last by the LO lane that recorded it:
+        // its cached errors give the same inliers as a fresh sweep (the workers are idle
+        // between LOs, so their lanes are read here without a race)
+        Lane *L = &lanes_[0];
+        for (Lane &c : lanes_)
+            if (c.valid && std::memcmp(&m, &c.model, sizeof(Model)) == 0) {
+                L = &c;
+                break;
+            }
+        S_->best_num_inliers = inliers(*L, m, thr_, S_->inlier_indices);
         for (int t = 0; t < 3; ++t)
             S_->inlier_ratios[t] = n_ > 0 ? (double)S_->inlier_indices[t].size() / (double)n_ : 0.0;
         for (int s = 0; s < 2; ++s) max_per[s] = num_required(s);
@@ -1292,13 +1301,13 @@ class Run {
     // The non-minimal sample of an LO step is unusable (NonMinimalSolver returns 0,
     // or Solve() sees no residuals): the step is skipped without drawing.
     bool step_skipped(const std::vector<int> &sample_all) const {
-        std::vector<int> smp[3];
-        split(sample_all, n_, smp);
+        // (the sizes split() would give, counted without building the lists: this runs
+        // on the estimator thread before the parallel steps start)
+        int cnt[3] = {0, 0, 0};
+        for (const int idx : sample_all) cnt[(idx >= n_) + (idx >= 2 * n_)]++;
         const int kmd = variant_ == kCal ? 3 : 4;
-        if (((int)smp[0].size() < kmd && (int)smp[1].size() < kmd) || (int)smp[2].size() < min_sample_size_)
-            return true;
-        const size_t nres = (cfg_.lo_type != 1 ? smp[0].size() + smp[1].size() : 0) +
-                            (cfg_.lo_type != 2 ? smp[2].size() : 0);
+        if ((cnt[0] < kmd && cnt[1] < kmd) || cnt[2] < min_sample_size_) return true;
+        const size_t nres = (cfg_.lo_type != 1 ? (size_t)cnt[0] + cnt[1] : 0) + (cfg_.lo_type != 2 ? (size_t)cnt[2] : 0);
         return nres == 0;
     }
     struct StepOut {
@@ -1414,9 +1423,10 @@ class Run {
                 std::vector<uint64_t> start(R);
                 uint64_t pos = sel.draws();
                 const uint64_t per_step = (uint64_t)(1 + o_.num_lsq_iterations) * (uint64_t)lsq_fit_draws(st);
+                const bool skip0 = step_skipped(sample0), skip1 = R > 1 && step_skipped(sample1);
                 for (int r = 0; r < R; ++r) {
                     start[r] = pos;
-                    if (!step_skipped(r == 0 ? sample0 : sample1)) pos += per_step;
+                    if (!(r == 0 ? skip0 : skip1)) pos += per_step;
                 }
                 const Mt19937 base_sel = sel;
                 // the speculation hook runs as job 1, beside the steps: step 0 (the
@@ -1566,12 +1576,15 @@ class Run {
     const bool lo_timing_ = std::getenv("MADPOSE_LO_TIMING") != nullptr;
     std::mutex lm_stat_mu_;
     double lm_stat_[4] = {0, 0, 0, 0};
-    // the fused MD + 5pt launch up to this batch size (MADPOSE_SOLVE_FUSE_MAX): larger
-    // batches fill the GPU, where the fused kernel's 216 VGPRs (two waves per SIMD) cost
-    // the 5pt root stage its third wave -- cal 5.62 (always fused) -> 5.46 ms per pair
-    // (up to 8192), 3 x 200 pairs on one box, profiles/r05/r5o
+    // the fused MD + 5pt launches up to this batch size (MADPOSE_SOLVE_FUSE_MAX; default:
+    // every batch).  Round 5's one-stage fused kernel (216 VGPRs, two waves per SIMD) cost
+    // the 5pt root stage its third wave on big batches (cal 5.62 always fused -> 5.46 ms
+    // up to 8192, profiles/r05/r5o); the two-stage form (md_setup_pt5 + md_root_tail5)
+    // runs the big batches faster than the MD side stream beside the point chain: cal
+    // gpu_solve 2.10 -> 2.02 ms, 3.99 -> 3.90 ms per pair (5 same-box A/B pairs,
+    // profiles/r06/fuse_all)
     const int64_t fuse_max_ = [] {
-        return (int64_t)env_int("MADPOSE_SOLVE_FUSE_MAX", 8192, 0, 1ll << 40);
+        return (int64_t)env_int("MADPOSE_SOLVE_FUSE_MAX", 1ll << 40, 0, 1ll << 40);
     }();
 
     // cut_on_record: the batch lies at or past lo_starting_iterations, so its first new

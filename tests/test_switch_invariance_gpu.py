@@ -14,7 +14,8 @@ post-LO speculation predicted after the LO prefix instead of before it
 it drawn (MADPOSE_LO_CHAIN) or launched (MADPOSE_LO_CHAIN_LAUNCH) in the same job; the
 scoring without its exact early exit (MADPOSE_SCORE_EXIT) or record skip
 (MADPOSE_RECORD_SKIP), with an exit check after every trip (MADPOSE_SCORE_CHECK), and the
-fused MD + 5pt launch for no batch or for every batch (MADPOSE_SOLVE_FUSE_MAX), and the
+fused MD + 5pt launch for no batch or only up to 8192 iterations instead of every batch
+(MADPOSE_SOLVE_FUSE_MAX), and the
 exact MD solver in one launch with its setup repeated in every lane of a sample instead of
 the setup and root stages (MADPOSE_MD_TWO_STAGE).  A value
 that does not parse is refused loudly (host/env.h)."""
@@ -39,7 +40,7 @@ SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOS
             "score_single_trips": {"MADPOSE_SCORE_PAIR": "0"},
             "score_no_exit": {"MADPOSE_SCORE_EXIT": "0"}, "no_record_skip": {"MADPOSE_RECORD_SKIP": "0"},
             "score_check_every_trip": {"MADPOSE_SCORE_CHECK": "1,1"},
-            "fuse_never": {"MADPOSE_SOLVE_FUSE_MAX": "0"}, "fuse_always": {"MADPOSE_SOLVE_FUSE_MAX": "65536"},
+            "fuse_never": {"MADPOSE_SOLVE_FUSE_MAX": "0"}, "fuse_up_to_8192": {"MADPOSE_SOLVE_FUSE_MAX": "8192"},
             "md_one_stage": {"MADPOSE_MD_TWO_STAGE": "0"}, "md_two_stage_everywhere": {"MADPOSE_MD_TWO_STAGE": "2"}}
 
 
