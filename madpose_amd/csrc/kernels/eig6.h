@@ -117,6 +117,34 @@ __global__ void __launch_bounds__(64) pt_pencil6_kernel(PairData D, const int *l
 
 // (EISPACK sign transfer, used by the generated QR of eig15_gen.h)
 __device__ inline double e6_sign(double a, double b) { return b >= 0 ? fabs(a) : -fabs(a); }
+// The bulge reflectors' reciprocals (1 / |p|+|q|+|r|, 1 / s, 1 / (p + s), all nonzero
+// there): the hardware reciprocal refined by two Newton steps (within about an ulp, 5
+// FP64 instructions on the sweep's serial chain instead of the division's 11), branch-free
+// (a range guard's branch cost the straight-line sweep more than it saved).  Both QR
+// kernels (one sample per wave, samples per lane) run this code, so their roots stay
+// bit-identical to each other.
+// sqrt(p^2 + q^2 + r^2) of a reflector whose (p, q, r) were scaled to |p|+|q|+|r| = 1
+// (or are all zero): the argument lies in [1/3, 1] or is 0, so the hardware inverse
+// square root refined by one Newton step on each of the root and its half reciprocal
+// (8 FP64 instructions) needs none of the general sqrt's range scaling (16); within
+// about an ulp
+__device__ inline double e6_sqrt_unit(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    const double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return x == 0.0 ? 0.0 : g;
+}
+__device__ inline double e6_rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
 
 // ---------------------------------------------------------------------------
 // The 15 x 15 eigenproblem with one sample per lane, every access static:
