@@ -524,6 +524,97 @@ MP_HD void smallest_right_sv4(const double (&A0)[4][4], double *v) {
     for (int i = 0; i < 4; ++i) v[i] = w[0] * V[i][0] + w[1] * V[i][1] + w[2] * V[i][2] + w[3] * V[i][3];
 }
 
+// The same Jacobi sweeps with the rotations' quotients and square roots by the hardware
+// reciprocal / inverse square root refined by Newton steps (within about an ulp, a third
+// of the instructions of the IEEE sequences) on the device, the IEEE operations on the
+// host: the two-focal recoverPose tests (mp_pt67.h), whose models are not the oracle's
+// to the bit anyway (the 7pt roots differ in the last bits: ocml cbrt / acos / cos).
+// smallest_right_sv4 above stays exact: it is dlt_null4's fallback, bit-identical to
+// the oracle's.  Every argument is positive and finite here (al be > 0 where ga != 0;
+// 1 + zeta^2, 1 + t^2 >= 1), and the sign symmetry recover_pose_good_pair relies on
+// holds (the reciprocal is odd, the inverse square root sees even quantities only).
+MP_HD double svd_rcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
+MP_HD double svd_rsq(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = y * fma(-h * y, y, 1.5);
+    return y * fma(-h * y, y, 1.5);
+#else
+    return 1.0 / sqrt(x);
+#endif
+}
+MP_HD void smallest_right_sv4_fast(const double (&A0)[4][4], double *v) {
+#pragma clang fp contract(off)
+    double A[4][4], V[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            A[i][j] = A0[i][j];
+            V[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    for (int sweep = 0; sweep < 20; ++sweep) {
+        double off = 0.0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int q = p + 1; q < 4; ++q) {
+                double al = 0, be = 0, ga = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    al += A[i][p] * A[i][p];
+                    be += A[i][q] * A[i][q];
+                    ga += A[i][p] * A[i][q];
+                }
+                const double rel = (ga != 0.0) ? fabs(ga) * svd_rsq(al * be) : 0.0;
+                off = fmax(off, rel);
+                if (rel > 1e-16) {
+                    const double zeta = (be - al) * svd_rcp(2.0 * ga);
+                    const double u = 1.0 + zeta * zeta;
+                    const double t = (zeta >= 0 ? 1.0 : -1.0) * svd_rcp(fabs(zeta) + u * svd_rsq(u));
+                    const double c = svd_rsq(1.0 + t * t), s = c * t;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const double ap = A[i][p], aq = A[i][q];
+                        A[i][p] = c * ap - s * aq;
+                        A[i][q] = s * ap + c * aq;
+                        const double vp = V[i][p], vq = V[i][q];
+                        V[i][p] = c * vp - s * vq;
+                        V[i][q] = s * vp + c * vq;
+                    }
+                }
+            }
+        if (!(off > 1e-15)) break;
+    }
+    double nrm[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) nrm[j] = A[0][j] * A[0][j] + A[1][j] * A[1][j] + A[2][j] * A[2][j] + A[3][j] * A[3][j];
+    int k = 0;
+    double best = nrm[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+        if (nrm[j] < best) {
+            best = nrm[j];
+            k = j;
+        }
+    double w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = (k == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = w[0] * V[i][0] + w[1] * V[i][1] + w[2] * V[i][2] + w[3] * V[i][3];
+}
+
 // The same vector for the DLT triangulation of the depth fits (the chosen pose: A of
 // rank 3 up to noise) without the Jacobi sweeps -- round 6: without FMA contraction,
 // the oracle's dlt_null4 (oracle/src/pt.cpp) to the bit, fallback included: Householder QR of A (A^T A = R^T R,

@@ -373,9 +373,10 @@ MP_HD bool recover_pose_good(const RecoverCands &rc, int k, const double *p0, co
     }
     // one-sided Jacobi SVD (OpenCV's cv::SVD): for the wrong candidates the two
     // smallest singular values are often close, where inverse iteration (dlt_null4)
-    // converges slowly and the cheirality signs rest on the exact SVD vector
+    // converges slowly and the cheirality signs rest on the SVD vector (the sweeps'
+    // quotients and roots to about an ulp: smallest_right_sv4_fast)
     double Qh[4];
-    smallest_right_sv4(A, Qh);
+    smallest_right_sv4_fast(A, Qh);
     bool ok = Qh[2] * Qh[3] > 0;
     const double X0 = Qh[0] / Qh[3], X1 = Qh[1] / Qh[3], X2 = Qh[2] / Qh[3];
     ok = ok && X2 < dist;
@@ -414,7 +415,7 @@ MP_HD void recover_pose_good_pair(const RecoverCands &rc, int kr, const double *
         A[3][j] = p1[1] * P1[2][j] - P1[1][j];
     }
     double Qh[4];
-    smallest_right_sv4(A, Qh);
+    smallest_right_sv4_fast(A, Qh);
 #pragma unroll
     for (int sgn = 0; sgn < 2; ++sgn) {
         const double q3 = sgn ? -Qh[3] : Qh[3], t2 = sgn ? -P1[2][3] : P1[2][3];
