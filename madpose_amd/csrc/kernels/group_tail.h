@@ -269,7 +269,9 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
         }
         __syncthreads();
         if (!used) {
-            const double l = pick(a, pcol) / sh.U[g][kk][pcol];
+            // (the quotients by the pivot through its reciprocal: the shared-focal tail is
+            // held to the oracle by tolerance, not to the bit)
+            const double l = pick(a, pcol) * svd_rcp(sh.U[g][kk][pcol]);
 #pragma unroll
             for (int c = 0; c < 10; ++c)
                 if (!(cols >> c & 1u) && c != pcol) a[c] -= l * sh.U[g][kk][c];
@@ -290,7 +292,7 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
             double s = 0.0;
             for (int q = kk + 1; q < 9; ++q) s += sh.U[g][kk][sh.pc[g][q]] * sh.z[g][sh.pc[g][q]];
             s += sh.U[g][kk][fc] * sh.z[g][fc];
-            sh.z[g][sh.pc[g][kk]] = -s / sh.U[g][kk][sh.pc[g][kk]];
+            sh.z[g][sh.pc[g][kk]] = -s * svd_rcp(sh.U[g][kk][sh.pc[g][kk]]);
         }
     }
     __syncthreads();
@@ -351,14 +353,14 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
         no_pose();
         return;
     }
-    const double foc = 1.0 / sqrt(w);
+    const double foc = svd_rsq(w), ifoc = w * foc; // (1 / foc = sqrt(w))
     double Fm[9], nn = 0.0;
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
         Fm[e] = x * cd[e] + y * cd[9 + e] + cd[18 + e];
         nn += Fm[e] * Fm[e];
     }
-    nn = 1.0 / sqrt(nn);
+    nn = svd_rsq(nn);
     double E[9];
 #pragma unroll
     for (int p = 0; p < 3; ++p)
@@ -370,11 +372,11 @@ __global__ void __launch_bounds__(64) pt_tail6_group_kernel(PairData D, PairCons
     const bool has = r < K;
     const int i = s[has ? r : K - 1];
     const double pa[3] = {D.x0u[i], D.x0v[i], 1.0}, pb[3] = {D.x1u[i], D.x1v[i], 1.0};
-    const double ia = 1.0 / sqrt(dot3(pa, pa)), ib = 1.0 / sqrt(dot3(pb, pb));
+    const double ia = svd_rsq(dot3(pa, pa)), ib = svd_rsq(dot3(pb, pb));
     // the bearing's xy divided by the focal, re-normalised (sixpt_poses_for_root)
-    const double ba[3] = {pa[0] * ia / foc, pa[1] * ia / foc, pa[2] * ia},
-                 bb[3] = {pb[0] * ib / foc, pb[1] * ib / foc, pb[2] * ib};
-    const double na = 1.0 / sqrt(dot3(ba, ba)), nb = 1.0 / sqrt(dot3(bb, bb));
+    const double ba[3] = {pa[0] * ia * ifoc, pa[1] * ia * ifoc, pa[2] * ia},
+                 bb[3] = {pb[0] * ib * ifoc, pb[1] * ib * ifoc, pb[2] * ib};
+    const double na = svd_rsq(dot3(ba, ba)), nb = svd_rsq(dot3(bb, bb));
     const double c1[1][3] = {{ba[0] * na, ba[1] * na, ba[2] * na}}, c2[1][3] = {{bb[0] * nb, bb[1] * nb, bb[2] * nb}};
     const double p0[1][2] = {{pa[0], pa[1]}}, p1[1][2] = {{pb[0], pb[1]}};
     const double dd0[1] = {D.d0[i]}, dd1[1] = {D.d1[i]};
