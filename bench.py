@@ -735,7 +735,7 @@ def pin_rank(local_rank, local_world, per_ccd=True):
     # the LM pool: the calling thread plus up to 7 workers, leaving the estimator, the
     # sampler and the LO lanes their cores; spin only on a share of its own
     os.environ.setdefault("MADPOSE_LO_THREADS", str(max(1, min(8, len(share) - 4))))
-    os.environ.setdefault("MADPOSE_LO_SPIN", "300" if len(share) >= 12 else "0")
+    os.environ.setdefault("MADPOSE_LO_SPIN", "1000" if len(share) >= 12 else "0")  # (host/lm.cpp lo_spin_us)
     PIN_INFO.update({"cpus": len(share), "cpu_list": share, "gpu_local": bool(local), "pinned": True,
                      "l3_domains": len(set(cpu_l3(share).values())),
                      "lo_threads": int(os.environ["MADPOSE_LO_THREADS"])})

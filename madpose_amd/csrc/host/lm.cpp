@@ -111,10 +111,14 @@ constexpr size_t kPoolBlocks = 2048;
 // microseconds, and a futex wake-up per evaluation would cost about as much as the
 // evaluation's share per thread.  The spin is bounded by time, not by a pause count
 // (pause latency differs ~10x across x86 generations): MADPOSE_LO_SPIN = microseconds
-// (0 = block right away).  Default 300, or 0 when the process's CPU affinity share is
+// (0 = block right away).  Default 1000, or 0 when the process's CPU affinity share is
 // smaller than kSpinCpusPerRank per rank on this host (LOCAL_WORLD_SIZE): spinning
 // pays while the host has idle CPUs and costs when ranks oversubscribe one share
 // (two ranks on one 16-CPU share, 730 pairs/s spinning vs 840 blocking).
+// 1000 rather than round 5's 300: with 8 pairs in flight the pool's jobs from different
+// pairs come further apart than 300 us, and a worker that has gone to sleep costs a
+// wake-up -- ScanNet stand-in +3-6 % (7 of 8 same-box A/B pairs), tf -2.5 %, cal and sf
+// within noise (profiles/r06/spin); blocking at once (0) costs the stand-in 15-25 %.
 constexpr int kSpinCpusPerRank = 12; // about the threads one rank keeps busy (LO lanes, pool, sampler)
 }  // namespace
 
@@ -127,7 +131,7 @@ int lo_spin_us() {
         if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
         const char *l = std::getenv("LOCAL_WORLD_SIZE");
         const int ranks = std::max(1, l ? std::atoi(l) : 1);
-        return (cpus > 0 && cpus < kSpinCpusPerRank * ranks) ? 0 : 300;
+        return (cpus > 0 && cpus < kSpinCpusPerRank * ranks) ? 0 : 1000;
     }();
     return v;
 }
