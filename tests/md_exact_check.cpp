@@ -73,3 +73,17 @@ extern "C" int mdx_check_pose(int variant, const double *x, const double *y, con
     }
     return n;
 }
+
+// The DLT null vector of a 4x4 matrix by both one-sided Jacobi forms of mp_math.h: the
+// exact one (dlt_null4's fallback, the oracle's) and the one with the rotations'
+// quotients and square roots rewritten for refined hardware reciprocals
+// (smallest_right_sv4_fast, the two-focal recoverPose tests).  On the host both use
+// IEEE arithmetic, so this checks the rewrite's algebra (|ga| / sqrt(al be) as
+// |ga| rsq(al be), sqrt(1 + zeta^2) as u rsq(u)).
+extern "C" void sv4_check(const double *a, double *v_exact, double *v_fast) {
+    double A[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) A[i][j] = a[4 * i + j];
+    mp::smallest_right_sv4(A, v_exact);
+    mp::smallest_right_sv4_fast(A, v_fast);
+}

@@ -56,6 +56,7 @@ def mdx(tmp_path_factory):
         n = lib.mdx_check_pose(v, *[t.ctypes.data_as(_dp) for t in a], out.ctypes.data_as(_dp))
         return out[:17 * n].reshape(n, 17)
     solve.pose = pose
+    solve.so_path = so
     return solve
 
 
@@ -125,3 +126,24 @@ def test_estimator_diag_samples_bit_exact(mdx):
         x = np.c_[a0[idx], np.ones(4)]
         y = np.c_[a1[idx], np.ones(4)]
         _check(mdx, variant, x, y, np.asarray(p["depth0"], float)[idx], np.asarray(p["depth1"], float)[idx])
+
+
+def test_fast_sv4_matches_exact_form(mdx):
+    """smallest_right_sv4_fast (the two-focal recoverPose tests) against the exact
+    one-sided Jacobi (dlt_null4's fallback) on DLT-shaped and random 4x4 matrices, host
+    build: the same right singular vector up to sign, within 1e-10."""
+    lib = ctypes.CDLL(mdx.so_path)
+    rng = np.random.default_rng(5)
+    for t in range(400):
+        if t % 2:
+            A = rng.normal(size=(4, 4))
+        else:  # rank 3 + noise, as a DLT matrix of a consistent point
+            B = rng.normal(size=(4, 3))
+            A = B @ rng.normal(size=(3, 4)) + 1e-6 * rng.normal(size=(4, 4))
+        a = np.ascontiguousarray(A, dtype=np.float64)
+        ve, vf = np.zeros(4), np.zeros(4)
+        lib.sv4_check(a.ctypes.data_as(_dp), ve.ctypes.data_as(_dp), vf.ctypes.data_as(_dp))
+        s = 1.0 if np.dot(ve, vf) >= 0 else -1.0
+        assert np.allclose(ve, s * vf, atol=1e-10), (t, ve, vf)
+        sv = np.linalg.svd(A)[2][-1]
+        assert abs(abs(np.dot(sv, ve)) - 1.0) < 1e-8, (t, sv, ve)
