@@ -198,10 +198,11 @@ MP_HD void bougnoux_sq(const double *F, double *f0_sq, double *f1_sq) {
     null3(F, F + 3, F + 6, e1); // F e1 = 0
     const double c0[3] = {F[0], F[3], F[6]}, c1[3] = {F[1], F[4], F[7]}, c2[3] = {F[2], F[5], F[8]};
     null3(c0, c1, c2, e2); // e2^T F = 0
+    const double i1 = svd_rcp(e1[2]), i2 = svd_rcp(e2[2]);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        e1[k] /= e1[2];
-        e2[k] /= e2[2];
+        e1[k] *= i1;
+        e2[k] *= i2;
     }
     // row (-e2y, e2x, 0) F  and  row (-e1y, e1x, 0) F^T
     double L[3], M[3];
@@ -210,8 +211,8 @@ MP_HD void bougnoux_sq(const double *F, double *f0_sq, double *f1_sq) {
         L[c] = -e2[1] * F[c] + e2[0] * F[3 + c];
         M[c] = -e1[1] * F[3 * c] + e1[0] * F[3 * c + 1];
     }
-    *f0_sq = -(L[2] * F[8]) / (L[0] * F[6] + L[1] * F[7]);
-    *f1_sq = -(M[2] * F[8]) / (M[0] * F[2] + M[1] * F[5]);
+    *f0_sq = -(L[2] * F[8]) * svd_rcp(L[0] * F[6] + L[1] * F[7]);
+    *f1_sq = -(M[2] * F[8]) * svd_rcp(M[0] * F[2] + M[1] * F[5]);
 }
 
 // Cyclic Jacobi eigen-decomposition of a symmetric 3x3 matrix (A becomes diagonal,
@@ -234,10 +235,12 @@ MP_HD void jacobi_eig3(double (&A)[3][3], double (&V)[3][3]) {
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int q = p + 1; q < 3; ++q) {
-                if (A[p][q] == 0.0) continue;
-                const double th = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
-                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(1.0 + th * th));
-                const double c = 1.0 / sqrt(1.0 + t * t), s = t * c;
+                // rotations below 1e-150 of the diagonal are skipped so th*th stays finite
+                if (!(fabs(A[p][q]) > 1e-150 * (fabs(A[p][p]) + fabs(A[q][q])))) continue;
+                const double th = (A[q][q] - A[p][p]) * svd_rcp(2.0 * A[p][q]);
+                const double u = fma(th, th, 1.0);
+                const double t = (th >= 0 ? 1.0 : -1.0) * svd_rcp(fabs(th) + u * svd_rsq(u));
+                const double c = svd_rsq(fma(t, t, 1.0)), s = t * c;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     const double akp = A[k][p], akq = A[k][q];
