@@ -381,7 +381,8 @@ MP_HD bool recover_pose_good(const RecoverCands &rc, int k, const double *p0, co
     double Qh[4];
     smallest_right_sv4_fast(A, Qh);
     bool ok = Qh[2] * Qh[3] > 0;
-    const double X0 = Qh[0] / Qh[3], X1 = Qh[1] / Qh[3], X2 = Qh[2] / Qh[3];
+    const double iq = svd_rcp(Qh[3]);
+    const double X0 = Qh[0] * iq, X1 = Qh[1] * iq, X2 = Qh[2] * iq;
     ok = ok && X2 < dist;
     const double z1 = P1[2][0] * X0 + P1[2][1] * X1 + P1[2][2] * X2 + P1[2][3];
     return ok && z1 > 0 && z1 < dist;
@@ -419,11 +420,12 @@ MP_HD void recover_pose_good_pair(const RecoverCands &rc, int kr, const double *
     }
     double Qh[4];
     smallest_right_sv4_fast(A, Qh);
+    const double iq3 = svd_rcp(Qh[3]); // (odd: the two signs' quotients mirror exactly)
 #pragma unroll
     for (int sgn = 0; sgn < 2; ++sgn) {
-        const double q3 = sgn ? -Qh[3] : Qh[3], t2 = sgn ? -P1[2][3] : P1[2][3];
+        const double q3 = sgn ? -Qh[3] : Qh[3], t2 = sgn ? -P1[2][3] : P1[2][3], iq = sgn ? -iq3 : iq3;
         bool ok = Qh[2] * q3 > 0;
-        const double X0 = Qh[0] / q3, X1 = Qh[1] / q3, X2 = Qh[2] / q3;
+        const double X0 = Qh[0] * iq, X1 = Qh[1] * iq, X2 = Qh[2] * iq;
         ok = ok && X2 < dist;
         const double z1 = P1[2][0] * X0 + P1[2][1] * X1 + P1[2][2] * X2 + t2;
         ok = ok && z1 > 0 && z1 < dist;
