@@ -89,7 +89,7 @@ __device__ __forceinline__ bool e6g_gj_step(double (&g)[NC], int n, unsigned &ro
         piv = (c == pc) ? prow[c] : piv;
         mul = (c == pc) ? g[c] : mul;
     });
-    const double ip = 1.0 / piv;
+    const double ip = e6_rcp(piv);
     static_for<NC>([&](auto c) {
         const double nv = prow[c] * ip;
         g[c] = (r == pr) ? nv : fma(-mul, nv, g[c]);
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
             });
             double piv = 0.0;
             static_for<4>([&](auto c) { piv = (c == bc) ? prw[c] : piv; });
-            const double ip = best > 0.0 ? 1.0 / piv : 0.0;
+            const double ip = best > 0.0 ? e6_rcp(piv) : 0.0;
             static_for<4>([&](auto r) {
                 static_for<4>([&](auto c) {
                     const double nv = prw[c] * ip;
@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
         const double hA = zA - (i == k ? alpha : 0.0), hB = zB;
         const double vn = e6g_sum(fma(hB, hB, hA * hA));
         if (!(vn > 0.0)) return; // (uniform)
-        const double sc = 2.0 / vn;
+        const double sc = 2.0 * e6_rcp(vn);
         static_for<5>([&](auto j) {
             if constexpr (decltype(j)::value > k) {
                 const double d = sc * e6g_sum(fma(hB, ZB[j], hA * ZA[j]));
@@ -330,20 +330,24 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
                 });
                 const double r = gbcast<q>(rs);
                 if (c != 0.0 && r != 0.0) {
-                    double g = r / radix, f = 1.0;
+                    // (fi = 1 / f exactly -- f is a power of two -- so (c + r) * fi is the
+                    // quotient (c + r) / f to the bit, without a division)
+                    double g = r / radix, f = 1.0, fi = 1.0;
                     const double s = c + r;
                     while (c < g) {
                         f *= radix;
+                        fi *= 1.0 / radix;
                         c *= sqrdx;
                     }
                     g = r * radix;
                     while (c > g) {
                         f /= radix;
+                        fi *= radix;
                         c /= sqrdx;
                     }
-                    if ((c + r) / f < 0.95 * s) {
+                    if ((c + r) * fi < 0.95 * s) {
                         done = false;
-                        g = 1.0 / f;
+                        g = fi;
                         if (i == q) static_for<N>([&](auto j) { h[j] *= g; });
                         h[q] *= f;
                     }
@@ -370,9 +374,10 @@ __global__ void __launch_bounds__(64) pt_defl6_grp_kernel(double *pen, int nlist
             h[m] = t;
         }
         const double x = gbcast<m>(h[m - 1]);
+        const double ix = e6_rcp(x);
         double y = 0.0;
         if (i > m && i < N) {
-            y = h[m - 1] / x;
+            y = h[m - 1] * ix;
             h[m - 1] = y;
         }
         static_for<N>([&](auto j) {
