@@ -1263,11 +1263,13 @@ hipError_t launch_md_solve_staged(hipStream_t s, const PairData &D, const PairCo
 // the shared-focal root stage by the deflated eigenproblem: the pencil (16-lane groups,
 // eig6.h), its deflation + balance + Hessenberg form (16-lane groups, eig6_defl_grp.h),
 // then the lockstep Francis QR (one sample per lane, eig6.h / eig15_gen.h)
-// samples per wave of the lockstep QR: about one wave per SIMD (1024 on MI355X;
+// samples per wave of the lockstep QR: at most 768 waves, three quarters of the SIMDs,
+// since the shared-focal MD kernel holds SIMDs beside it (768 / 640 against 1024 and
+// 1536: sf gpu_solve 7.33 against 7.56 / 8.30 ms per pair, profiles/r06/eig_waves;
 // MADPOSE_EIG_WAVES overrides, MADPOSE_EIG_WAVES=16 packs 64 samples per wave at 1024)
 int eig_spw(int nlist) {
     static const int waves = [] {
-        return (int)env_int("MADPOSE_EIG_WAVES", 1024, 1, 1 << 20);
+        return (int)env_int("MADPOSE_EIG_WAVES", 768, 1, 1 << 20);
     }();
     return std::min(64, std::max(1, (nlist + waves - 1) / waves));
 }

@@ -33,7 +33,7 @@ pytestmark = pytest.mark.gpu
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "switch_worker.py")
 SETTINGS = {"early_alone": {"MADPOSE_EARLY_CONT": "1"}, "early_always": {"MADPOSE_EARLY_CONT": "2"},
             "mdx_one_lane": {"MADPOSE_MDX_R": "1"}, "mdx_two_lanes": {"MADPOSE_MDX_R": "2"}, "sampler_scalar": {"MADPOSE_SAMPLER_SIMD": "0"},
-            "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"},
+            "eig_packed": {"MADPOSE_EIG_WAVES": "16"}, "eig_waves_1024": {"MADPOSE_EIG_WAVES": "1024"}, "draw_by_draw": {"MADPOSE_SAMPLER_TWO_PASS": "0"},
             "solve_unfused": {"MADPOSE_SOLVE_FUSE": "0"}, "early_big": {"MADPOSE_EARLY_CONT": "3"}, "lo_late_hook": {"MADPOSE_LO_EARLY_HOOK": "0"},
             "lo_no_speculation": {"MADPOSE_LO_SPECULATE": "0"}, "lo_no_chain": {"MADPOSE_LO_CHAIN": "0"},
             "lo_chain_launched": {"MADPOSE_LO_CHAIN_LAUNCH": "1"},
